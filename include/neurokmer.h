@@ -1,0 +1,151 @@
+/*
+ * neurokmer.h — C ABI of the MI355X-native NeuroKmer k-mer -> spike hot path.
+ *
+ * Drop-in boundary for the reference crate's `SpikingKmerCounter`
+ * (MrObadiahEJ/NeuroKmer, src/spiking_hash.rs).  Every entry point below names
+ * the reference item it replaces.  Plain C types only: pointers + sizes, no
+ * torch or HIP types.  Return convention: 0 = OK, negative = NK_E_* code; the
+ * message of the last failure on the calling thread is nk_last_error().  No
+ * C++ exception crosses this boundary.  One handle is used by one thread at a
+ * time (the reference's `&mut self`).
+ *
+ * Compute runs on one AMD Instinct MI355X (gfx950) per handle.  There is no CPU
+ * fallback: nk_new() fails with NK_E_NO_DEVICE when no gfx950 device is
+ * present.
+ */
+#ifndef NEUROKMER_H
+#define NEUROKMER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NK_ABI_VERSION 1
+
+/* error codes */
+#define NK_OK 0
+#define NK_E_INVALID (-1)     /* bad argument (k == 0, pool == 0 with k-mers, ...) */
+#define NK_E_NO_DEVICE (-2)   /* no usable gfx950 device / HIP runtime failure */
+#define NK_E_OOM (-3)         /* device or host allocation failed */
+#define NK_E_IO (-4)          /* file open/read failure */
+#define NK_E_PARSE (-5)       /* FASTA/FASTQ parse failure (empty file, bad first byte) */
+#define NK_E_UNSUPPORTED (-6) /* feature not available in this build / for these arguments */
+#define NK_E_DEVICE (-7)      /* kernel launch or device-side failure */
+
+typedef struct nk_counter nk_counter;
+
+/* k-mer key width.  NK_KMER_COMPAT reproduces the reference's release-build
+ * u64 semantics for every k (k > 32 keeps the last 32 forward bases and the
+ * reference's masked-shift reverse strand, src/models.rs:188,192-194,260-266).
+ * It is the only mode in ABI v1. */
+#define NK_KMER_COMPAT 0
+
+typedef struct nk_opts {
+  int32_t device;        /* HIP device ordinal (default 0) */
+  int32_t kmer_width;    /* NK_KMER_COMPAT */
+  uint32_t top_n;        /* neurons whose "unique k-mers colliding" are tracked
+                            by every process call (default 20 = src/main.rs:50) */
+  uint32_t reserved[13];
+} nk_opts;
+
+/* Fills *o with the defaults above. */
+void nk_opts_default(nk_opts *o);
+
+/* SpikingKmerCounter::new(k, threshold, leak, refractory, spike_cost,
+ * pool_size, use_canonical)  — src/spiking_hash.rs:40-77.
+ * opts may be NULL.  Returns NULL on failure (see nk_last_error()). */
+nk_counter *nk_new(size_t k, float threshold, float leak, uint32_t refractory,
+                   double spike_cost, size_t pool_size, int use_canonical,
+                   const nk_opts *opts);
+void nk_free(nk_counter *c);
+
+/* SpikingKmerCounter::process_parallel(&mut self, seqs: &[Vec<u8>])
+ * — src/spiking_hash.rs:84-201.  Host records: record i is
+ * bases[rec_offsets[i] .. rec_offsets[i+1]), rec_offsets has n_recs+1 entries,
+ * rec_offsets[0] == 0.  Borrowed for the duration of the call. */
+int nk_process_parallel(nk_counter *c, const uint8_t *bases,
+                        const uint64_t *rec_offsets, size_t n_recs);
+
+/* Same, with bases and rec_offsets already resident in device memory of the
+ * handle's device (16-byte aligned `d_bases`).  `stream` is a hipStream_t or
+ * NULL for the handle's own stream.  n_bases == rec_offsets[n_recs]. */
+int nk_process_parallel_device(nk_counter *c, const uint8_t *d_bases,
+                               const uint64_t *d_rec_offsets, size_t n_recs,
+                               size_t n_bases, void *stream);
+
+/* SpikingKmerCounter::process_file_streaming(&mut self, path)
+ * — src/spiking_hash.rs:277-486 (FASTA/FASTQ, format from the first byte). */
+int nk_process_file_streaming(nk_counter *c, const char *path);
+
+/* Split-phase form of the two calls above, for multi-GPU use (one process per
+ * GPU; the caller all-reduces the u64 currents between the phases):
+ *   nk_accumulate_device   — zero + accumulate this shard's currents
+ *   <caller: allreduce(nk_device_currents(c), pool_size u64, sum)>
+ *   nk_finalize            — LIF + top-N (+ uniques of this shard's k-mers)
+ * `streaming_semantics` = 1 applies process_file_streaming's LIF rule (zero
+ * current neurons also step, src/spiking_hash.rs:544-659), 0 process_parallel's
+ * (they are skipped, :189-191). */
+int nk_accumulate_device(nk_counter *c, const uint8_t *d_bases,
+                         const uint64_t *d_rec_offsets, size_t n_recs,
+                         size_t n_bases, void *stream);
+int nk_finalize(nk_counter *c, int streaming_semantics, void *stream);
+/* After nk_finalize on a shard: the distinct k-mer keys of this shard that map
+ * to the current top-N neurons (device buffer owned by the handle, valid until
+ * the next call).  The caller gathers every shard's list and hands the union
+ * to nk_merge_top_kmers(), which recomputes the uniques column exactly. */
+int nk_top_kmers(nk_counter *c, const uint64_t **d_keys, size_t *n_keys);
+int nk_merge_top_kmers(nk_counter *c, const uint64_t *d_keys, size_t n_keys, void *stream);
+
+/* SpikingKmerCounter::top_abundant_neurons(&self, n) — src/spiking_hash.rs:661-673.
+ * Writes min(n, pool_size) rows into out (caller-allocated), returns the count
+ * written, or a negative error.  Rows are ordered by spikes descending, ties
+ * by ascending neuron index (the reference's stable sort).  `uniques` is the
+ * number of distinct k-mers of the last process call mapped to that neuron;
+ * it is exact for rows < opts.top_n and NK_E_UNSUPPORTED is returned for
+ * n > opts.top_n. */
+typedef struct nk_top_row {
+  uint64_t idx;
+  uint64_t spikes;
+  uint32_t uniques;
+  uint32_t _pad;
+} nk_top_row;
+long nk_top_abundant_neurons(nk_counter *c, size_t n, nk_top_row *out);
+
+/* SpikingKmerCounter::get_count(&self, kmer) — src/spiking_hash.rs:675-682.
+ * ABI v1: NK_E_UNSUPPORTED (the exact k-mer table is not built on device yet). */
+int nk_get_count(nk_counter *c, uint64_t kmer, uint32_t *out, int *present);
+
+/* EnergyTracker / accessors — src/models.rs:145-173, src/spiking_hash.rs:684-695 */
+uint64_t nk_total_spikes(const nk_counter *c);        /* energy.total_spikes() */
+double nk_energy_used(const nk_counter *c);           /* energy_used() */
+void nk_set_steps(nk_counter *c, uint64_t steps);     /* set_steps */
+uint64_t nk_get_steps(const nk_counter *c);           /* get_steps */
+size_t nk_pool_size(const nk_counter *c);
+size_t nk_k(const nk_counter *c);
+int nk_use_canonical(const nk_counter *c);
+
+/* Parity views (device -> host copies of per-neuron state; n = pool_size). */
+int nk_copy_currents(nk_counter *c, uint64_t *out, size_t n);
+int nk_copy_spike_counts(nk_counter *c, uint64_t *out, size_t n);
+int nk_copy_voltages(nk_counter *c, float *out, size_t n);
+int nk_copy_refractory(nk_counter *c, uint32_t *out, size_t n);
+/* Device pointer of the u64 currents vector (pool_size entries). */
+uint64_t *nk_device_currents(nk_counter *c);
+/* Resets neurons, currents and energy to the state nk_new() left them in. */
+int nk_reset(nk_counter *c);
+
+/* Per-stage device timings of the last process/finalize call, milliseconds
+ * (hipEvents on the stream the kernels ran on).  Returns the number of stages
+ * written (<= cap); names are static strings. */
+int nk_last_timings(const nk_counter *c, const char **names, float *ms, int cap);
+
+const char *nk_last_error(void);
+const char *nk_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NEUROKMER_H */

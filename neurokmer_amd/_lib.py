@@ -1,0 +1,125 @@
+"""Loader for the in-tree HIP library (neurokmer_amd/lib/libneurokmer.so).
+
+There is no CPU fallback: if the library is missing, or no gfx950 device is
+present, every entry point raises.  The library is loaded from the package
+directory (never from site-packages) so a GPU run visibly uses the in-tree
+native code.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libneurokmer.so")
+CLI_PATH = os.path.join(_HERE, "bin", "neurokmer")
+
+NK_OK = 0
+NK_E_INVALID = -1
+NK_E_NO_DEVICE = -2
+NK_E_OOM = -3
+NK_E_IO = -4
+NK_E_PARSE = -5
+NK_E_UNSUPPORTED = -6
+NK_E_DEVICE = -7
+
+# every symbol include/neurokmer.h declares
+EXPORTS = (
+    "nk_opts_default", "nk_new", "nk_free", "nk_process_parallel", "nk_process_parallel_device",
+    "nk_process_file_streaming", "nk_accumulate_device", "nk_finalize", "nk_top_kmers",
+    "nk_merge_top_kmers", "nk_top_abundant_neurons", "nk_get_count", "nk_total_spikes",
+    "nk_energy_used", "nk_set_steps", "nk_get_steps", "nk_pool_size", "nk_k",
+    "nk_use_canonical", "nk_copy_currents", "nk_copy_spike_counts", "nk_copy_voltages",
+    "nk_copy_refractory", "nk_device_currents", "nk_reset", "nk_last_timings", "nk_last_error",
+    "nk_version",
+)
+
+
+class NkOpts(C.Structure):
+    _fields_ = [("device", C.c_int32), ("kmer_width", C.c_int32), ("top_n", C.c_uint32),
+                ("reserved", C.c_uint32 * 13)]
+
+
+class NkTopRow(C.Structure):
+    _fields_ = [("idx", C.c_uint64), ("spikes", C.c_uint64), ("uniques", C.c_uint32),
+                ("_pad", C.c_uint32)]
+
+
+class NeuroKmerError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def _share_torch_runtime() -> None:
+    # torch ships its own libamdhip64 (same SONAME as /opt/rocm's).  Loading
+    # torch first makes this library bind to that one runtime, so device
+    # pointers and streams are shared with torch in one process.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
+def load(share_torch: bool = True):
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NeuroKmerError(NK_E_NO_DEVICE,
+                             f"HIP library not built: {LIB_PATH} missing "
+                             "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
+    if share_torch:
+        _share_torch_runtime()
+    L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+    vp, sz, u64, u32 = C.c_void_p, C.c_size_t, C.c_uint64, C.c_uint32
+    P = C.POINTER
+    sig = {
+        "nk_opts_default": (None, [P(NkOpts)]),
+        "nk_new": (vp, [sz, C.c_float, C.c_float, u32, C.c_double, sz, C.c_int, P(NkOpts)]),
+        "nk_free": (None, [vp]),
+        "nk_process_parallel": (C.c_int, [vp, vp, vp, sz]),
+        "nk_process_parallel_device": (C.c_int, [vp, vp, vp, sz, sz, vp]),
+        "nk_process_file_streaming": (C.c_int, [vp, C.c_char_p]),
+        "nk_accumulate_device": (C.c_int, [vp, vp, vp, sz, sz, vp]),
+        "nk_finalize": (C.c_int, [vp, C.c_int, vp]),
+        "nk_top_kmers": (C.c_int, [vp, P(vp), P(sz)]),
+        "nk_merge_top_kmers": (C.c_int, [vp, vp, sz, vp]),
+        "nk_top_abundant_neurons": (C.c_long, [vp, sz, P(NkTopRow)]),
+        "nk_get_count": (C.c_int, [vp, u64, P(u32), P(C.c_int)]),
+        "nk_total_spikes": (u64, [vp]),
+        "nk_energy_used": (C.c_double, [vp]),
+        "nk_set_steps": (None, [vp, u64]),
+        "nk_get_steps": (u64, [vp]),
+        "nk_pool_size": (sz, [vp]),
+        "nk_k": (sz, [vp]),
+        "nk_use_canonical": (C.c_int, [vp]),
+        "nk_copy_currents": (C.c_int, [vp, vp, sz]),
+        "nk_copy_spike_counts": (C.c_int, [vp, vp, sz]),
+        "nk_copy_voltages": (C.c_int, [vp, vp, sz]),
+        "nk_copy_refractory": (C.c_int, [vp, vp, sz]),
+        "nk_device_currents": (vp, [vp]),
+        "nk_reset": (C.c_int, [vp]),
+        "nk_last_timings": (C.c_int, [vp, P(C.c_char_p), P(C.c_float), C.c_int]),
+        "nk_last_error": (C.c_char_p, []),
+        "nk_version": (C.c_char_p, []),
+    }
+    for name, (rt, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = rt
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def last_error() -> str:
+    return load().nk_last_error().decode(errors="replace")
+
+
+def check(rc: int) -> int:
+    if rc < 0:
+        raise NeuroKmerError(rc, last_error())
+    return rc

@@ -1,0 +1,171 @@
+"""`SpikingKmerCounter` — Python mirror of the reference's public API, backed by
+the MI355X C ABI (include/neurokmer.h).  Same names, argument meaning and
+results as src/spiking_hash.rs; errors raise NeuroKmerError (the reference
+panics or returns Err).
+
+    c = SpikingKmerCounter(31, 1.0, 0.95, 2, 1.0, 2_000_000, True)
+    c.process_parallel(seqs)              # src/spiking_hash.rs:84
+    c.process_file_streaming(path)        # :277
+    c.top_abundant_neurons(20)            # :661  -> [(idx, spikes, uniques)]
+    c.energy.total_spikes(); c.energy_used()   # src/models.rs:166, :684
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import NkOpts, NkTopRow, check
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data if a.size else 0
+
+
+def records_to_arrays(seqs: Iterable[bytes]):
+    """list of record byte strings -> (bases uint8, offsets uint64[n+1])."""
+    seqs = [bytes(s) for s in seqs]
+    offs = np.zeros(len(seqs) + 1, np.uint64)
+    if seqs:
+        np.cumsum(np.fromiter((len(s) for s in seqs), np.uint64, len(seqs)), out=offs[1:])
+    bases = np.frombuffer(b"".join(seqs), np.uint8) if seqs else np.zeros(0, np.uint8)
+    return bases, offs
+
+
+class EnergyTracker:
+    """src/models.rs:145-173 view (spike totals live in the native handle)."""
+
+    def __init__(self, owner: "SpikingKmerCounter"):
+        self._o = owner
+
+    def total_spikes(self) -> int:
+        return int(self._o._L.nk_total_spikes(self._o._h))
+
+    def total_energy(self) -> float:
+        return float(self._o._L.nk_energy_used(self._o._h))
+
+
+class SpikingKmerCounter:
+    def __init__(self, k: int, threshold: float, leak: float, refractory: int,
+                 spike_cost: float, pool_size: int, use_canonical: bool, *,
+                 device: int = 0, top_n: int = 20):
+        self._L = _lib.load()
+        o = NkOpts()
+        self._L.nk_opts_default(C.byref(o))
+        o.device = device
+        o.top_n = top_n
+        self._h = None
+        h = self._L.nk_new(k, threshold, leak, refractory, spike_cost, pool_size,
+                           1 if use_canonical else 0, C.byref(o))
+        if not h:
+            raise _lib.NeuroKmerError(_lib.NK_E_NO_DEVICE, _lib.last_error())
+        self._h = h
+        self.k = k
+        self.pool_size = pool_size
+        self.use_canonical = bool(use_canonical)
+        self.top_n = top_n
+        self.energy = EnergyTracker(self)
+
+    def close(self):
+        if self._h:
+            self._L.nk_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- processing --------------------------------------------------------
+    def process_parallel(self, seqs: Sequence[bytes]) -> None:
+        """src/spiking_hash.rs:84-201 (records in host memory)."""
+        self.process_parallel_arrays(*records_to_arrays(seqs))
+
+    def process_parallel_arrays(self, bases: np.ndarray, offsets: np.ndarray) -> None:
+        bases = np.ascontiguousarray(bases, np.uint8)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        check(self._L.nk_process_parallel(self._h, _ptr(bases), _ptr(offsets), offsets.size - 1))
+
+    def process_parallel_device(self, d_bases: int, d_offsets: int, n_recs: int, n_bases: int,
+                                stream: int = 0) -> None:
+        """Input already in HBM (raw device pointers, e.g. torch tensor.data_ptr())."""
+        check(self._L.nk_process_parallel_device(self._h, d_bases, d_offsets, n_recs, n_bases,
+                                                 stream or None))
+
+    def process_file_streaming(self, path: str) -> None:
+        """src/spiking_hash.rs:277-486."""
+        check(self._L.nk_process_file_streaming(self._h, str(path).encode()))
+
+    # split phase (multi-GPU: allreduce currents between the two)
+    def accumulate_device(self, d_bases: int, d_offsets: int, n_recs: int, n_bases: int,
+                          stream: int = 0) -> None:
+        check(self._L.nk_accumulate_device(self._h, d_bases, d_offsets, n_recs, n_bases,
+                                           stream or None))
+
+    def finalize(self, streaming: bool = False, stream: int = 0) -> None:
+        check(self._L.nk_finalize(self._h, 1 if streaming else 0, stream or None))
+
+    def top_kmers_device(self):
+        """-> (device pointer, count) of this shard's distinct top-N k-mer keys."""
+        p = C.c_void_p()
+        n = C.c_size_t()
+        check(self._L.nk_top_kmers(self._h, C.byref(p), C.byref(n)))
+        return (p.value or 0), n.value
+
+    def merge_top_kmers(self, d_keys: int, n_keys: int, stream: int = 0) -> None:
+        check(self._L.nk_merge_top_kmers(self._h, d_keys, n_keys, stream or None))
+
+    def device_currents_ptr(self) -> int:
+        return self._L.nk_device_currents(self._h) or 0
+
+    def reset(self) -> None:
+        check(self._L.nk_reset(self._h))
+
+    # ---- results -----------------------------------------------------------
+    def top_abundant_neurons(self, n: int):
+        """src/spiking_hash.rs:661-673 -> [(neuron_idx, spikes, unique_kmers)]"""
+        rows = (NkTopRow * max(n, 1))()
+        m = check(self._L.nk_top_abundant_neurons(self._h, n, rows))
+        return [(int(rows[i].idx), int(rows[i].spikes), int(rows[i].uniques)) for i in range(m)]
+
+    def get_count(self, kmer: int) -> Optional[int]:
+        """src/spiking_hash.rs:675-682 (NK_E_UNSUPPORTED in ABI v1)."""
+        out = C.c_uint32()
+        present = C.c_int()
+        check(self._L.nk_get_count(self._h, kmer, C.byref(out), C.byref(present)))
+        return int(out.value) if present.value else None
+
+    def energy_used(self) -> float:
+        return float(self._L.nk_energy_used(self._h))
+
+    def set_steps(self, steps: int) -> None:
+        self._L.nk_set_steps(self._h, steps)
+
+    def get_steps(self) -> int:
+        return int(self._L.nk_get_steps(self._h))
+
+    def _copy(self, fn, dtype):
+        out = np.zeros(self.pool_size, dtype)
+        check(getattr(self._L, fn)(self._h, _ptr(out), out.size))
+        return out
+
+    def currents(self) -> np.ndarray:
+        return self._copy("nk_copy_currents", np.uint64)
+
+    def spike_counts(self) -> np.ndarray:
+        return self._copy("nk_copy_spike_counts", np.uint64)
+
+    def voltages(self) -> np.ndarray:
+        return self._copy("nk_copy_voltages", np.float32)
+
+    def refractory(self) -> np.ndarray:
+        return self._copy("nk_copy_refractory", np.uint32)
+
+    def last_timings(self) -> dict:
+        names = (C.c_char_p * 8)()
+        ms = (C.c_float * 8)()
+        n = self._L.nk_last_timings(self._h, names, ms, 8)
+        return {names[i].decode(): float(ms[i]) for i in range(n)}

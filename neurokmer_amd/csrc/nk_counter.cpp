@@ -1,0 +1,626 @@
+// nk_counter.cpp — host orchestrator behind the C ABI (include/neurokmer.h).
+//
+// Mirrors SpikingKmerCounter (src/spiking_hash.rs:16-715) with all per-neuron
+// state resident in HBM of one MI355X:
+//   currents u64[P] | voltage f32[P] | refractory u32[P] | spike_count u64[P]
+// and drives the gfx950 kernels of nk_kernels.hip on one HIP stream.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "neurokmer.h"
+#include "nk_fastx.h"
+#include "nk_kernels.h"
+
+using namespace nk;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                  \
+  do {                                                                                \
+    hipError_t e_ = (expr);                                                           \
+    if (e_ != hipSuccess)                                                             \
+      return fail(NK_E_DEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                  __FILE__, __LINE__);                                                \
+  } while (0)
+
+template <typename T>
+struct DevBuf {
+  T *p = nullptr;
+  size_t n = 0;
+  int ensure(size_t want) {
+    if (want <= n) return NK_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    if (hipMalloc((void **)&p, std::max<size_t>(want, 1) * sizeof(T)) != hipSuccess) {
+      p = nullptr;
+      return fail(NK_E_OOM, "hipMalloc of %zu bytes failed", want * sizeof(T));
+    }
+    n = want;
+    return NK_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+constexpr int kLifTable = 1 << 16;
+constexpr int kStages = 6;
+const char *kStageNames[kStages] = {"index", "count", "lif", "topn", "uniques", "total"};
+
+}  // namespace
+
+struct nk_counter {
+  size_t k = 0, pool = 0;
+  float thr = 1.0f, leak = 0.95f;
+  uint32_t refr = 2;
+  double cost = 1.0;
+  int canonical = 0;
+  uint64_t steps = 1000;
+  nk_opts opts{};
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+
+  // neuron state (HBM)
+  DevBuf<uint64_t> cur, sc;
+  DevBuf<float> v;
+  DevBuf<uint32_t> r;
+  // scratch
+  DevBuf<uint32_t> tile_rec, hist, tie_cnt, uniq, special;
+  DevBuf<uint64_t> stats;  // [0] new spikes, [1] max spike count
+  DevBuf<LifEntry> lif_tbl;
+  DevBuf<TopState> topst;
+  DevBuf<TopCand> cand;
+  DevBuf<uint64_t> top_cur;
+  DevBuf<unsigned long long> set_keys;
+  DevBuf<uint64_t> top_keys;
+  DevBuf<unsigned long long> top_keys_n;
+  DevBuf<uint32_t> radix_h;
+  uint64_t set_cap = 0;
+  size_t n_top_keys = 0;
+  // host copies of input (host-array entry points)
+  DevBuf<uint8_t> in_bases;
+  DevBuf<uint64_t> in_offs;
+  // LIF table cache key
+  bool lif_valid = false;
+  LifParams lif_key{};
+  // input of the last accumulate (for the uniques pass)
+  KmerInput last_in{};
+  bool have_input = false;
+  // energy (src/models.rs:145-173)
+  uint64_t total_spikes = 0, total_energy = 0;
+  // top rows of the last finalize
+  std::vector<nk_top_row> top;
+  std::vector<uint64_t> top_cur_h;
+  bool top_valid = false;
+  // timings
+  hipEvent_t ev[kStages + 1] = {};
+  float stage_ms[kStages] = {};
+  int n_stage = 0;
+};
+
+static uint64_t cost_fixed(double cost) {  // Rust `(cost * 1000.0) as u64`
+  double x = cost * 1000.0;
+  if (!(x > 0.0)) return 0;
+  if (x >= 18446744073709551616.0) return UINT64_MAX;
+  return (uint64_t)x;
+}
+
+static hipStream_t pick_stream(nk_counter *c, void *s) {
+  return s ? (hipStream_t)s : c->own_stream;
+}
+
+static int zero_state(nk_counter *c) {
+  if (!c->pool) return NK_OK;
+  HIPCHK(hipMemsetAsync(c->cur.p, 0, c->pool * 8, c->own_stream));
+  HIPCHK(hipMemsetAsync(c->sc.p, 0, c->pool * 8, c->own_stream));
+  HIPCHK(hipMemsetAsync(c->v.p, 0, c->pool * 4, c->own_stream));
+  HIPCHK(hipMemsetAsync(c->r.p, 0, c->pool * 4, c->own_stream));
+  HIPCHK(hipStreamSynchronize(c->own_stream));
+  c->total_spikes = c->total_energy = 0;
+  c->top_valid = false;
+  c->have_input = false;
+  return NK_OK;
+}
+
+template <typename T>
+static int copy_out(nk_counter *c, const DevBuf<T> &b, T *out, size_t n) {
+  if (!c || (!out && n)) return fail(NK_E_INVALID, "null argument");
+  if (n != c->pool) return fail(NK_E_INVALID, "n (%zu) must equal pool_size (%zu)", n, c->pool);
+  if (!n) return NK_OK;
+  (void)hipSetDevice(c->device);
+  HIPCHK(hipStreamSynchronize(c->own_stream));
+  HIPCHK(hipMemcpy(out, b.p, n * sizeof(T), hipMemcpyDeviceToHost));
+  return NK_OK;
+}
+
+extern "C" {
+
+void nk_opts_default(nk_opts *o) {
+  memset(o, 0, sizeof *o);
+  o->device = 0;
+  o->kmer_width = NK_KMER_COMPAT;
+  o->top_n = 20;
+}
+
+const char *nk_last_error(void) { return g_err.c_str(); }
+const char *nk_version(void) { return "neurokmer-mi355x 0.1.0 (abi 1, gfx950)"; }
+
+nk_counter *nk_new(size_t k, float threshold, float leak, uint32_t refractory, double spike_cost,
+                   size_t pool_size, int use_canonical, const nk_opts *opts) {
+  if (k == 0) {
+    fail(NK_E_INVALID, "k must be >= 1 (the reference panics on k == 0)");
+    return nullptr;
+  }
+  nk_opts o;
+  if (opts) o = *opts;
+  else nk_opts_default(&o);
+  if (o.kmer_width != NK_KMER_COMPAT) {
+    fail(NK_E_UNSUPPORTED, "kmer_width %d not supported in ABI v1", o.kmer_width);
+    return nullptr;
+  }
+  if (o.top_n > (uint32_t)kMaxTopN) {
+    fail(NK_E_INVALID, "top_n %u exceeds %d", o.top_n, kMaxTopN);
+    return nullptr;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    fail(NK_E_NO_DEVICE, "no HIP device available (this library has no CPU fallback)");
+    return nullptr;
+  }
+  if (o.device < 0 || o.device >= ndev) {
+    fail(NK_E_NO_DEVICE, "device %d out of range (%d devices)", o.device, ndev);
+    return nullptr;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, o.device) != hipSuccess ||
+      strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    fail(NK_E_NO_DEVICE, "device %d is %s, this build targets gfx950 only", o.device,
+         prop.gcnArchName);
+    return nullptr;
+  }
+  if (hipSetDevice(o.device) != hipSuccess) {
+    fail(NK_E_NO_DEVICE, "hipSetDevice(%d) failed", o.device);
+    return nullptr;
+  }
+  nk_counter *c = new nk_counter();
+  c->k = k;
+  c->pool = pool_size;
+  c->thr = threshold;
+  c->leak = leak;
+  c->refr = refractory;
+  c->cost = spike_cost;
+  c->canonical = use_canonical ? 1 : 0;
+  c->opts = o;
+  c->device = o.device;
+  bool ok = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) == hipSuccess;
+  for (int i = 0; ok && i <= kStages; ++i) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
+  size_t P = pool_size ? pool_size : 1;
+  ok = ok && !c->cur.ensure(P) && !c->sc.ensure(P) && !c->v.ensure(P) && !c->r.ensure(P) &&
+       !c->hist.ensure(kHistBins) && !c->stats.ensure(2) && !c->topst.ensure(1) &&
+       !c->cand.ensure(kMaxTopN) && !c->top_cur.ensure(kMaxTopN) &&
+       !c->uniq.ensure(kMaxTopN) && !c->special.ensure(kMaxTopN) &&
+       !c->top_keys_n.ensure(1) && !c->radix_h.ensure(256);
+  if (!ok || zero_state(c) != NK_OK) {
+    std::string e = g_err.empty() ? "device allocation failed" : g_err;
+    nk_free(c);
+    fail(NK_E_OOM, "%s", e.c_str());
+    return nullptr;
+  }
+  return c;
+}
+
+void nk_free(nk_counter *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
+  c->cur.release(); c->sc.release(); c->v.release(); c->r.release();
+  c->tile_rec.release(); c->hist.release(); c->tie_cnt.release(); c->uniq.release();
+  c->special.release(); c->stats.release(); c->lif_tbl.release(); c->topst.release();
+  c->cand.release(); c->top_cur.release(); c->set_keys.release(); c->top_keys.release();
+  c->top_keys_n.release(); c->radix_h.release(); c->in_bases.release(); c->in_offs.release();
+  for (int i = 0; i <= kStages; ++i)
+    if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete c;
+}
+
+int nk_reset(nk_counter *c) {
+  if (!c) return fail(NK_E_INVALID, "null counter");
+  (void)hipSetDevice(c->device);
+  return zero_state(c);
+}
+
+// ---------------------------------------------------------------------------
+// accumulate: currents = histogram of H(kmer) % pool over this input
+// ---------------------------------------------------------------------------
+int nk_accumulate_device(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_offs,
+                         size_t n_recs, size_t n_bases, void *stream) {
+  if (!c) return fail(NK_E_INVALID, "null counter");
+  if (n_bases && ((uintptr_t)d_bases & 15))
+    return fail(NK_E_INVALID, "device bases must be 16-byte aligned");
+  if (n_bases && !n_recs) return fail(NK_E_INVALID, "bases without records");
+  if (c->pool == 0 && n_bases >= c->k)
+    return fail(NK_E_INVALID, "pool_size 0 with k-mers present (the reference panics on % 0)");
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  KmerInput in{};
+  in.bases = d_bases;
+  in.offsets = d_offs;
+  in.n_recs = n_recs;
+  in.n_bases = n_bases;
+  in.n_tiles = n_tiles_for(n_bases);
+  int rc = c->tile_rec.ensure(std::max<uint64_t>(in.n_tiles, 1));
+  if (rc) return rc;
+  in.tile_rec = c->tile_rec.p;
+  HIPCHK(hipEventRecord(c->ev[0], s));
+  if (c->pool) HIPCHK(hipMemsetAsync(c->cur.p, 0, c->pool * 8, s));
+  HIPCHK(launch_tile_rec(in, c->tile_rec.p, s));
+  HIPCHK(hipEventRecord(c->ev[1], s));
+  HIPCHK(launch_count(in, (int)c->k, c->canonical, c->pool, c->cur.p, s));
+  HIPCHK(hipEventRecord(c->ev[2], s));
+  c->last_in = in;
+  c->have_input = true;
+  c->top_valid = false;
+  return NK_OK;
+}
+
+// ---------------------------------------------------------------------------
+// exact radix refine of the top-N threshold (spike counts >= 4095; rare)
+// ---------------------------------------------------------------------------
+static int refine_threshold(nk_counter *c, uint64_t want, uint64_t max_sc, TopState &st,
+                            hipStream_t s) {
+  int top_bit = 63;
+  while (top_bit > 0 && !((max_sc >> top_bit) & 1)) --top_bit;
+  int shift = (top_bit / 8) * 8;
+  uint64_t prefix = 0, above = 0;
+  for (;;) {
+    HIPCHK(hipMemsetAsync(c->radix_h.p, 0, 256 * 4, s));
+    HIPCHK(launch_radix_hist(c->sc.p, c->pool, shift, prefix, c->radix_h.p, s));
+    uint32_t h[256];
+    HIPCHK(hipMemcpyAsync(h, c->radix_h.p, sizeof h, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    int d = 255;
+    for (; d >= 0; --d) {
+      if (above + h[d] >= want) break;
+      above += h[d];
+    }
+    if (d < 0) d = 0;
+    prefix = (prefix << 8) | (uint64_t)d;
+    if (shift == 0) break;
+    shift -= 8;
+  }
+  st.T = prefix;
+  st.n_above = above;
+  st.need = want - above;
+  st.emit_above = 0;
+  st.refine = 0;
+  return NK_OK;
+}
+
+static int lif_and_top(nk_counter *c, int streaming, hipStream_t s) {
+  const uint64_t P = c->pool;
+  LifParams lp;
+  lp.steps = c->steps;
+  lp.thr = c->thr;
+  lp.leak = c->leak;
+  lp.refr = c->refr;
+  lp.skip_zero = streaming ? 0 : 1;
+  int rc;
+  // closed-form results for fresh neurons with count < 65536, cached per params
+  if (!c->lif_valid || c->lif_key.steps != lp.steps || c->lif_key.thr != lp.thr ||
+      c->lif_key.leak != lp.leak || c->lif_key.refr != lp.refr ||
+      memcmp(&c->lif_key.thr, &lp.thr, 4) || memcmp(&c->lif_key.leak, &lp.leak, 4)) {
+    if ((rc = c->lif_tbl.ensure(kLifTable))) return rc;
+    HIPCHK(launch_lif_table(c->lif_tbl.p, kLifTable, lp, s));
+    c->lif_key = lp;
+    c->lif_valid = true;
+  }
+  HIPCHK(hipMemsetAsync(c->hist.p, 0, kHistBins * 4, s));
+  HIPCHK(hipMemsetAsync(c->stats.p, 0, 16, s));
+  // streaming with steps == 0 returns before touching neurons (src/spiking_hash.rs:549-551)
+  LifParams run = lp;
+  HIPCHK(launch_lif_apply(c->cur.p, c->v.p, c->r.p, c->sc.p, P, run, c->lif_tbl.p, kLifTable,
+                          c->hist.p, c->stats.p, s));
+  HIPCHK(hipEventRecord(c->ev[3], s));
+  // top-N
+  const uint64_t want = std::min<uint64_t>(c->opts.top_n, P);
+  HIPCHK(launch_topn_threshold(c->hist.p, want, P, c->topst.p, s));
+  TopState st;
+  uint64_t stats[2];
+  HIPCHK(hipMemcpyAsync(&st, c->topst.p, sizeof st, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(stats, c->stats.p, sizeof stats, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  c->total_spikes += stats[0];
+  c->total_energy += stats[0] * cost_fixed(c->cost);
+  c->top.clear();
+  if (want) {
+    if (st.refine) {
+      if ((rc = refine_threshold(c, want, stats[1], st, s))) return rc;
+      HIPCHK(hipMemcpyAsync(c->topst.p, &st, sizeof st, hipMemcpyHostToDevice, s));
+    }
+    const unsigned nb = (unsigned)((P + 2047) / 2048);
+    if ((rc = c->tie_cnt.ensure(nb))) return rc;
+    HIPCHK(launch_topn_count(c->sc.p, P, c->topst.p, c->tie_cnt.p, s));
+    HIPCHK(launch_topn_emit(c->sc.p, P, c->topst.p, c->tie_cnt.p, c->cand.p, s));
+    HIPCHK(launch_topn_sort(c->cand.p, (uint32_t)want, c->cur.p, c->top_cur.p, s));
+    std::vector<TopCand> h(want);
+    c->top_cur_h.resize(want);
+    HIPCHK(hipMemcpyAsync(h.data(), c->cand.p, want * sizeof(TopCand), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(c->top_cur_h.data(), c->top_cur.p, want * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    c->top.resize(want);
+    for (uint64_t i = 0; i < want; ++i) {
+      c->top[i].idx = h[i].idx;
+      c->top[i].spikes = h[i].sc;
+      c->top[i].uniques = 0;
+      c->top[i]._pad = 0;
+    }
+  }
+  HIPCHK(hipEventRecord(c->ev[4], s));
+  return NK_OK;
+}
+
+static int uniques_pass(nk_counter *c, hipStream_t s) {
+  const uint32_t m = (uint32_t)c->top.size();
+  if (!m || !c->have_input || !c->last_in.n_tiles) {
+    HIPCHK(hipEventRecord(c->ev[5], s));
+    return NK_OK;
+  }
+  // upper bound of distinct keys in the top rows = sum of their currents
+  uint64_t sum = 0;
+  for (uint32_t i = 0; i < m; ++i) sum += c->top_cur_h[i];
+  uint64_t cap = 64;
+  while (cap < 2 * sum + 2) cap <<= 1;
+  int rc;
+  if ((rc = c->set_keys.ensure(cap))) return rc;
+  c->set_cap = cap;
+  HIPCHK(launch_set_fill(c->set_keys.p, cap, s));
+  HIPCHK(hipMemsetAsync(c->uniq.p, 0, m * 4, s));
+  HIPCHK(hipMemsetAsync(c->special.p, 0, m * 4, s));
+  UniqArgs u{};
+  u.top = c->cand.p;
+  u.n_top = m;
+  u.tbl_size = (uint32_t)top_tbl_size(m);
+  u.set_keys = c->set_keys.p;
+  u.set_mask = cap - 1;
+  u.uniq = c->uniq.p;
+  u.special = c->special.p;
+  HIPCHK(launch_uniques(c->last_in, (int)c->k, c->canonical, c->pool, u, s));
+  std::vector<uint32_t> un(m);
+  HIPCHK(hipMemcpyAsync(un.data(), c->uniq.p, m * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipEventRecord(c->ev[5], s));
+  HIPCHK(hipStreamSynchronize(s));
+  for (uint32_t i = 0; i < m; ++i) c->top[i].uniques = un[i];
+  c->n_top_keys = (size_t)-1;  // compacted lazily by nk_top_kmers
+  return NK_OK;
+}
+
+static void collect_timings(nk_counter *c, bool with_count) {
+  // ev[0] start | ev[1] after index | ev[2] after count | ev[3] after lif |
+  // ev[4] after topn | ev[5] after uniques | ev[6] finalize start
+  auto el = [](hipEvent_t a, hipEvent_t b) {
+    float ms = 0;
+    return hipEventElapsedTime(&ms, a, b) == hipSuccess ? ms : 0.0f;
+  };
+  c->stage_ms[0] = with_count ? el(c->ev[0], c->ev[1]) : 0.0f;
+  c->stage_ms[1] = with_count ? el(c->ev[1], c->ev[2]) : 0.0f;
+  c->stage_ms[2] = el(with_count ? c->ev[2] : c->ev[6], c->ev[3]);
+  c->stage_ms[3] = el(c->ev[3], c->ev[4]);
+  c->stage_ms[4] = el(c->ev[4], c->ev[5]);
+  c->stage_ms[5] = el(with_count ? c->ev[0] : c->ev[6], c->ev[5]);
+  c->n_stage = kStages;
+}
+
+int nk_finalize(nk_counter *c, int streaming, void *stream) {
+  if (!c) return fail(NK_E_INVALID, "null counter");
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  HIPCHK(hipEventRecord(c->ev[6], s));
+  int rc = lif_and_top(c, streaming, s);
+  if (rc) return rc;
+  rc = uniques_pass(c, s);
+  if (rc) return rc;
+  c->top_valid = true;
+  collect_timings(c, false);
+  return NK_OK;
+}
+
+static int process_device(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_offs,
+                          size_t n_recs, size_t n_bases, void *stream, int streaming) {
+  int rc = nk_accumulate_device(c, d_bases, d_offs, n_recs, n_bases, stream);
+  if (rc) return rc;
+  hipStream_t s = pick_stream(c, stream);
+  if ((rc = lif_and_top(c, streaming, s))) return rc;
+  if ((rc = uniques_pass(c, s))) return rc;
+  c->top_valid = true;
+  collect_timings(c, true);
+  return NK_OK;
+}
+
+int nk_process_parallel_device(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_offs,
+                               size_t n_recs, size_t n_bases, void *stream) {
+  return process_device(c, d_bases, d_offs, n_recs, n_bases, stream, 0);
+}
+
+static int check_offsets(const uint64_t *offs, size_t n_recs) {
+  if (!offs) return fail(NK_E_INVALID, "null offsets");
+  if (offs[0] != 0) return fail(NK_E_INVALID, "rec_offsets[0] must be 0");
+  for (size_t i = 0; i < n_recs; ++i)
+    if (offs[i + 1] < offs[i]) return fail(NK_E_INVALID, "rec_offsets not monotone at %zu", i);
+  return NK_OK;
+}
+
+static bool any_kmer(const uint64_t *offs, size_t n_recs, size_t k) {
+  for (size_t i = 0; i < n_recs; ++i)
+    if (offs[i + 1] - offs[i] >= k) return true;
+  return false;
+}
+
+static int process_host(nk_counter *c, const uint8_t *bases, const uint64_t *offs, size_t n_recs,
+                        int streaming) {
+  if (!c) return fail(NK_E_INVALID, "null counter");
+  int rc = check_offsets(offs, n_recs);
+  if (rc) return rc;
+  const size_t n_bases = (size_t)offs[n_recs];
+  if (c->pool == 0) {
+    if (any_kmer(offs, n_recs, c->k))
+      return fail(NK_E_INVALID, "pool_size 0 with k-mers present (the reference panics on % 0)");
+    // nothing to do: no neurons, no k-mers
+    c->top.clear();
+    c->top_valid = true;
+    return NK_OK;
+  }
+  (void)hipSetDevice(c->device);
+  hipStream_t s = c->own_stream;
+  if ((rc = c->in_bases.ensure(n_bases + 16))) return rc;
+  if ((rc = c->in_offs.ensure(n_recs + 1))) return rc;
+  if (n_bases) HIPCHK(hipMemcpyAsync(c->in_bases.p, bases, n_bases, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(c->in_offs.p, offs, (n_recs + 1) * 8, hipMemcpyHostToDevice, s));
+  return process_device(c, c->in_bases.p, c->in_offs.p, n_recs, n_bases, s, streaming);
+}
+
+int nk_process_parallel(nk_counter *c, const uint8_t *bases, const uint64_t *offs, size_t n_recs) {
+  return process_host(c, bases, offs, n_recs, 0);
+}
+
+int nk_process_file_streaming(nk_counter *c, const char *path) {
+  if (!c) return fail(NK_E_INVALID, "null counter");
+  std::vector<uint8_t> bases;
+  std::vector<uint64_t> offs;
+  std::string err;
+  int rc = read_fastx_all(path, bases, offs, err);
+  if (rc) return fail(rc, "%s", err.c_str());
+  return process_host(c, bases.data(), offs.data(), offs.size() - 1, 1);
+}
+
+int nk_top_kmers(nk_counter *c, const uint64_t **d_keys, size_t *n_keys) {
+  if (!c || !d_keys || !n_keys) return fail(NK_E_INVALID, "null argument");
+  (void)hipSetDevice(c->device);
+  hipStream_t s = c->own_stream;
+  const uint32_t m = (uint32_t)c->top.size();
+  if (!m || !c->set_cap) {
+    *d_keys = nullptr;
+    *n_keys = 0;
+    return NK_OK;
+  }
+  int rc;
+  if ((rc = c->top_keys.ensure(c->set_cap + 1))) return rc;
+  HIPCHK(hipMemsetAsync(c->top_keys_n.p, 0, 8, s));
+  HIPCHK(launch_set_compact(c->set_keys.p, c->set_cap, c->special.p, m, c->cand.p, c->pool,
+                            c->top_keys.p, c->top_keys_n.p, s));
+  unsigned long long n = 0;
+  HIPCHK(hipMemcpyAsync(&n, c->top_keys_n.p, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  *d_keys = c->top_keys.p;
+  *n_keys = (size_t)n;
+  return NK_OK;
+}
+
+int nk_merge_top_kmers(nk_counter *c, const uint64_t *d_keys, size_t n_keys, void *stream) {
+  if (!c) return fail(NK_E_INVALID, "null counter");
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  const uint32_t m = (uint32_t)c->top.size();
+  if (!m) return NK_OK;
+  uint64_t cap = 64;
+  while (cap < 2 * (uint64_t)n_keys + 2) cap <<= 1;
+  int rc;
+  if ((rc = c->set_keys.ensure(cap))) return rc;
+  c->set_cap = cap;
+  HIPCHK(launch_set_fill(c->set_keys.p, cap, s));
+  HIPCHK(hipMemsetAsync(c->uniq.p, 0, m * 4, s));
+  HIPCHK(hipMemsetAsync(c->special.p, 0, m * 4, s));
+  UniqArgs u{};
+  u.top = c->cand.p;
+  u.n_top = m;
+  u.tbl_size = (uint32_t)top_tbl_size(m);
+  u.set_keys = c->set_keys.p;
+  u.set_mask = cap - 1;
+  u.uniq = c->uniq.p;
+  u.special = c->special.p;
+  HIPCHK(launch_set_merge(d_keys, n_keys, c->pool, u, s));
+  std::vector<uint32_t> un(m);
+  HIPCHK(hipMemcpyAsync(un.data(), c->uniq.p, m * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  for (uint32_t i = 0; i < m; ++i) c->top[i].uniques = un[i];
+  return NK_OK;
+}
+
+long nk_top_abundant_neurons(nk_counter *c, size_t n, nk_top_row *out) {
+  if (!c) return fail(NK_E_INVALID, "null counter");
+  size_t m = std::min(n, c->pool);
+  if (m && !out) return fail(NK_E_INVALID, "null output");
+  if (!c->top_valid) {
+    // fresh (or reset) neurons: all spike counts 0 -> indices in order, no k-mers
+    if (n > c->opts.top_n)
+      return fail(NK_E_UNSUPPORTED, "uniques tracked for top_n=%u rows only", c->opts.top_n);
+    for (size_t i = 0; i < m; ++i) out[i] = nk_top_row{i, 0, 0, 0};
+    return (long)m;
+  }
+  if (n > c->opts.top_n && n > c->top.size())
+    return fail(NK_E_UNSUPPORTED, "uniques tracked for top_n=%u rows only (opts.top_n)",
+                c->opts.top_n);
+  m = std::min(m, c->top.size());
+  for (size_t i = 0; i < m; ++i) out[i] = c->top[i];
+  return (long)m;
+}
+
+int nk_get_count(nk_counter *c, uint64_t, uint32_t *, int *) {
+  (void)c;
+  return fail(NK_E_UNSUPPORTED, "get_count: exact k-mer table not built on device in ABI v1");
+}
+
+uint64_t nk_total_spikes(const nk_counter *c) { return c ? c->total_spikes : 0; }
+double nk_energy_used(const nk_counter *c) {
+  return c ? (double)c->total_energy / 1000.0 : 0.0;
+}
+void nk_set_steps(nk_counter *c, uint64_t steps) {
+  if (c) c->steps = steps;
+}
+uint64_t nk_get_steps(const nk_counter *c) { return c ? c->steps : 0; }
+size_t nk_pool_size(const nk_counter *c) { return c ? c->pool : 0; }
+size_t nk_k(const nk_counter *c) { return c ? c->k : 0; }
+int nk_use_canonical(const nk_counter *c) { return c ? c->canonical : 0; }
+uint64_t *nk_device_currents(nk_counter *c) { return c ? c->cur.p : nullptr; }
+
+int nk_copy_currents(nk_counter *c, uint64_t *out, size_t n) { return copy_out(c, c->cur, out, n); }
+int nk_copy_spike_counts(nk_counter *c, uint64_t *out, size_t n) {
+  return copy_out(c, c->sc, out, n);
+}
+int nk_copy_voltages(nk_counter *c, float *out, size_t n) { return copy_out(c, c->v, out, n); }
+int nk_copy_refractory(nk_counter *c, uint32_t *out, size_t n) {
+  return copy_out(c, c->r, out, n);
+}
+
+int nk_last_timings(const nk_counter *c, const char **names, float *ms, int cap) {
+  if (!c) return 0;
+  int n = std::min(cap, c->n_stage);
+  for (int i = 0; i < n; ++i) {
+    if (names) names[i] = kStageNames[i];
+    if (ms) ms[i] = c->stage_ms[i];
+  }
+  return n;
+}
+
+}  // extern "C"

@@ -1,0 +1,151 @@
+// nk_device.h — device-side building blocks shared by the NeuroKmer gfx950 kernels.
+//
+// Everything here is the MI355X restatement of the reference's per-k-mer math:
+//   * SipHash-1-3, key (0,0), over the 8 little-endian bytes of a u64 k-mer
+//     (siphasher 1.0.2 SipHasher13, src/spiking_hash.rs:78-82);
+//   * exact u64 `hash % pool` without a hardware 64-bit divide;
+//   * the LIF update `v = v*leak + c` with two f32 roundings, never fused
+//     (src/models.rs:34-51), solved in closed form per neuron.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace nk {
+
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int b) {
+  return (x << b) | (x >> (64 - b));
+}
+
+#define NK_SIPROUND                                                  \
+  do {                                                               \
+    v0 += v1; v1 = rotl64(v1, 13); v1 ^= v0; v0 = rotl64(v0, 32);    \
+    v2 += v3; v3 = rotl64(v3, 16); v3 ^= v2;                         \
+    v0 += v3; v3 = rotl64(v3, 21); v3 ^= v0;                         \
+    v2 += v1; v1 = rotl64(v1, 17); v1 ^= v2; v2 = rotl64(v2, 32);    \
+  } while (0)
+
+// SipHash-1-3 with key (0,0) of one u64 written as 8 LE bytes:
+// one compression round for the message block, one for the length block
+// (b = 8 << 56), three finalization rounds.  Constants of the first round
+// fold at compile time.
+__device__ __forceinline__ uint64_t sip13_u64(uint64_t m) {
+  uint64_t v0 = 0x736f6d6570736575ULL;
+  uint64_t v1 = 0x646f72616e646f6dULL;
+  uint64_t v2 = 0x6c7967656e657261ULL;
+  uint64_t v3 = 0x7465646279746573ULL ^ m;
+  NK_SIPROUND;
+  v0 ^= m;
+  const uint64_t b = 8ULL << 56;
+  v3 ^= b;
+  NK_SIPROUND;
+  v0 ^= b;
+  v2 ^= 0xffULL;
+  NK_SIPROUND;
+  NK_SIPROUND;
+  NK_SIPROUND;
+  return v0 ^ v1 ^ v2 ^ v3;
+}
+
+// Exact h % P for any P >= 1 given magic = floor((2^64-1)/P):
+// q = mulhi(h, magic) is floor(h/P) - {0,1,2}, so at most two corrections.
+struct FastMod {
+  uint64_t p;
+  uint64_t magic;
+};
+
+__device__ __forceinline__ uint64_t fastmod(uint64_t h, FastMod fm) {
+  uint64_t q = __umul64hi(h, fm.magic);
+  uint64_t r = h - q * fm.p;
+  if (r >= fm.p) r -= fm.p;
+  if (r >= fm.p) r -= fm.p;
+  return r;
+}
+
+// ---- LIF -------------------------------------------------------------------
+// One LifNeuron::update with input c (src/models.rs:34-51); f32 ops rounded
+// separately (__fmul_rn/__fadd_rn are never contracted into an FMA).
+__device__ __forceinline__ float lif_step(float v, float leak, float c) {
+  return __fadd_rn(__fmul_rn(v, leak), c);
+}
+
+// Exactly `steps` calls of LifNeuron::update starting from (v, r), with
+// c = (count as f64 / steps as f64) as f32.  The map v -> v*leak + c is a
+// function of v alone, so (a) a repeated value means every later step repeats
+// it, and (b) after a spike the state is always (0, refractory): the rest is
+// periodic with period refractory + m, m = steps from 0 to the next spike.
+// Returns the spikes fired; updates v and r in place.  Cost O(m + tail).
+__device__ __forceinline__ uint64_t lif_closed(float c, uint64_t steps, float thr, float leak,
+                                               uint32_t refr, float &v, uint32_t &r) {
+  uint64_t t = 0;
+  uint64_t spikes = 0;
+  // refractory drain
+  {
+    uint64_t d = (uint64_t)r < steps ? (uint64_t)r : steps;
+    r -= (uint32_t)d;
+    t += d;
+  }
+  // integrate from the current voltage
+  bool fired = false;
+  while (t < steps) {
+    ++t;
+    float nv = lif_step(v, leak, c);
+    if (nv >= thr) {
+      v = 0.0f;
+      r = refr;
+      spikes = 1;
+      fired = true;
+      break;
+    }
+    if (nv == v) {  // fixed point below threshold: nothing changes any more
+      v = nv;
+      t = steps;
+      break;
+    }
+    v = nv;
+  }
+  if (!fired || t == steps) return spikes;
+  uint64_t remaining = steps - t;  // state (0, refr)
+  if (remaining <= (uint64_t)refr) {
+    r = refr - (uint32_t)remaining;
+    return spikes;
+  }
+  // m: integrate steps from 0 to the next spike, within the steps available
+  uint64_t avail = remaining - refr;
+  float x = 0.0f;
+  uint64_t m = 0;
+  bool fires = false;
+  while (m < avail) {
+    ++m;
+    float nx = lif_step(x, leak, c);
+    if (nx >= thr) { fires = true; break; }
+    if (nx == x) { x = nx; break; }
+    x = nx;
+  }
+  if (!fires) {  // never reaches threshold again: refractory then settle at x
+    v = x;
+    r = 0;
+    return spikes;
+  }
+  uint64_t period = (uint64_t)refr + m;
+  uint64_t n = remaining / period;
+  spikes += n;
+  uint64_t rem = remaining - n * period;  // < period, starts in state (0, refr)
+  if (rem <= (uint64_t)refr) {
+    v = 0.0f;
+    r = refr - (uint32_t)rem;
+    return spikes;
+  }
+  r = 0;
+  float y = 0.0f;
+  for (uint64_t s = 0; s < rem - refr; ++s) y = lif_step(y, leak, c);  // < m steps: no spike
+  v = y;
+  return spikes;
+}
+
+__device__ __forceinline__ float lif_current(uint64_t count, uint64_t steps) {
+  // (total_current as f64 / steps as f64) as f32  — src/spiking_hash.rs:188,193,196
+  double tot = (double)count;
+  return (float)(tot / (double)steps);
+}
+
+}  // namespace nk

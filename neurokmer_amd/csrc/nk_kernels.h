@@ -1,0 +1,90 @@
+// nk_kernels.h — host-side launchers of the gfx950 kernels (internal; not ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace nk {
+
+constexpr int kTile = 4096;      // k-mer start positions per workgroup
+constexpr int kBlock = 256;      // threads per workgroup (4 waves)
+constexpr int kHistBins = 4096;  // spike-count histogram for top-N selection
+constexpr int kMaxTopN = 1024;
+
+struct LifParams {
+  uint64_t steps;
+  float thr;
+  float leak;
+  uint32_t refr;
+  int32_t skip_zero;
+};
+
+struct LifEntry {  // closed-form result for a fresh neuron (v = 0, r = 0)
+  uint64_t spikes;
+  float v;
+  uint32_t r;
+};
+
+struct TopState {
+  uint64_t T;          // spike count of the N-th row
+  uint64_t n_above;    // rows with spikes > T (all selected)
+  uint64_t need;       // rows with spikes == T to take, lowest index first
+  uint64_t emit_above; // device-side cursor
+  uint32_t refine;     // 1: T lies in the overflow bin, exact radix refine needed
+  uint32_t pad;
+};
+
+struct TopCand {
+  uint64_t idx;
+  uint64_t sc;
+};
+
+// input description shared by the k-mer kernels
+struct KmerInput {
+  const uint8_t *bases;
+  const uint64_t *offsets;
+  uint64_t n_recs;
+  uint64_t n_bases;
+  const uint32_t *tile_rec;  // first record of every tile
+  uint64_t n_tiles;
+};
+
+struct UniqArgs {
+  const TopCand *top;  // top-N rows (sorted)
+  uint32_t n_top;
+  uint32_t tbl_size;   // LDS probe table size (pow2 >= 2*n_top)
+  unsigned long long *set_keys;  // global hash set of k-mer keys
+  uint64_t set_mask;
+  uint32_t *uniq;      // per top row: distinct keys
+  uint32_t *special;   // per top row: key == ~0 seen
+};
+
+hipError_t launch_tile_rec(const KmerInput &in, uint32_t *tile_rec, hipStream_t s);
+hipError_t launch_count(const KmerInput &in, int k, int canonical, uint64_t pool,
+                        uint64_t *currents, hipStream_t s);
+hipError_t launch_uniques(const KmerInput &in, int k, int canonical, uint64_t pool,
+                          const UniqArgs &u, hipStream_t s);
+hipError_t launch_lif_table(LifEntry *tbl, int n, LifParams lp, hipStream_t s);
+hipError_t launch_lif_apply(const uint64_t *currents, float *v, uint32_t *r, uint64_t *sc,
+                            uint64_t pool, LifParams lp, const LifEntry *tbl, int tbl_n,
+                            uint32_t *hist, uint64_t *stats, hipStream_t s);
+hipError_t launch_topn_threshold(const uint32_t *hist, uint64_t n, uint64_t pool, TopState *st,
+                                 hipStream_t s);
+hipError_t launch_radix_hist(const uint64_t *sc, uint64_t pool, int shift, uint64_t prefix,
+                             uint32_t *hist256, hipStream_t s);
+hipError_t launch_topn_count(const uint64_t *sc, uint64_t pool, const TopState *st,
+                             uint32_t *tie_cnt, hipStream_t s);
+hipError_t launch_topn_emit(const uint64_t *sc, uint64_t pool, TopState *st,
+                            const uint32_t *tie_cnt, TopCand *cand, hipStream_t s);
+hipError_t launch_topn_sort(TopCand *cand, uint32_t m, const uint64_t *currents,
+                            uint64_t *top_cur, hipStream_t s);
+hipError_t launch_set_fill(unsigned long long *keys, uint64_t cap, hipStream_t s);
+hipError_t launch_set_compact(const unsigned long long *keys, uint64_t cap, const uint32_t *special,
+                              uint32_t n_top, const TopCand *top, uint64_t pool,
+                              uint64_t *out, unsigned long long *count, hipStream_t s);
+hipError_t launch_set_merge(const uint64_t *keys, uint64_t n, uint64_t pool, const UniqArgs &u,
+                            hipStream_t s);
+
+uint64_t top_tbl_size(uint32_t n_top);
+uint64_t n_tiles_for(uint64_t n_bases);
+
+}  // namespace nk

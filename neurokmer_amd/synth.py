@@ -1,0 +1,142 @@
+"""Deterministic synthetic sequence generator.
+
+i.i.d. uniform ACGT driven by splitmix64 in counter mode, seed 0x4E4B4D52
+("NKMR"), so the same stream can be produced on the host (here, numpy), by the
+C++ CLI tools, or by a device kernel for the 100 GB configs.  Base i of the
+stream is ``"ACGT"[(z[i >> 5] >> (2 * (i & 31))) & 3]`` with
+``z[j] = splitmix64_mix(seed + (j + 1) * 0x9E3779B97F4A7C15)``.
+
+Options that make parity fixtures non-trivial:
+  * planted repeats: ``repeats_per_mb`` copies of a ``motif_len``-bp motif in
+    every 1,000,000-base block (hot neurons, saturated spikes, top-N ties);
+  * ``n_rate``: fraction of bases replaced by runs of 'N' (and, with
+    ``mixed_case``, lowercase bases and a few other IUPAC bytes), which
+    exercise the reference's "anything else -> 0" rules (src/models.rs:231-251)
+    and pack_kmer's skip rule (src/utils.rs:26-39).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+SEED = 0x4E4B4D52
+GAMMA = np.uint64(0x9E3779B97F4A7C15)
+_ACGT = np.frombuffer(b"ACGT", dtype=np.uint8)
+
+
+def _mix(z: np.ndarray) -> np.ndarray:
+    z = z.astype(np.uint64, copy=True)
+    with np.errstate(over="ignore"):
+        z ^= z >> np.uint64(30)
+        z *= np.uint64(0xBF58476D1CE4E5B9)
+        z ^= z >> np.uint64(27)
+        z *= np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    return z
+
+
+def random_words(n_words: int, seed: int = SEED, start: int = 0) -> np.ndarray:
+    j = np.arange(start + 1, start + n_words + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        return _mix(np.uint64(seed & 0xFFFFFFFFFFFFFFFF) + j * GAMMA)
+
+
+def random_bases(n: int, seed: int = SEED, chunk: int = 1 << 24) -> np.ndarray:
+    """n bases of the splitmix64 stream as ASCII ACGT (uint8)."""
+    out = np.empty(n, dtype=np.uint8)
+    shifts = (np.arange(32, dtype=np.uint64) * np.uint64(2))
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        w0, w1 = s >> 5, (e + 31) >> 5
+        words = random_words(w1 - w0, seed, w0)
+        codes = ((words[:, None] >> shifts[None, :]) & np.uint64(3)).astype(np.uint8).ravel()
+        off = s - (w0 << 5)
+        out[s:e] = _ACGT[codes[off:off + (e - s)]]
+    return out
+
+
+def _plant_repeats(bases: np.ndarray, seed: int, per_mb: int, motif_len: int) -> None:
+    block = 1_000_000
+    motif = random_bases(motif_len, seed ^ 0xA5A5A5A5A5A5A5A5)
+    slot = block // per_mb
+    n_blocks = (bases.size + block - 1) // block
+    for b in range(n_blocks):
+        jit = random_words(per_mb, seed ^ 0x5EED0000 ^ b)
+        for j in range(per_mb):
+            # one copy per slot; when slot <= motif_len copies overlap (later wins)
+            room = slot - motif_len
+            pos = b * block + j * slot + (int(jit[j] % np.uint64(room)) if room > 0 else 0)
+            if pos >= bases.size:
+                break
+            end = min(pos + motif_len, bases.size)
+            bases[pos:end] = motif[:end - pos]
+
+
+def _sprinkle(bases: np.ndarray, seed: int, n_rate: float, mixed_case: bool) -> None:
+    n = bases.size
+    if n == 0:
+        return
+    w = random_words(max(1, n // 64 + 1), seed ^ 0x0DDBA115)
+    if n_rate > 0:
+        runs = max(1, int(n * n_rate / 8))
+        for t in range(runs):
+            z = int(w[t % w.size]) ^ (t * 0x9E3779B97F4A7C15 & 0xFFFFFFFFFFFFFFFF)
+            pos = z % n
+            ln = 1 + (z >> 40) % 15
+            bases[pos:pos + ln] = ord("N")
+    if mixed_case:
+        z = random_words(n // 16 + 1, seed ^ 0x1CA5E)
+        sel = np.repeat(z, 16)[:n]
+        lower = (sel & np.uint64(0xF)) == 0          # ~1/16 lowercase
+        bases[lower] = bases[lower] | 0x20
+        odd = (sel >> np.uint64(8) & np.uint64(0x3FF)) == 7  # ~1/1024 other bytes
+        others = np.frombuffer(b"RYKMSWBDHVn.-", dtype=np.uint8)
+        idx = (sel[odd] >> np.uint64(20)) % np.uint64(others.size)
+        bases[odd] = others[idx.astype(np.int64)]
+
+
+def make_records(total_bases: int, n_recs: int, seed: int = SEED, repeats_per_mb: int = 0,
+                 motif_len: int = 200, n_rate: float = 0.0, mixed_case: bool = False):
+    """-> (bases uint8[total], offsets uint64[n_recs+1]) : equal-length records,
+    the first (total % n_recs) records one base longer."""
+    bases = random_bases(total_bases, seed)
+    if repeats_per_mb:
+        _plant_repeats(bases, seed, repeats_per_mb, motif_len)
+    if n_rate > 0 or mixed_case:
+        _sprinkle(bases, seed, n_rate, mixed_case)
+    q, r = divmod(total_bases, n_recs)
+    lens = np.full(n_recs, q, dtype=np.uint64)
+    lens[:r] += 1
+    offsets = np.zeros(n_recs + 1, dtype=np.uint64)
+    np.cumsum(lens, out=offsets[1:])
+    return bases, offsets
+
+
+def make_reads(n_reads: int, read_len: int = 150, seed: int = SEED, **kw):
+    """FASTQ-style short reads: n_reads records of read_len bases."""
+    return make_records(n_reads * read_len, n_reads, seed, **kw)
+
+
+def write_fasta(path: str, bases: np.ndarray, offsets: np.ndarray, width: int = 60) -> None:
+    with open(path, "wb") as f:
+        for i in range(offsets.size - 1):
+            s, e = int(offsets[i]), int(offsets[i + 1])
+            f.write(b">s%d\n" % i)
+            seq = bases[s:e].tobytes()
+            for p in range(0, len(seq), width):
+                f.write(seq[p:p + width])
+                f.write(b"\n")
+
+
+def write_fastq(path: str, bases: np.ndarray, offsets: np.ndarray, qual: int = ord("I")) -> None:
+    with open(path, "wb") as f:
+        for i in range(offsets.size - 1):
+            s, e = int(offsets[i]), int(offsets[i + 1])
+            f.write(b"@r%d\n" % i)
+            f.write(bases[s:e].tobytes())
+            f.write(b"\n+\n")
+            f.write(bytes([qual]) * (e - s))
+            f.write(b"\n")
+
+
+def records_list(bases: np.ndarray, offsets: np.ndarray) -> list[bytes]:
+    return [bases[int(offsets[i]):int(offsets[i + 1])].tobytes() for i in range(offsets.size - 1)]

@@ -1,0 +1,202 @@
+"""ctypes binding of the C restatement (oracle/nk_oracle.c) -- TEST INFRASTRUCTURE ONLY.
+
+Importable only from tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg.  The product (neurokmer_amd) never loads this library.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libnk_oracle.so")
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = C.CDLL(_LIB_PATH)
+        u8p, u64p, f32p, u32p = (C.POINTER(C.c_uint8), C.POINTER(C.c_uint64),
+                                 C.POINTER(C.c_float), C.POINTER(C.c_uint32))
+        L.nko_siphash.restype = C.c_uint64
+        L.nko_siphash.argtypes = [C.c_int, C.c_int, C.c_uint64, C.c_uint64, u8p, C.c_size_t]
+        L.nko_sip13_u64.restype = C.c_uint64
+        L.nko_sip13_u64.argtypes = [C.c_uint64]
+        L.nko_map_kmer.restype = C.c_uint64
+        L.nko_map_kmer.argtypes = [C.c_uint64, C.c_uint64]
+        L.nko_pack_kmer.restype = C.c_uint64
+        L.nko_pack_kmer.argtypes = [u8p, C.c_size_t]
+        L.nko_kmer_keys.restype = C.c_size_t
+        L.nko_kmer_keys.argtypes = [u8p, C.c_size_t, C.c_size_t, C.c_int, u64p]
+        L.nko_lif.restype = None
+        L.nko_lif.argtypes = [C.c_uint64, C.c_uint64, C.c_float, C.c_float, C.c_uint32, C.c_int,
+                              f32p, u32p, u64p]
+        L.nko_new.restype = C.c_void_p
+        L.nko_new.argtypes = [C.c_size_t, C.c_float, C.c_float, C.c_uint32, C.c_double,
+                              C.c_size_t, C.c_int]
+        L.nko_free.argtypes = [C.c_void_p]
+        for fn in ("nko_process_parallel", "nko_process_streaming"):
+            f = getattr(L, fn)
+            f.restype = C.c_int
+            f.argtypes = [C.c_void_p, u8p, u64p, C.c_size_t, C.c_int]
+        L.nko_process_sequence.restype = C.c_int
+        L.nko_process_sequence.argtypes = [C.c_void_p, u8p, C.c_size_t]
+        for fn, rt in (("nko_currents", u64p), ("nko_voltages", f32p), ("nko_refractory", u32p),
+                       ("nko_spike_counts", u64p), ("nko_kmer_per_neuron", u32p)):
+            f = getattr(L, fn)
+            f.restype = rt
+            f.argtypes = [C.c_void_p]
+        for fn, rt in (("nko_total_spikes", C.c_uint64), ("nko_total_energy_fixed", C.c_uint64),
+                       ("nko_energy_used", C.c_double), ("nko_distinct_kmers", C.c_size_t),
+                       ("nko_get_steps", C.c_uint64)):
+            f = getattr(L, fn)
+            f.restype = rt
+            f.argtypes = [C.c_void_p]
+        L.nko_set_steps.argtypes = [C.c_void_p, C.c_uint64]
+        L.nko_top_abundant.restype = C.c_size_t
+        L.nko_top_abundant.argtypes = [C.c_void_p, C.c_size_t, u64p, u64p, u32p]
+        L.nko_get_count.restype = C.c_int
+        L.nko_get_count.argtypes = [C.c_void_p, C.c_uint64, u32p]
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray, ct):
+    return a.ctypes.data_as(C.POINTER(ct))
+
+
+def siphash(c, d, k0, k1, msg: bytes) -> int:
+    buf = np.frombuffer(msg, dtype=np.uint8) if msg else np.zeros(1, np.uint8)
+    return int(lib().nko_siphash(c, d, k0, k1, _ptr(buf, C.c_uint8), len(msg)))
+
+
+def sip13_u64(m: int) -> int:
+    return int(lib().nko_sip13_u64(m))
+
+
+def kmer_keys(seq: bytes, k: int, canonical: bool) -> np.ndarray:
+    n = max(0, len(seq) - k + 1)
+    out = np.zeros(max(n, 1), np.uint64)
+    buf = np.frombuffer(seq, dtype=np.uint8) if seq else np.zeros(1, np.uint8)
+    m = lib().nko_kmer_keys(_ptr(buf, C.c_uint8), len(seq), k, int(canonical),
+                            _ptr(out, C.c_uint64))
+    return out[:m]
+
+
+def lif(count, steps, thr, leak, refr, skip_zero, v=0.0, r=0, spikes=0):
+    cv, cr, cs = C.c_float(v), C.c_uint32(r), C.c_uint64(spikes)
+    lib().nko_lif(count, steps, thr, leak, refr, int(skip_zero), C.byref(cv), C.byref(cr),
+                  C.byref(cs))
+    return cv.value, cr.value, cs.value
+
+
+def records_to_arrays(seqs):
+    """list[bytes] -> (bases u8, offsets u64[n+1])."""
+    offs = np.zeros(len(seqs) + 1, np.uint64)
+    np.cumsum([len(s) for s in seqs], out=offs[1:]) if seqs else None
+    bases = np.frombuffer(b"".join(seqs), dtype=np.uint8) if seqs else np.zeros(0, np.uint8)
+    return bases, offs
+
+
+class OracleCounter:
+    """SpikingKmerCounter restated in C (see oracle/nk_oracle.h)."""
+
+    def __init__(self, k, threshold, leak, refractory, spike_cost, pool_size, use_canonical):
+        self._L = lib()
+        self.pool = pool_size
+        self._h = self._L.nko_new(k, threshold, leak, refractory, spike_cost, pool_size,
+                                  int(use_canonical))
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._L.nko_free(self._h)
+            self._h = None
+
+    def _run(self, fn, bases, offsets, n_threads):
+        bases = np.ascontiguousarray(bases, np.uint8)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        b = bases if bases.size else np.zeros(1, np.uint8)
+        rc = fn(self._h, _ptr(b, C.c_uint8), _ptr(offsets, C.c_uint64), offsets.size - 1,
+                n_threads)
+        if rc != 0:
+            raise RuntimeError("oracle rejected the input (k == 0 or pool == 0)")
+
+    def process_parallel_arrays(self, bases, offsets, n_threads=1):
+        self._run(self._L.nko_process_parallel, bases, offsets, n_threads)
+
+    def process_streaming_arrays(self, bases, offsets, n_threads=1):
+        self._run(self._L.nko_process_streaming, bases, offsets, n_threads)
+
+    def process_parallel(self, seqs, n_threads=1):
+        self.process_parallel_arrays(*records_to_arrays(seqs), n_threads)
+
+    def process_streaming(self, seqs, n_threads=1):
+        self.process_streaming_arrays(*records_to_arrays(seqs), n_threads)
+
+    def process_sequence(self, seq: bytes):
+        buf = np.frombuffer(seq, dtype=np.uint8) if seq else np.zeros(1, np.uint8)
+        if self._L.nko_process_sequence(self._h, _ptr(buf, C.c_uint8), len(seq)) != 0:
+            raise RuntimeError("oracle rejected the input")
+
+    def _arr(self, fn, dt):
+        p = getattr(self._L, fn)(self._h)
+        return np.ctypeslib.as_array(p, shape=(self.pool,)).astype(dt, copy=True) if self.pool \
+            else np.zeros(0, dt)
+
+    def currents(self):
+        return self._arr("nko_currents", np.uint64)
+
+    def voltages(self):
+        return self._arr("nko_voltages", np.float32)
+
+    def refractory(self):
+        return self._arr("nko_refractory", np.uint32)
+
+    def spike_counts(self):
+        return self._arr("nko_spike_counts", np.uint64)
+
+    def kmer_per_neuron(self):
+        return self._arr("nko_kmer_per_neuron", np.uint32)
+
+    @property
+    def total_spikes(self):
+        return int(self._L.nko_total_spikes(self._h))
+
+    @property
+    def total_energy_fixed(self):
+        return int(self._L.nko_total_energy_fixed(self._h))
+
+    def energy_used(self):
+        return float(self._L.nko_energy_used(self._h))
+
+    def distinct_kmers(self):
+        return int(self._L.nko_distinct_kmers(self._h))
+
+    def set_steps(self, s):
+        self._L.nko_set_steps(self._h, s)
+
+    def get_steps(self):
+        return int(self._L.nko_get_steps(self._h))
+
+    def top_abundant_neurons(self, n):
+        idx = np.zeros(max(n, 1), np.uint64)
+        sp = np.zeros(max(n, 1), np.uint64)
+        un = np.zeros(max(n, 1), np.uint32)
+        m = self._L.nko_top_abundant(self._h, n, _ptr(idx, C.c_uint64), _ptr(sp, C.c_uint64),
+                                     _ptr(un, C.c_uint32))
+        return [(int(idx[i]), int(sp[i]), int(un[i])) for i in range(m)]
+
+    def get_count(self, kmer):
+        out = C.c_uint32(0)
+        return int(out.value) if self._L.nko_get_count(self._h, kmer, C.byref(out)) else None

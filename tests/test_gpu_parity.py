@@ -1,0 +1,302 @@
+"""GPU parity: the HIP path (through the C ABI) vs the CPU restatement.
+
+Every comparison is bit-exact: u64 currents, u64 spike counts, f32 voltages
+(bitwise), u32 refractory ticks, total spikes, energy, top-N rows including
+"unique k-mers colliding".  Inputs are seeded synthetic records with N runs,
+lowercase bases, other IUPAC bytes, empty records and records shorter than k.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")  # import first: one shared HIP runtime
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+from neurokmer_amd import SpikingKmerCounter, synth  # noqa: E402
+from neurokmer_amd import _lib  # noqa: E402
+from oracle import cbind, pyref  # noqa: E402
+
+
+def ragged_records(total=60_000, seed=7, max_len=4000, **kw):
+    bases, _ = synth.make_records(total, 1, seed=seed, **kw)
+    rng = np.random.default_rng(seed)
+    lens = []
+    s = 0
+    while s < total:
+        L = int(rng.integers(0, max_len))
+        if rng.random() < 0.1:
+            L = int(rng.integers(0, 40))  # short (often < k) and empty records
+        L = min(L, total - s)
+        lens.append(L)
+        s += L
+    offs = np.zeros(len(lens) + 1, np.uint64)
+    np.cumsum(lens, out=offs[1:])
+    return bases, offs
+
+
+def assert_same(gpu, ref, n=20):
+    np.testing.assert_array_equal(gpu.currents(), ref.currents())
+    np.testing.assert_array_equal(gpu.spike_counts(), ref.spike_counts())
+    np.testing.assert_array_equal(gpu.voltages().view(np.uint32), ref.voltages().view(np.uint32))
+    np.testing.assert_array_equal(gpu.refractory(), ref.refractory())
+    assert gpu.energy.total_spikes() == ref.total_spikes
+    assert gpu.energy_used() == ref.energy_used()
+    assert gpu.top_abundant_neurons(n) == ref.top_abundant_neurons(n)
+
+
+def run_both(bases, offs, k, pool, canon, thr=1.0, leak=0.95, refr=2, cost=1.0, steps=None,
+             top_n=20, streaming=False):
+    g = SpikingKmerCounter(k, thr, leak, refr, cost, pool, canon, top_n=top_n)
+    r = cbind.OracleCounter(k, thr, leak, refr, cost, pool, canon)
+    if steps is not None:
+        g.set_steps(steps)
+        r.set_steps(steps)
+    if streaming:
+        # the streaming LIF rule on in-memory records goes through the split API
+        d_b = torch.from_numpy(np.concatenate([bases, np.zeros(16, np.uint8)])).cuda()
+        d_o = torch.from_numpy(offs.view(np.int64)).cuda()
+        torch.cuda.synchronize()
+        g.accumulate_device(d_b.data_ptr(), d_o.data_ptr(), offs.size - 1, int(offs[-1]))
+        g.finalize(streaming=True)
+        r.process_streaming_arrays(bases, offs)
+    else:
+        g.process_parallel_arrays(bases, offs)
+        r.process_parallel_arrays(bases, offs)
+    return g, r
+
+
+KS = (1, 2, 3, 5, 11, 15, 16, 17, 21, 31, 32, 33, 40, 63)
+
+
+@pytest.mark.parametrize("canon", [True, False])
+@pytest.mark.parametrize("k", KS)
+def test_parity_mixed_bytes(k, canon):
+    bases, offs = ragged_records(n_rate=0.01, mixed_case=True, seed=11 + k)
+    g, r = run_both(bases, offs, k, 5003, canon)
+    assert_same(g, r)
+
+
+@pytest.mark.parametrize("pool", [1, 2, 7, 64, 100_003, (1 << 20) + 7])
+def test_parity_pools(pool):
+    bases, offs = ragged_records(total=120_000, repeats_per_mb=3000, motif_len=150, seed=3)
+    g, r = run_both(bases, offs, 31, pool, True)
+    assert_same(g, r)
+
+
+def test_parity_planted_repeats_ties():
+    # hot neurons saturate (334 spikes) -> many ties in the top-N, broken by index
+    bases, offs = synth.make_records(400_000, 7, repeats_per_mb=20_000, motif_len=60, seed=5)
+    g, r = run_both(bases, offs, 21, 20_000, True, top_n=200)
+    assert_same(g, r, n=200)
+
+
+@pytest.mark.parametrize("steps", [0, 1, 7, 999, 5000, 20000])
+def test_parity_steps(steps):
+    # steps=20000 pushes spike counts past the 4095-bin histogram: exact radix refine
+    bases, offs = synth.make_records(200_000, 3, repeats_per_mb=5000, motif_len=80, seed=9)
+    g, r = run_both(bases, offs, 25, 3001, True, steps=steps)
+    assert_same(g, r)
+
+
+@pytest.mark.parametrize("thr,leak,refr,cost", [(0.5, 1.0, 0, 2.5), (0.0, 0.95, 2, 1.0),
+                                                  (1.0, 0.0, 5, 0.001), (3.0, 0.99, 1, 1.0),
+                                                  (1.0, 0.95, 1000, 1.0)])
+def test_parity_lif_params(thr, leak, refr, cost):
+    bases, offs = synth.make_records(150_000, 4, repeats_per_mb=4000, motif_len=90, seed=13)
+    g, r = run_both(bases, offs, 19, 1999, True, thr=thr, leak=leak, refr=refr, cost=cost)
+    assert_same(g, r)
+
+
+@pytest.mark.parametrize("canon", [True, False])
+def test_streaming_lif_rule(canon):
+    bases, offs = ragged_records(total=80_000, n_rate=0.002, seed=21)
+    g, r = run_both(bases, offs, 23, 40_000, canon, streaming=True, thr=0.0)
+    assert_same(g, r)
+
+
+def test_state_persists_across_calls():
+    b1, o1 = synth.make_records(100_000, 3, repeats_per_mb=6000, motif_len=70, seed=1)
+    b2, o2 = synth.make_records(90_000, 5, repeats_per_mb=9000, motif_len=50, seed=2)
+    g = SpikingKmerCounter(17, 1.0, 0.95, 2, 1.0, 777, True)
+    r = cbind.OracleCounter(17, 1.0, 0.95, 2, 1.0, 777, True)
+    for b, o in ((b1, o1), (b2, o2), (b1, o1)):
+        g.process_parallel_arrays(b, o)
+        r.process_parallel_arrays(b, o)
+        assert_same(g, r)
+    g.reset()
+    assert g.energy.total_spikes() == 0
+    assert g.top_abundant_neurons(5) == [(i, 0, 0) for i in range(5)]
+
+
+def test_python_restatement_agrees():
+    # tiny case through the pure-Python restatement as a second, independent oracle
+    bases, offs = ragged_records(total=6000, n_rate=0.01, mixed_case=True, seed=99, max_len=900)
+    seqs = synth.records_list(bases, offs)
+    for k, canon in ((21, False), (31, True), (33, True)):
+        g = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, 211, canon)
+        g.process_parallel(seqs)
+        p = pyref.SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, 211, canon)
+        p.process_parallel(seqs)
+        assert list(g.currents()) == p.currents
+        assert list(g.spike_counts()) == p.sc
+        assert g.top_abundant_neurons(20) == p.top_abundant_neurons(20)
+
+
+def test_device_entry_point_and_alignment():
+    bases, offs = synth.make_records(300_000, 7, repeats_per_mb=500, seed=17)
+    d_b = torch.from_numpy(bases).cuda()
+    d_o = torch.from_numpy(offs.view(np.int64)).cuda()
+    torch.cuda.synchronize()
+    g = SpikingKmerCounter(31, 1.0, 0.95, 2, 1.0, 50_000, True)
+    g.process_parallel_device(d_b.data_ptr(), d_o.data_ptr(), 7, bases.size)
+    r = cbind.OracleCounter(31, 1.0, 0.95, 2, 1.0, 50_000, True)
+    r.process_parallel_arrays(bases, offs)
+    assert_same(g, r)
+    with pytest.raises(_lib.NeuroKmerError):
+        g.process_parallel_device(d_b.data_ptr() + 1, d_o.data_ptr(), 7, bases.size - 1)
+
+
+def test_split_phase_two_shards_equals_whole():
+    """Multi-GPU protocol on one device: two shards accumulated separately,
+    currents summed (what RCCL all-reduce does), finalized on one counter,
+    then the shards' top k-mer keys merged -> identical to the whole input."""
+    bases, offs = synth.make_records(240_000, 8, repeats_per_mb=8000, motif_len=64, seed=23)
+    cut = 4  # shard = whole records
+    sh = []
+    for lo, hi in ((0, cut), (cut, 8)):
+        b = bases[int(offs[lo]):int(offs[hi])]
+        o = (offs[lo:hi + 1] - offs[lo]).astype(np.uint64)
+        sh.append((torch.from_numpy(np.concatenate([b, np.zeros(16, np.uint8)])).cuda(),
+                   torch.from_numpy(o.view(np.int64)).cuda(), hi - lo, b.size))
+    torch.cuda.synchronize()
+    a = SpikingKmerCounter(21, 1.0, 0.95, 2, 1.0, 9001, True)
+    b_ = SpikingKmerCounter(21, 1.0, 0.95, 2, 1.0, 9001, True)
+    a.accumulate_device(sh[0][0].data_ptr(), sh[0][1].data_ptr(), sh[0][2], sh[0][3])
+    b_.accumulate_device(sh[1][0].data_ptr(), sh[1][1].data_ptr(), sh[1][2], sh[1][3])
+    tot = a.currents() + b_.currents()
+    t = torch.from_numpy(tot.view(np.int64)).cuda()
+    for c in (a, b_):  # what the RCCL all-reduce leaves on every rank
+        cur = torch.as_tensor(_CAI(c.device_currents_ptr(), tot.size), device="cuda")
+        cur.copy_(t)
+        torch.cuda.synchronize()
+        c.finalize(False)
+    keys = []
+    for c in (a, b_):
+        p, n = c.top_kmers_device()
+        keys.append(torch.as_tensor(_CAI(p, n), device="cuda").clone() if n
+                    else torch.zeros(0, dtype=torch.int64, device="cuda"))
+    allk = torch.cat(keys)
+    a.merge_top_kmers(allk.data_ptr(), allk.numel())
+    r = cbind.OracleCounter(21, 1.0, 0.95, 2, 1.0, 9001, True)
+    r.process_parallel_arrays(bases, offs)
+    assert_same(a, r)
+
+
+class _CAI:
+    def __init__(self, ptr, n):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<i8", "data": (ptr, False),
+                                         "version": 3}
+
+
+def _fasta(tmp_path, bases, offs, name="in.fa"):
+    p = tmp_path / name
+    synth.write_fasta(str(p), bases, offs, width=60)
+    return str(p)
+
+
+def test_file_streaming_fasta(tmp_path):
+    bases, offs = ragged_records(total=70_000, n_rate=0.003, mixed_case=True, seed=31)
+    path = _fasta(tmp_path, bases, offs)
+    g = SpikingKmerCounter(27, 1.0, 0.95, 2, 1.0, 3333, True)
+    g.process_file_streaming(path)
+    r = cbind.OracleCounter(27, 1.0, 0.95, 2, 1.0, 3333, True)
+    r.process_streaming_arrays(bases, offs)
+    assert_same(g, r)
+
+
+def test_file_streaming_fastq(tmp_path):
+    bases, offs = synth.make_reads(2000, 150, seed=41, repeats_per_mb=20_000, motif_len=60)
+    p = tmp_path / "in.fq"
+    synth.write_fastq(str(p), bases, offs)
+    g = SpikingKmerCounter(31, 1.0, 0.95, 2, 1.0, 7919, True)
+    g.process_file_streaming(str(p))
+    r = cbind.OracleCounter(31, 1.0, 0.95, 2, 1.0, 7919, True)
+    r.process_streaming_arrays(bases, offs)
+    assert_same(g, r)
+
+
+@pytest.mark.parametrize("canon,streaming", [(True, False), (False, False), (True, True)])
+def test_cli_stdout_block(tmp_path, canon, streaming):
+    bases, offs = synth.make_records(50_000, 3, repeats_per_mb=20_000, motif_len=50, seed=51)
+    path = _fasta(tmp_path, bases, offs)
+    args = [_lib.CLI_PATH, "-i", path, "-k", "21", "--pool-size", "4001"]
+    if canon:
+        args.append("--canonical")
+    if streaming:
+        args.append("--streaming")
+    out = subprocess.run(args, capture_output=True, check=True, text=True).stdout
+    seqs = synth.records_list(bases, offs)
+    p = pyref.SpikingKmerCounter(21, 1.0, 0.95, 2, 1.0, 4001, canon)
+    (p.process_streaming if streaming else p.process_parallel)(seqs)
+    block = pyref.cli_result_block(p, 4001, streaming)
+    assert out.endswith(block), out[-2000:]
+    if not streaming:
+        assert f"  In-memory total current: {sum(p.currents)}\n" in out
+
+
+def test_errors_fail_loudly():
+    with pytest.raises(_lib.NeuroKmerError):
+        SpikingKmerCounter(0, 1.0, 0.95, 2, 1.0, 100, True)
+    g = SpikingKmerCounter(5, 1.0, 0.95, 2, 1.0, 0, True)
+    with pytest.raises(_lib.NeuroKmerError):
+        g.process_parallel([b"ACGTACGTAC"])
+    g.process_parallel([b"ACG"])  # no k-mers: the reference does not panic either
+    g2 = SpikingKmerCounter(5, 1.0, 0.95, 2, 1.0, 10, True)
+    with pytest.raises(_lib.NeuroKmerError):
+        g2.top_abundant_neurons(21)  # uniques tracked for top_n rows only
+    with pytest.raises(_lib.NeuroKmerError):
+        g2.get_count(0)
+
+
+@pytest.mark.parametrize("shape", ["config2"])
+def test_full_size_properties(shape):
+    """Config-2 size (115 Mbases, 7 records, k=31, pool=2M): size-independent
+    properties at full size + bit-exact parity on a prefix."""
+    bases, offs = synth.make_records(115_000_000, 7, repeats_per_mb=64, motif_len=200)
+    d_b = torch.from_numpy(bases).cuda()
+    d_o = torch.from_numpy(offs.view(np.int64)).cuda()
+    torch.cuda.synchronize()
+    g = SpikingKmerCounter(31, 1.0, 0.95, 2, 1.0, 2_000_000, True)
+    g.process_parallel_device(d_b.data_ptr(), d_o.data_ptr(), 7, bases.size)
+    cur1, sc1, top1 = g.currents(), g.spike_counts(), g.top_abundant_neurons(20)
+    nk = int(np.clip(np.diff(offs.astype(np.int64)) - 30, 0, None).sum())
+    assert int(cur1.sum()) == nk                      # every k-mer counted once
+    assert int(sc1.sum()) == g.energy.total_spikes()  # spikes conserved
+    g.reset()
+    g.process_parallel_device(d_b.data_ptr(), d_o.data_ptr(), 7, bases.size)
+    np.testing.assert_array_equal(g.currents(), cur1)  # deterministic
+    assert g.top_abundant_neurons(20) == top1
+    # linearity: per-record shards sum to the whole
+    acc = np.zeros_like(cur1)
+    h = SpikingKmerCounter(31, 1.0, 0.95, 2, 1.0, 2_000_000, True)
+    for i in range(7):
+        lo, hi = int(offs[i]), int(offs[i + 1])
+        o = np.array([0, hi - lo], np.uint64)
+        sub = torch.from_numpy(np.ascontiguousarray(bases[lo:hi])).cuda()
+        so = torch.from_numpy(o.view(np.int64)).cuda()
+        torch.cuda.synchronize()
+        h.accumulate_device(sub.data_ptr(), so.data_ptr(), 1, hi - lo)
+        acc += h.currents()
+    np.testing.assert_array_equal(acc, cur1)
+    # bit-exact vs the oracle on a 2 Mbase prefix of every record
+    per = 300_000
+    segs = [bases[int(offs[i]):int(offs[i]) + per] for i in range(7)]
+    po = np.arange(8, dtype=np.uint64) * per
+    pb = np.concatenate(segs)
+    gg, rr = run_both(pb, po, 31, 2_000_000, True)
+    assert_same(gg, rr)
