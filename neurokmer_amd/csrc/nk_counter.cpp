@@ -65,8 +65,8 @@ struct DevBuf {
 };
 
 constexpr int kLifTable = 1 << 16;
-constexpr int kStages = 6;
-const char *kStageNames[kStages] = {"index", "count", "lif", "topn", "uniques", "total"};
+constexpr int kStages = 7;
+const char *kStageNames[kStages] = {"index", "count", "hist", "lif", "topn", "uniques", "total"};
 
 }  // namespace
 
@@ -104,6 +104,14 @@ struct nk_counter {
   // LIF table cache key
   bool lif_valid = false;
   LifParams lif_key{};
+  // partitioned count (k <= 32, pool <= kMaxBuckets * 32768)
+  DevBuf<uint16_t> p_off, p_pos;
+  DevBuf<unsigned long long> p_fill;
+  DevBuf<uint2> p_desc;
+  DevBuf<uint32_t> p_over, partials, tbuckets;
+  PartArgs last_pa{};
+  bool part_used = false;
+  bool part_overflow_top = false;
   // input of the last accumulate (for the uniques pass)
   KmerInput last_in{};
   bool have_input = false;
@@ -114,7 +122,7 @@ struct nk_counter {
   std::vector<uint64_t> top_cur_h;
   bool top_valid = false;
   // timings
-  hipEvent_t ev[kStages + 1] = {};
+  hipEvent_t ev[kStages + 1] = {};  // see collect_timings
   float stage_ms[kStages] = {};
   int n_stage = 0;
 };
@@ -235,6 +243,8 @@ void nk_free(nk_counter *c) {
   (void)hipSetDevice(c->device);
   if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
   c->cur.release(); c->sc.release(); c->v.release(); c->r.release();
+  c->p_off.release(); c->p_pos.release(); c->p_fill.release(); c->p_desc.release();
+  c->p_over.release(); c->partials.release(); c->tbuckets.release();
   c->tile_rec.release(); c->hist.release(); c->tie_cnt.release(); c->uniq.release();
   c->special.release(); c->stats.release(); c->lif_tbl.release(); c->topst.release();
   c->cand.release(); c->top_cur.release(); c->set_keys.release(); c->top_keys.release();
@@ -269,16 +279,50 @@ int nk_accumulate_device(nk_counter *c, const uint8_t *d_bases, const uint64_t *
   in.offsets = d_offs;
   in.n_recs = n_recs;
   in.n_bases = n_bases;
-  in.n_tiles = n_tiles_for(n_bases);
+  const uint64_t B = (c->pool + kBinsPerBucket - 1) >> kBinBits;
+  const bool part = c->k <= 32 && c->pool > 0 && B <= (uint64_t)kMaxBuckets;
+  const uint64_t tile = part ? kPartTile : kTile;
+  in.n_tiles = n_tiles_for(n_bases, tile);
   int rc = c->tile_rec.ensure(std::max<uint64_t>(in.n_tiles, 1));
   if (rc) return rc;
   in.tile_rec = c->tile_rec.p;
   HIPCHK(hipEventRecord(c->ev[0], s));
   if (c->pool) HIPCHK(hipMemsetAsync(c->cur.p, 0, c->pool * 8, s));
-  HIPCHK(launch_tile_rec(in, c->tile_rec.p, s));
+  HIPCHK(launch_tile_rec(in, tile, c->tile_rec.p, s));
   HIPCHK(hipEventRecord(c->ev[1], s));
-  HIPCHK(launch_count(in, (int)c->k, c->canonical, c->pool, c->cur.p, s));
-  HIPCHK(hipEventRecord(c->ev[2], s));
+  c->part_used = part && in.n_tiles > 0;
+  if (c->part_used) {
+    // bucket regions: 1.25x the fair share + one tile of slack (overflow is
+    // still exact: the excess is counted with direct atomics)
+    uint64_t cap = n_bases / B * 5 / 4 + kPartTile;
+    cap = (cap + 63) & ~63ull;
+    const uint32_t slices = (uint32_t)std::max<uint64_t>(1, (256 + B - 1) / B);
+    if ((rc = c->p_off.ensure(B * cap)) || (rc = c->p_pos.ensure(B * cap)) ||
+        (rc = c->p_fill.ensure(B)) || (rc = c->p_desc.ensure(B * in.n_tiles)) ||
+        (rc = c->p_over.ensure(B)) || (rc = c->partials.ensure(slices * c->pool)))
+      return rc;
+    PartArgs pa{};
+    pa.n_buckets = (uint32_t)B;
+    pa.cap = cap;
+    pa.off = c->p_off.p;
+    pa.pos = c->p_pos.p;
+    pa.fill = c->p_fill.p;
+    pa.desc = c->p_desc.p;
+    pa.max_segs = in.n_tiles;
+    pa.overflow = c->p_over.p;
+    pa.currents = (unsigned long long *)c->cur.p;
+    HIPCHK(hipMemsetAsync(c->p_fill.p, 0, B * 8, s));
+    HIPCHK(hipMemsetAsync(c->p_over.p, 0, B * 4, s));
+    HIPCHK(launch_part(in, (int)c->k, c->canonical, c->pool, pa, s));
+    HIPCHK(hipEventRecord(c->ev[2], s));
+    HIPCHK(launch_bucket_hist(pa, c->pool, slices, c->partials.p, s));
+    HIPCHK(launch_partials_add(c->partials.p, slices, c->pool, c->cur.p, s));
+    c->last_pa = pa;
+  } else {
+    HIPCHK(launch_count(in, (int)c->k, c->canonical, c->pool, c->cur.p, s));
+    HIPCHK(hipEventRecord(c->ev[2], s));
+  }
+  HIPCHK(hipEventRecord(c->ev[3], s));
   c->last_in = in;
   c->have_input = true;
   c->top_valid = false;
@@ -342,7 +386,7 @@ static int lif_and_top(nk_counter *c, int streaming, hipStream_t s) {
   LifParams run = lp;
   HIPCHK(launch_lif_apply(c->cur.p, c->v.p, c->r.p, c->sc.p, P, run, c->lif_tbl.p, kLifTable,
                           c->hist.p, c->stats.p, s));
-  HIPCHK(hipEventRecord(c->ev[3], s));
+  HIPCHK(hipEventRecord(c->ev[4], s));
   // top-N
   const uint64_t want = std::min<uint64_t>(c->opts.top_n, P);
   HIPCHK(launch_topn_threshold(c->hist.p, want, P, c->topst.p, s));
@@ -368,7 +412,15 @@ static int lif_and_top(nk_counter *c, int streaming, hipStream_t s) {
     c->top_cur_h.resize(want);
     HIPCHK(hipMemcpyAsync(h.data(), c->cand.p, want * sizeof(TopCand), hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(c->top_cur_h.data(), c->top_cur.p, want * 8, hipMemcpyDeviceToHost, s));
+    std::vector<uint32_t> over;
+    if (c->part_used && c->have_input) {
+      over.resize(c->last_pa.n_buckets);
+      HIPCHK(hipMemcpyAsync(over.data(), c->p_over.p, over.size() * 4, hipMemcpyDeviceToHost, s));
+    }
     HIPCHK(hipStreamSynchronize(s));
+    c->part_overflow_top = false;
+    for (uint64_t i = 0; i < want && !over.empty(); ++i)
+      if (over[h[i].idx >> kBinBits]) c->part_overflow_top = true;
     c->top.resize(want);
     for (uint64_t i = 0; i < want; ++i) {
       c->top[i].idx = h[i].idx;
@@ -377,14 +429,14 @@ static int lif_and_top(nk_counter *c, int streaming, hipStream_t s) {
       c->top[i]._pad = 0;
     }
   }
-  HIPCHK(hipEventRecord(c->ev[4], s));
+  HIPCHK(hipEventRecord(c->ev[5], s));
   return NK_OK;
 }
 
 static int uniques_pass(nk_counter *c, hipStream_t s) {
   const uint32_t m = (uint32_t)c->top.size();
   if (!m || !c->have_input || !c->last_in.n_tiles) {
-    HIPCHK(hipEventRecord(c->ev[5], s));
+    HIPCHK(hipEventRecord(c->ev[6], s));
     return NK_OK;
   }
   // upper bound of distinct keys in the top rows = sum of their currents
@@ -406,29 +458,49 @@ static int uniques_pass(nk_counter *c, hipStream_t s) {
   u.set_mask = cap - 1;
   u.uniq = c->uniq.p;
   u.special = c->special.p;
-  HIPCHK(launch_uniques(c->last_in, (int)c->k, c->canonical, c->pool, u, s));
+  if (c->part_used && !c->part_overflow_top) {
+    // scan only the buckets that hold top neurons
+    std::vector<uint32_t> tb;
+    for (uint32_t i = 0; i < m; ++i) tb.push_back((uint32_t)(c->top[i].idx >> kBinBits));
+    std::sort(tb.begin(), tb.end());
+    tb.erase(std::unique(tb.begin(), tb.end()), tb.end());
+    if ((rc = c->tbuckets.ensure(tb.size()))) return rc;
+    HIPCHK(hipMemcpyAsync(c->tbuckets.p, tb.data(), tb.size() * 4, hipMemcpyHostToDevice, s));
+    const uint32_t slices = (uint32_t)std::max<size_t>(1, (512 + tb.size() - 1) / tb.size());
+    HIPCHK(launch_part_uniques(c->last_in, (int)c->k, c->canonical, c->last_pa, u, c->tbuckets.p,
+                               (uint32_t)tb.size(), slices, s));
+  } else {
+    // full rescan (k > 32, large pools, or a top bucket overflowed its region)
+    KmerInput in = c->last_in;
+    in.n_tiles = n_tiles_for(in.n_bases, kTile);
+    if ((rc = c->tile_rec.ensure(std::max<uint64_t>(in.n_tiles, 1)))) return rc;
+    in.tile_rec = c->tile_rec.p;
+    HIPCHK(launch_tile_rec(in, kTile, c->tile_rec.p, s));
+    HIPCHK(launch_uniques(in, (int)c->k, c->canonical, c->pool, u, s));
+  }
   std::vector<uint32_t> un(m);
   HIPCHK(hipMemcpyAsync(un.data(), c->uniq.p, m * 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipEventRecord(c->ev[5], s));
+  HIPCHK(hipEventRecord(c->ev[6], s));
   HIPCHK(hipStreamSynchronize(s));
   for (uint32_t i = 0; i < m; ++i) c->top[i].uniques = un[i];
-  c->n_top_keys = (size_t)-1;  // compacted lazily by nk_top_kmers
   return NK_OK;
 }
 
 static void collect_timings(nk_counter *c, bool with_count) {
-  // ev[0] start | ev[1] after index | ev[2] after count | ev[3] after lif |
-  // ev[4] after topn | ev[5] after uniques | ev[6] finalize start
+  // ev[0] start | ev[1] after index | ev[2] after K1 count (K1a) | ev[3] after
+  // K1b/K1c | ev[4] after lif | ev[5] after topn | ev[6] after uniques |
+  // ev[7] finalize start
   auto el = [](hipEvent_t a, hipEvent_t b) {
     float ms = 0;
     return hipEventElapsedTime(&ms, a, b) == hipSuccess ? ms : 0.0f;
   };
   c->stage_ms[0] = with_count ? el(c->ev[0], c->ev[1]) : 0.0f;
   c->stage_ms[1] = with_count ? el(c->ev[1], c->ev[2]) : 0.0f;
-  c->stage_ms[2] = el(with_count ? c->ev[2] : c->ev[6], c->ev[3]);
-  c->stage_ms[3] = el(c->ev[3], c->ev[4]);
+  c->stage_ms[2] = with_count ? el(c->ev[2], c->ev[3]) : 0.0f;
+  c->stage_ms[3] = el(with_count ? c->ev[3] : c->ev[7], c->ev[4]);
   c->stage_ms[4] = el(c->ev[4], c->ev[5]);
-  c->stage_ms[5] = el(with_count ? c->ev[0] : c->ev[6], c->ev[5]);
+  c->stage_ms[5] = el(c->ev[5], c->ev[6]);
+  c->stage_ms[6] = el(with_count ? c->ev[0] : c->ev[7], c->ev[6]);
   c->n_stage = kStages;
 }
 
@@ -436,7 +508,7 @@ int nk_finalize(nk_counter *c, int streaming, void *stream) {
   if (!c) return fail(NK_E_INVALID, "null counter");
   (void)hipSetDevice(c->device);
   hipStream_t s = pick_stream(c, stream);
-  HIPCHK(hipEventRecord(c->ev[6], s));
+  HIPCHK(hipEventRecord(c->ev[7], s));
   int rc = lif_and_top(c, streaming, s);
   if (rc) return rc;
   rc = uniques_pass(c, s);

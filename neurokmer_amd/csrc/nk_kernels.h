@@ -9,6 +9,13 @@ constexpr int kTile = 4096;      // k-mer start positions per workgroup
 constexpr int kBlock = 256;      // threads per workgroup (4 waves)
 constexpr int kHistBins = 4096;  // spike-count histogram for top-N selection
 constexpr int kMaxTopN = 1024;
+// partitioned count
+constexpr int kPartTile = 8192;       // positions per K1a workgroup
+constexpr int kPartBlock = 512;       // threads per K1a workgroup
+constexpr int kBinBits = 15;
+constexpr int kBinsPerBucket = 1 << kBinBits;  // 32768 u32 bins = 128 KiB LDS
+constexpr int kMaxBuckets = 256;      // pool <= 8,388,608 takes the partitioned path
+constexpr int kHistBlock = 1024;
 
 struct LifParams {
   uint64_t steps;
@@ -48,6 +55,18 @@ struct KmerInput {
   uint64_t n_tiles;
 };
 
+struct PartArgs {
+  uint32_t n_buckets;
+  uint64_t cap;                   // records per bucket region
+  uint16_t *off;                  // [bucket][cap] bin offset within the bucket
+  uint16_t *pos;                  // [bucket][cap] k-mer position within its tile
+  unsigned long long *fill;       // [bucket] records (low 40 bits) | segments << 40
+  uint2 *desc;                    // [bucket][max_segs] {tile, first record}
+  uint64_t max_segs;
+  uint32_t *overflow;             // [bucket] region overflowed (records counted directly)
+  unsigned long long *currents;   // overflow target
+};
+
 struct UniqArgs {
   const TopCand *top;  // top-N rows (sorted)
   uint32_t n_top;
@@ -58,7 +77,8 @@ struct UniqArgs {
   uint32_t *special;   // per top row: key == ~0 seen
 };
 
-hipError_t launch_tile_rec(const KmerInput &in, uint32_t *tile_rec, hipStream_t s);
+hipError_t launch_tile_rec(const KmerInput &in, uint64_t tile_size, uint32_t *tile_rec,
+                           hipStream_t s);
 hipError_t launch_count(const KmerInput &in, int k, int canonical, uint64_t pool,
                         uint64_t *currents, hipStream_t s);
 hipError_t launch_uniques(const KmerInput &in, int k, int canonical, uint64_t pool,
@@ -84,7 +104,17 @@ hipError_t launch_set_compact(const unsigned long long *keys, uint64_t cap, cons
 hipError_t launch_set_merge(const uint64_t *keys, uint64_t n, uint64_t pool, const UniqArgs &u,
                             hipStream_t s);
 
+hipError_t launch_part(const KmerInput &in, int k, int canonical, uint64_t pool,
+                       const PartArgs &pa, hipStream_t s);
+hipError_t launch_bucket_hist(const PartArgs &pa, uint64_t pool, uint32_t slices,
+                              uint32_t *partials, hipStream_t s);
+hipError_t launch_partials_add(const uint32_t *partials, uint32_t slices, uint64_t pool,
+                               uint64_t *currents, hipStream_t s);
+hipError_t launch_part_uniques(const KmerInput &in, int k, int canonical, const PartArgs &pa,
+                               const UniqArgs &u, const uint32_t *tbuckets, uint32_t n_tb,
+                               uint32_t slices, hipStream_t s);
+
 uint64_t top_tbl_size(uint32_t n_top);
-uint64_t n_tiles_for(uint64_t n_bases);
+uint64_t n_tiles_for(uint64_t n_bases, uint64_t tile);
 
 }  // namespace nk

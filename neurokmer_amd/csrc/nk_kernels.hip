@@ -20,47 +20,12 @@
 
 #include "nk_device.h"
 #include "nk_kernels.h"
+#include "nk_tile.h"
 
 namespace nk {
 
-constexpr int kHalo = 64;                       // bases staged past the tile
-constexpr int kStage = kTile + kHalo;           // 4160 bytes
-constexpr int kChunks = kStage / 16;            // 260 16-B chunks
 constexpr int kPerThread = kTile / kBlock;      // 16 positions per lane
 constexpr unsigned long long kEmpty = ~0ULL;
-
-// ---------------------------------------------------------------------------
-// byte -> 2-bit code conversion (4 bytes at a time).  A/a 0, C/c 1, G/g 2,
-// T/t 3, anything else 0 on BOTH strands (src/models.rs:231-251).
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t eq_bytes(uint32_t t, uint32_t c) {
-  uint32_t z = t ^ c;
-  return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u;  // 0x80 where byte == c
-}
-
-struct Conv4 {
-  uint32_t fnib;  // 4 forward codes, first base in bits 7:6
-  uint32_t rnib;  // 4 complement codes, first base in bits 1:0
-  uint32_t inv;   // 4 invalid-byte bits, first base in bit 0
-};
-
-__device__ __forceinline__ Conv4 conv4(uint32_t x) {
-  uint32_t t = x | 0x20202020u;
-  uint32_t valid = eq_bytes(t, 0x61616161u) | eq_bytes(t, 0x63636363u) |
-                   eq_bytes(t, 0x67676767u) | eq_bytes(t, 0x74747474u);
-  uint32_t vm = valid >> 7;  // 0x01 per valid byte
-  uint32_t vm3 = vm * 3u;
-  uint32_t code = ((x >> 1) ^ (x >> 2)) & 0x03030303u & vm3;
-  uint32_t comp = (code ^ 0x03030303u) & vm3;
-  Conv4 o;
-  o.fnib = ((code << 6) & 0xC0u) | ((code >> 4) & 0x30u) | ((code >> 14) & 0x0Cu) |
-           ((code >> 24) & 0x03u);
-  o.rnib = (comp & 0x03u) | ((comp >> 6) & 0x0Cu) | ((comp >> 12) & 0x30u) |
-           ((comp >> 18) & 0xC0u);
-  uint32_t m = ~vm & 0x01010101u;
-  o.inv = (m & 1u) | ((m >> 7) & 2u) | ((m >> 14) & 4u) | ((m >> 21) & 8u);
-  return o;
-}
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
@@ -68,29 +33,14 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
-__device__ __forceinline__ uint32_t code_of(uint8_t b) {
-  uint32_t t = b | 0x20u;
-  bool v = (t == 'a') | (t == 'c') | (t == 'g') | (t == 't');
-  return v ? (((uint32_t)b >> 1) ^ ((uint32_t)b >> 2)) & 3u : 0u;
-}
-__device__ __forceinline__ uint32_t comp_of(uint8_t b) {
-  uint32_t t = b | 0x20u;
-  bool v = (t == 'a') | (t == 'c') | (t == 'g') | (t == 't');
-  return v ? ((((uint32_t)b >> 1) ^ ((uint32_t)b >> 2)) & 3u) ^ 3u : 0u;
-}
-__device__ __forceinline__ bool valid_byte(uint8_t b) {
-  uint32_t t = b | 0x20u;
-  return (t == 'a') | (t == 'c') | (t == 'g') | (t == 't');
-}
-
 // ---------------------------------------------------------------------------
 // first record of each tile: largest r < n_recs with offsets[r] <= tile start
 // ---------------------------------------------------------------------------
 __global__ void k_tile_rec(const uint64_t *__restrict__ offsets, uint64_t n_recs,
-                           uint64_t n_tiles, uint32_t *__restrict__ tile_rec) {
+                           uint64_t n_tiles, uint64_t tile_size, uint32_t *__restrict__ tile_rec) {
   uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_tiles) return;
-  uint64_t pos = t * (uint64_t)kTile;
+  uint64_t pos = t * tile_size;
   uint64_t lo = 0, hi = n_recs;  // invariant: offsets[lo] <= pos, answer in [lo, hi)
   while (hi - lo > 1) {
     uint64_t mid = (lo + hi) >> 1;
@@ -154,105 +104,19 @@ template <bool CANON, int MODE>
 __global__ __launch_bounds__(kBlock) void k_kmers(KmerInput in, int k, FastMod fm,
                                                   unsigned long long *__restrict__ currents,
                                                   UniqArgs u) {
-  __shared__ uint32_t sF[kChunks + 2];
-  __shared__ uint32_t sR[kChunks + 2];
-  __shared__ uint16_t sINV[kChunks + 4];
-  __shared__ uint32_t sWIN[kTile / 32];
-  __shared__ uint4 sRAW[CANON ? 1 : kChunks];
+  __shared__ TileLds<kTile, !CANON> L;
   extern __shared__ uint64_t dyn[];  // MODE 1: probe table
-
-  const int tid = threadIdx.x;
-  const uint64_t T0 = (uint64_t)blockIdx.x * kTile;
-  const uint64_t n_bases = in.n_bases;
-
-  // 1. stage the tile: coalesced 16-B loads -> bit streams
-  for (int c = tid; c < kChunks; c += kBlock) {
-    uint64_t g = T0 + 16ull * c;
-    uint4 v;
-    if (g + 16 <= n_bases) {
-      v = *reinterpret_cast<const uint4 *>(in.bases + g);
-    } else {
-      uint32_t w[4] = {0, 0, 0, 0};
-      for (int j = 0; j < 16; ++j)
-        if (g + j < n_bases) w[j >> 2] |= (uint32_t)in.bases[g + j] << (8 * (j & 3));
-      v = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-    Conv4 a = conv4(v.x), b = conv4(v.y), cc = conv4(v.z), d = conv4(v.w);
-    sF[c] = (a.fnib << 24) | (b.fnib << 16) | (cc.fnib << 8) | d.fnib;
-    sR[c] = a.rnib | (b.rnib << 8) | (cc.rnib << 16) | (d.rnib << 24);
-    sINV[c] = (uint16_t)(a.inv | (b.inv << 4) | (cc.inv << 8) | (d.inv << 12));
-    if (!CANON) sRAW[c] = v;
-  }
-  if (tid < 2) { sF[kChunks + tid] = 0; sR[kChunks + tid] = 0; }
-  if (tid < 4) sINV[kChunks + tid] = 0;
-  for (int i = tid; i < kTile / 32; i += kBlock) sWIN[i] = 0;
-
   uint64_t *tbl_idx = dyn;
   uint32_t *tbl_slot = reinterpret_cast<uint32_t *>(dyn + (MODE == 1 ? u.tbl_size : 0));
   if (MODE == 1) build_top_tbl(u, tbl_idx, tbl_slot);  // contains __syncthreads
-  __syncthreads();
-
-  // 2. windows crossing a record boundary (or running past the end) are not k-mers
-  {
-    const uint64_t limit = T0 + kTile + (uint64_t)k - 1;
-    const uint64_t r0 = in.tile_rec[blockIdx.x];
-    for (uint64_t r = r0 + 1 + tid; r <= in.n_recs; r += kBlock) {
-      uint64_t b = in.offsets[r];
-      if (b >= limit) break;
-      uint64_t lo = (b + 1 > (uint64_t)k) ? b + 1 - (uint64_t)k : 0;
-      if (lo < T0) lo = T0;
-      uint64_t hi = b < T0 + kTile ? b : T0 + kTile;
-      for (uint64_t q = lo - T0; q < hi - T0;) {  // <= 2 words for k <= 32
-        uint32_t w = (uint32_t)(q >> 5), s = (uint32_t)(q & 31);
-        uint32_t nb = (uint32_t)((hi - T0) - q);
-        uint32_t take = nb < 32 - s ? nb : 32 - s;
-        uint32_t bits = (take == 32 ? 0xFFFFFFFFu : ((1u << take) - 1u)) << s;
-        atomicOr(&sWIN[w], bits);
-        q += take;
-      }
-    }
-  }
-  __syncthreads();
-
-  const int twok = 2 * k;
-  const uint64_t mask2k = (k >= 32) ? ~0ULL : ((1ULL << twok) - 1ULL);
-  const uint32_t kmask = (k >= 32) ? 0xFFFFFFFFu : ((1u << k) - 1u);
-
+  const uint64_t T0 = (uint64_t)blockIdx.x * kTile;
+  stage_tile<kTile, kBlock, !CANON>(L, in, blockIdx.x, k);
 #pragma unroll 4
   for (int j = 0; j < kPerThread; ++j) {
-    const int q = j * kBlock + tid;
-    const uint64_t p = T0 + (uint64_t)q;
-    if (p + (uint64_t)k > n_bases) break;
-    if ((sWIN[q >> 5] >> (q & 31)) & 1u) continue;
-    const int w = q >> 4;
-    const int s = 2 * (q & 15);
-    uint64_t hi64 = ((uint64_t)sF[w] << 32) | sF[w + 1];
-    uint64_t x = (hi64 << s) | (((uint64_t)sF[w + 2] << s) >> 32);
-    uint64_t fwd = x >> (64 - twok);
-    uint64_t key;
-    if (CANON) {
-      uint64_t lo64 = ((uint64_t)sR[w + 1] << 32) | sR[w];
-      uint64_t y = (lo64 >> s) | (((uint64_t)sR[w + 2] << 32) << (32 - s));
-      uint64_t rev = y & mask2k;
-      key = fwd < rev ? fwd : rev;
-    } else {
-      // pack_kmer skips non-ACGT bytes (src/utils.rs:26-39)
-      const int iw = q >> 4;  // 16 bits per sINV entry
-      const int is = q & 15;
-      uint64_t z = ((uint64_t)sINV[iw] | ((uint64_t)sINV[iw + 1] << 16) |
-                    ((uint64_t)sINV[iw + 2] << 32) | ((uint64_t)sINV[iw + 3] << 48)) >> is;
-      if ((uint32_t)z & kmask) {
-        const uint8_t *raw = reinterpret_cast<const uint8_t *>(sRAW);
-        uint64_t pk = 0;
-        for (int i = 0; i < k; ++i) {
-          uint8_t bb = raw[q + i];
-          if (valid_byte(bb)) pk = (pk << 2) | code_of(bb);
-        }
-        key = pk;
-      } else {
-        key = fwd;
-      }
-    }
+    const int q = j * kBlock + threadIdx.x;
+    if (T0 + (uint64_t)q + (uint64_t)k > in.n_bases) break;
+    if (!window_valid(L, T0, q, k, in.n_bases)) continue;
+    const uint64_t key = window_key<kTile, !CANON, CANON>(L, q, k);
     const uint64_t idx = fastmod(sip13_u64(key), fm);
     if (MODE == 0) {
       atomicAdd(&currents[idx], 1ULL);
@@ -321,6 +185,212 @@ __global__ __launch_bounds__(kBlock) void k_kmers_compat(KmerInput in, int k, Fa
       int slot = probe_top(tbl_idx, tbl_slot, u.tbl_size - 1, idx);
       if (slot >= 0) set_insert(u, (uint32_t)slot, key);
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K1 partitioned (k <= 32, pool <= 256 * 32768): the MI355X-native count.
+//
+// Random per-k-mer global atomics run at the memory side (~20 G/s chip-wide),
+// 10x below what the hash rate allows.  Instead:
+//   K1a k_part     hash every k-mer of an 8192-position tile, counting-sort the
+//                  tile's (bin offset u16, tile position u16) records by bucket
+//                  (bucket = neuron >> 15) in LDS, reserve room in each bucket's
+//                  HBM array with ONE atomic per (tile, bucket), and write the
+//                  segments out coalesced.
+//   K1b k_bucket_hist  one workgroup per (bucket, slice): 32768-bin u32
+//                  histogram in LDS over a contiguous slice of the bucket's
+//                  records, written once as a partial.
+//   K1c k_partials_add currents[i] += sum of the partials (u64).
+// The records are kept: the uniques pass reads only the top neurons' buckets
+// instead of re-hashing the input.
+// ---------------------------------------------------------------------------
+constexpr int kPartPerThread = kPartTile / kPartBlock;  // 16
+
+template <bool CANON>
+__global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMod fm, PartArgs pa) {
+  __shared__ TileLds<kPartTile, !CANON> L;
+  __shared__ uint32_t s_cnt[kMaxBuckets];
+  __shared__ uint32_t s_start[kMaxBuckets + 1];
+  __shared__ uint32_t s_base[kMaxBuckets];
+  __shared__ uint32_t s_fit[kMaxBuckets];
+  __shared__ uint32_t s_sorted[kPartTile];
+
+  const int tid = threadIdx.x;
+  const uint64_t tile = blockIdx.x;
+  const uint64_t T0 = tile * (uint64_t)kPartTile;
+  const uint32_t B = pa.n_buckets;
+  for (uint32_t b = tid; b < B; b += kPartBlock) s_cnt[b] = 0;
+  stage_tile<kPartTile, kPartBlock, !CANON>(L, in, tile, k);  // syncs
+
+  // phase 1: key -> neuron -> (bucket, rank within the tile's bucket)
+  uint32_t E[kPartPerThread];  // bit31 valid | bucket << 13 | rank
+  uint32_t O[kPartPerThread];  // bin offset within the bucket
+#pragma unroll
+  for (int j = 0; j < kPartPerThread; ++j) {
+    const int q = j * kPartBlock + tid;
+    E[j] = 0;
+    O[j] = 0;
+    if (window_valid(L, T0, q, k, in.n_bases)) {
+      const uint64_t key = window_key<kPartTile, !CANON, CANON>(L, q, k);
+      const uint32_t idx = (uint32_t)fastmod(sip13_u64(key), fm);
+      const uint32_t b = idx >> kBinBits;
+      const uint32_t rank = atomicAdd(&s_cnt[b], 1u);
+      E[j] = 0x80000000u | (b << 13) | rank;
+      O[j] = idx & (kBinsPerBucket - 1);
+    }
+  }
+  __syncthreads();
+  // exclusive scan of the bucket counts (one wave) + HBM reservation (one
+  // atomic per non-empty bucket: entries in the low 40 bits, segments above)
+  if (tid < 64) {
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < B; b0 += 64) {
+      uint32_t b = b0 + tid;
+      uint32_t c = b < B ? s_cnt[b] : 0;
+      uint32_t x = c;
+      for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(x, o, 64);
+        if (tid >= o) x += y;
+      }
+      if (b < B) s_start[b] = carry + x - c;
+      carry += __shfl(x, 63, 64);
+    }
+    if (tid == 0) s_start[B] = carry;
+  }
+  for (uint32_t b = tid; b < B; b += kPartBlock) {
+    uint32_t c = s_cnt[b];
+    uint32_t fit = 0, base = 0;
+    if (c) {
+      unsigned long long ret = atomicAdd(&pa.fill[b], (unsigned long long)c | (1ull << 40));
+      uint64_t eb = ret & ((1ull << 40) - 1);
+      uint64_t seg = ret >> 40;
+      pa.desc[(uint64_t)b * pa.max_segs + seg] = make_uint2((uint32_t)tile, (uint32_t)eb);
+      fit = eb >= pa.cap ? 0u : (uint32_t)(pa.cap - eb < c ? pa.cap - eb : c);
+      if (fit < c) pa.overflow[b] = 1u;
+      base = (uint32_t)eb;
+    }
+    s_base[b] = base;
+    s_fit[b] = fit;
+  }
+  __syncthreads();
+  // phase 2: counting-sort the records in LDS
+#pragma unroll
+  for (int j = 0; j < kPartPerThread; ++j) {
+    if (E[j] & 0x80000000u) {
+      const uint32_t b = (E[j] >> 13) & 0x3FFFFu;
+      const uint32_t rank = E[j] & 0x1FFFu;
+      const uint32_t q = (uint32_t)(j * kPartBlock + tid);
+      s_sorted[s_start[b] + rank] = O[j] | (q << 16);
+    }
+  }
+  __syncthreads();
+  // phase 3: one wave per bucket segment -> coalesced writes into the bucket array
+  const int wave = tid >> 6, lane = tid & 63;
+  for (uint32_t b = wave; b < B; b += kPartBlock / 64) {
+    const uint32_t c = s_cnt[b];
+    if (!c) continue;
+    const uint32_t src = s_start[b], fit = s_fit[b];
+    const uint64_t dst = (uint64_t)b * pa.cap + s_base[b];
+    for (uint32_t t = lane; t < c; t += 64) {
+      const uint32_t v = s_sorted[src + t];
+      if (t < fit) {
+        pa.off[dst + t] = (uint16_t)(v & 0xFFFFu);
+        pa.pos[dst + t] = (uint16_t)(v >> 16);
+      } else {  // bucket region full: count directly (correct, slow, rare)
+        atomicAdd(&pa.currents[((uint64_t)b << kBinBits) | (v & 0xFFFFu)], 1ULL);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kHistBlock) void k_bucket_hist(PartArgs pa, uint64_t pool,
+                                                            uint32_t slices,
+                                                            uint32_t *__restrict__ partials) {
+  __shared__ uint32_t h[kBinsPerBucket];
+  const uint32_t b = blockIdx.y, r = blockIdx.x;
+  for (int i = threadIdx.x; i < kBinsPerBucket; i += kHistBlock) h[i] = 0;
+  __syncthreads();
+  uint64_t n = pa.fill[b] & ((1ull << 40) - 1);
+  if (n > pa.cap) n = pa.cap;
+  const uint64_t lo = n * r / slices, hi = n * (r + 1) / slices;
+  const uint16_t *src = pa.off + (uint64_t)b * pa.cap;
+  // 8 records (16 B) per lane per step where aligned
+  uint64_t i = lo;
+  for (; i < hi && (i & 7); ++i)
+    if (threadIdx.x == 0) atomicAdd(&h[src[i]], 1u);
+  const uint64_t hi8 = i + ((hi - i) & ~7ull);
+  for (uint64_t j = i + 8ull * threadIdx.x; j < hi8; j += 8ull * kHistBlock) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(src + j);
+    atomicAdd(&h[v.x & 0xFFFFu], 1u); atomicAdd(&h[v.x >> 16], 1u);
+    atomicAdd(&h[v.y & 0xFFFFu], 1u); atomicAdd(&h[v.y >> 16], 1u);
+    atomicAdd(&h[v.z & 0xFFFFu], 1u); atomicAdd(&h[v.z >> 16], 1u);
+    atomicAdd(&h[v.w & 0xFFFFu], 1u); atomicAdd(&h[v.w >> 16], 1u);
+  }
+  for (uint64_t j = hi8 + threadIdx.x; j < hi; j += kHistBlock) atomicAdd(&h[src[j]], 1u);
+  __syncthreads();
+  const uint64_t nb0 = (uint64_t)b << kBinBits;
+  const uint64_t nbins = pool - nb0 < (uint64_t)kBinsPerBucket ? pool - nb0 : kBinsPerBucket;
+  uint32_t *dst = partials + (uint64_t)r * pool + nb0;
+  for (uint32_t t = threadIdx.x; t < nbins; t += kHistBlock) dst[t] = h[t];
+}
+
+__global__ void k_partials_add(const uint32_t *__restrict__ partials, uint32_t slices,
+                               uint64_t pool, unsigned long long *__restrict__ currents) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < pool;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    unsigned long long s = currents[i];
+    for (uint32_t r = 0; r < slices; ++r) s += partials[(uint64_t)r * pool + i];
+    currents[i] = s;
+  }
+}
+
+// Uniques from the kept records: scan only the buckets holding top-N neurons.
+template <bool CANON>
+__global__ __launch_bounds__(kHistBlock) void k_part_uniq(KmerInput in, int k, PartArgs pa,
+                                                          UniqArgs u,
+                                                          const uint32_t *__restrict__ tbuckets,
+                                                          uint32_t slices) {
+  __shared__ uint32_t bits[kBinsPerBucket / 32];
+  __shared__ uint32_t t_off[kMaxTopN];
+  __shared__ uint32_t t_slot[kMaxTopN];
+  __shared__ uint32_t t_n;
+  const uint32_t b = tbuckets[blockIdx.y], r = blockIdx.x;
+  for (int i = threadIdx.x; i < kBinsPerBucket / 32; i += kHistBlock) bits[i] = 0;
+  if (threadIdx.x == 0) t_n = 0;
+  __syncthreads();
+  for (uint32_t s = threadIdx.x; s < u.n_top; s += kHistBlock) {
+    const uint64_t idx = u.top[s].idx;
+    if ((idx >> kBinBits) == b) {
+      const uint32_t off = (uint32_t)(idx & (kBinsPerBucket - 1));
+      const uint32_t t = atomicAdd(&t_n, 1u);
+      t_off[t] = off;
+      t_slot[t] = s;
+      atomicOr(&bits[off >> 5], 1u << (off & 31));
+    }
+  }
+  __syncthreads();
+  uint64_t n = pa.fill[b] & ((1ull << 40) - 1);
+  if (n > pa.cap) n = pa.cap;
+  const uint64_t nseg = pa.fill[b] >> 40;
+  const uint64_t lo = n * r / slices, hi = n * (r + 1) / slices;
+  const uint16_t *src = pa.off + (uint64_t)b * pa.cap;
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += kHistBlock) {
+    const uint32_t off = src[i];
+    if (!((bits[off >> 5] >> (off & 31)) & 1u)) continue;
+    uint32_t slot = 0;
+    for (uint32_t t = 0; t < t_n; ++t)
+      if (t_off[t] == off) slot = t_slot[t];
+    // segment holding record i: last descriptor with base <= i
+    const uint2 *d = pa.desc + (uint64_t)b * pa.max_segs;
+    uint64_t a = 0, z = nseg;  // d[a].y <= i < d[z].y
+    while (z - a > 1) {
+      uint64_t m = (a + z) >> 1;
+      if (d[m].y <= i) a = m;
+      else z = m;
+    }
+    const uint64_t p = (uint64_t)d[a].x * kPartTile + pa.pos[(uint64_t)b * pa.cap + i];
+    set_insert(u, slot, global_window_key<CANON>(in.bases, p, k));
   }
 }
 
@@ -618,7 +688,7 @@ static FastMod make_fastmod(uint64_t p) {
   return f;
 }
 
-uint64_t n_tiles_for(uint64_t n_bases) { return (n_bases + kTile - 1) / kTile; }
+uint64_t n_tiles_for(uint64_t n_bases, uint64_t tile) { return (n_bases + tile - 1) / tile; }
 
 uint64_t top_tbl_size(uint32_t n_top) {
   uint64_t s = 64;
@@ -628,11 +698,12 @@ uint64_t top_tbl_size(uint32_t n_top) {
 
 static size_t tbl_bytes(const UniqArgs &u) { return (size_t)u.tbl_size * (8 + 4); }
 
-hipError_t launch_tile_rec(const KmerInput &in, uint32_t *tile_rec, hipStream_t s) {
+hipError_t launch_tile_rec(const KmerInput &in, uint64_t tile_size, uint32_t *tile_rec,
+                           hipStream_t s) {
   if (!in.n_tiles) return hipSuccess;
   unsigned g = (unsigned)((in.n_tiles + 255) / 256);
   hipLaunchKernelGGL(k_tile_rec, dim3(g), dim3(256), 0, s, in.offsets, in.n_recs, in.n_tiles,
-                     tile_rec);
+                     tile_size, tile_rec);
   return hipGetLastError();
 }
 
@@ -748,6 +819,46 @@ hipError_t launch_set_merge(const uint64_t *keys, uint64_t n, uint64_t pool, con
   if (g > 2048) g = 2048;
   hipLaunchKernelGGL(k_set_merge, dim3(g), dim3(256), tbl_bytes(u), s, keys, n,
                      make_fastmod(pool), u);
+  return hipGetLastError();
+}
+
+hipError_t launch_part(const KmerInput &in, int k, int canonical, uint64_t pool,
+                       const PartArgs &pa, hipStream_t s) {
+  if (!in.n_tiles) return hipSuccess;
+  FastMod fm = make_fastmod(pool);
+  if (canonical)
+    hipLaunchKernelGGL(k_part<true>, dim3((unsigned)in.n_tiles), dim3(kPartBlock), 0, s, in, k, fm, pa);
+  else
+    hipLaunchKernelGGL(k_part<false>, dim3((unsigned)in.n_tiles), dim3(kPartBlock), 0, s, in, k, fm, pa);
+  return hipGetLastError();
+}
+
+hipError_t launch_bucket_hist(const PartArgs &pa, uint64_t pool, uint32_t slices,
+                              uint32_t *partials, hipStream_t s) {
+  hipLaunchKernelGGL(k_bucket_hist, dim3(slices, pa.n_buckets), dim3(kHistBlock), 0, s, pa, pool,
+                     slices, partials);
+  return hipGetLastError();
+}
+
+hipError_t launch_partials_add(const uint32_t *partials, uint32_t slices, uint64_t pool,
+                               uint64_t *currents, hipStream_t s) {
+  unsigned g = (unsigned)((pool + 255) / 256);
+  if (g > 4096) g = 4096;
+  if (!g) return hipSuccess;
+  hipLaunchKernelGGL(k_partials_add, dim3(g), dim3(256), 0, s, partials, slices, pool,
+                     (unsigned long long *)currents);
+  return hipGetLastError();
+}
+
+hipError_t launch_part_uniques(const KmerInput &in, int k, int canonical, const PartArgs &pa,
+                               const UniqArgs &u, const uint32_t *tbuckets, uint32_t n_tb,
+                               uint32_t slices, hipStream_t s) {
+  if (!n_tb) return hipSuccess;
+  dim3 g(slices, n_tb);
+  if (canonical)
+    hipLaunchKernelGGL(k_part_uniq<true>, g, dim3(kHistBlock), 0, s, in, k, pa, u, tbuckets, slices);
+  else
+    hipLaunchKernelGGL(k_part_uniq<false>, g, dim3(kHistBlock), 0, s, in, k, pa, u, tbuckets, slices);
   return hipGetLastError();
 }
 

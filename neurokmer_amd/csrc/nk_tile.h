@@ -1,0 +1,183 @@
+// nk_tile.h — LDS staging of one tile of bases and per-position k-mer keys
+// (k <= 32), shared by the counting, partitioning and uniques kernels.
+//
+// A tile covers TILE k-mer start positions [T0, T0+TILE).  Its bytes plus a
+// 64-base halo are loaded with coalesced 16-B loads and converted ONCE into
+//   F   forward 2-bit codes, MSB-first   (base i at bits 31-2i.. of word i/16)
+//   R   complement 2-bit codes, LSB-first (base i at bits 2i.. of word i/16)
+//   INV invalid-byte bits, LSB-first     (non-ACGT bytes, pack_kmer's skip set)
+//   WIN invalid-window bits               (window crosses a record end)
+// so that a lane extracts any window's forward value and reverse complement
+// with two funnel shifts: no per-k-mer rolling, no per-lane serial chain.
+// Code tables: A/a 0, C/c 1, G/g 2, T/t 3, anything else 0 on BOTH strands
+// (src/models.rs:231-251) — exactly what the reference's rolling hash sees.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nk_kernels.h"
+
+namespace nk {
+
+__device__ __forceinline__ uint32_t eq_bytes(uint32_t t, uint32_t c) {
+  uint32_t z = t ^ c;
+  return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u;  // 0x80 where byte == c
+}
+
+struct Conv4 {
+  uint32_t fnib;  // 4 forward codes, first base in bits 7:6
+  uint32_t rnib;  // 4 complement codes, first base in bits 1:0
+  uint32_t inv;   // 4 invalid-byte bits, first base in bit 0
+};
+
+__device__ __forceinline__ Conv4 conv4(uint32_t x) {
+  uint32_t t = x | 0x20202020u;
+  uint32_t valid = eq_bytes(t, 0x61616161u) | eq_bytes(t, 0x63636363u) |
+                   eq_bytes(t, 0x67676767u) | eq_bytes(t, 0x74747474u);
+  uint32_t vm = valid >> 7;  // 0x01 per valid byte
+  uint32_t vm3 = vm * 3u;
+  uint32_t code = ((x >> 1) ^ (x >> 2)) & 0x03030303u & vm3;
+  uint32_t comp = (code ^ 0x03030303u) & vm3;
+  Conv4 o;
+  o.fnib = ((code << 6) & 0xC0u) | ((code >> 4) & 0x30u) | ((code >> 14) & 0x0Cu) |
+           ((code >> 24) & 0x03u);
+  o.rnib = (comp & 0x03u) | ((comp >> 6) & 0x0Cu) | ((comp >> 12) & 0x30u) |
+           ((comp >> 18) & 0xC0u);
+  uint32_t m = ~vm & 0x01010101u;
+  o.inv = (m & 1u) | ((m >> 7) & 2u) | ((m >> 14) & 4u) | ((m >> 21) & 8u);
+  return o;
+}
+
+__device__ __forceinline__ bool valid_byte(uint8_t b) {
+  uint32_t t = b | 0x20u;
+  return (t == 'a') | (t == 'c') | (t == 'g') | (t == 't');
+}
+__device__ __forceinline__ uint32_t code_of(uint8_t b) {
+  return valid_byte(b) ? (((uint32_t)b >> 1) ^ ((uint32_t)b >> 2)) & 3u : 0u;
+}
+__device__ __forceinline__ uint32_t comp_of(uint8_t b) {
+  return valid_byte(b) ? ((((uint32_t)b >> 1) ^ ((uint32_t)b >> 2)) & 3u) ^ 3u : 0u;
+}
+
+template <int TILE, bool RAW>
+struct TileLds {
+  static constexpr int kChunks = (TILE + 64) / 16;
+  uint32_t F[kChunks + 2];
+  uint32_t R[kChunks + 2];
+  uint16_t INV[kChunks + 4];
+  uint32_t WIN[TILE / 32];
+  uint4 RAWB[RAW ? kChunks : 1];
+};
+
+// Loads the tile, builds F/R/INV/WIN.  Ends with a __syncthreads().
+template <int TILE, int BLOCK, bool RAW>
+__device__ __forceinline__ void stage_tile(TileLds<TILE, RAW> &L, const KmerInput &in,
+                                           uint64_t tile, int k) {
+  constexpr int kChunks = TileLds<TILE, RAW>::kChunks;
+  const int tid = threadIdx.x;
+  const uint64_t T0 = tile * (uint64_t)TILE;
+  const uint64_t n_bases = in.n_bases;
+  for (int c = tid; c < kChunks; c += BLOCK) {
+    uint64_t g = T0 + 16ull * c;
+    uint4 v;
+    if (g + 16 <= n_bases) {
+      v = *reinterpret_cast<const uint4 *>(in.bases + g);
+    } else {
+      uint32_t w[4] = {0, 0, 0, 0};
+      for (int j = 0; j < 16; ++j)
+        if (g + j < n_bases) w[j >> 2] |= (uint32_t)in.bases[g + j] << (8 * (j & 3));
+      v = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    Conv4 a = conv4(v.x), b = conv4(v.y), cc = conv4(v.z), d = conv4(v.w);
+    L.F[c] = (a.fnib << 24) | (b.fnib << 16) | (cc.fnib << 8) | d.fnib;
+    L.R[c] = a.rnib | (b.rnib << 8) | (cc.rnib << 16) | (d.rnib << 24);
+    L.INV[c] = (uint16_t)(a.inv | (b.inv << 4) | (cc.inv << 8) | (d.inv << 12));
+    if (RAW) L.RAWB[c] = v;
+  }
+  if (tid < 2) { L.F[kChunks + tid] = 0; L.R[kChunks + tid] = 0; }
+  if (tid < 4) L.INV[kChunks + tid] = 0;
+  for (int i = tid; i < TILE / 32; i += BLOCK) L.WIN[i] = 0;
+  __syncthreads();
+  // windows crossing a record end (or running past the input) are not k-mers
+  const uint64_t limit = T0 + TILE + (uint64_t)k - 1;
+  const uint64_t r0 = in.tile_rec[tile];
+  for (uint64_t r = r0 + 1 + tid; r <= in.n_recs; r += BLOCK) {
+    uint64_t b = in.offsets[r];
+    if (b >= limit) break;
+    uint64_t lo = (b + 1 > (uint64_t)k) ? b + 1 - (uint64_t)k : 0;
+    if (lo < T0) lo = T0;
+    uint64_t hi = b < T0 + TILE ? b : T0 + TILE;
+    for (uint64_t q = lo - T0; q < hi - T0;) {
+      uint32_t w = (uint32_t)(q >> 5), s = (uint32_t)(q & 31);
+      uint32_t nb = (uint32_t)((hi - T0) - q);
+      uint32_t take = nb < 32 - s ? nb : 32 - s;
+      uint32_t bits = (take == 32 ? 0xFFFFFFFFu : ((1u << take) - 1u)) << s;
+      atomicOr(&L.WIN[w], bits);
+      q += take;
+    }
+  }
+  __syncthreads();
+}
+
+// true if local position q starts a k-mer of some record
+template <int TILE, bool RAW>
+__device__ __forceinline__ bool window_valid(const TileLds<TILE, RAW> &L, uint64_t T0, int q,
+                                             int k, uint64_t n_bases) {
+  return T0 + (uint64_t)q + (uint64_t)k <= n_bases && !((L.WIN[q >> 5] >> (q & 31)) & 1u);
+}
+
+// The reference's key for the window at local position q (k <= 32):
+// canonical = min(forward, reverse complement) (src/models.rs:284-286,
+// src/spiking_hash.rs:108,121-122); otherwise pack_kmer, which skips
+// non-ACGT bytes (src/utils.rs:26-39).
+template <int TILE, bool RAW, bool CANON>
+__device__ __forceinline__ uint64_t window_key(const TileLds<TILE, RAW> &L, int q, int k) {
+  const int twok = 2 * k;
+  const int w = q >> 4;
+  const int s = 2 * (q & 15);
+  uint64_t hi64 = ((uint64_t)L.F[w] << 32) | L.F[w + 1];
+  uint64_t x = (hi64 << s) | (((uint64_t)L.F[w + 2] << s) >> 32);
+  uint64_t fwd = x >> (64 - twok);
+  if (CANON) {
+    const uint64_t mask2k = (k >= 32) ? ~0ULL : ((1ULL << twok) - 1ULL);
+    uint64_t lo64 = ((uint64_t)L.R[w + 1] << 32) | L.R[w];
+    uint64_t y = (lo64 >> s) | (((uint64_t)L.R[w + 2] << 32) << (32 - s));
+    uint64_t rev = y & mask2k;
+    return fwd < rev ? fwd : rev;
+  } else {
+    const uint32_t kmask = (k >= 32) ? 0xFFFFFFFFu : ((1u << k) - 1u);
+    const int iw = q >> 4, is = q & 15;
+    uint64_t z = ((uint64_t)L.INV[iw] | ((uint64_t)L.INV[iw + 1] << 16) |
+                  ((uint64_t)L.INV[iw + 2] << 32) | ((uint64_t)L.INV[iw + 3] << 48)) >> is;
+    if (!((uint32_t)z & kmask)) return fwd;
+    const uint8_t *raw = reinterpret_cast<const uint8_t *>(L.RAWB);
+    uint64_t pk = 0;
+    for (int i = 0; i < k; ++i) {
+      uint8_t bb = raw[q + i];
+      if (valid_byte(bb)) pk = (pk << 2) | code_of(bb);
+    }
+    return pk;
+  }
+}
+
+// Same key straight from global memory (rare: uniques hits only).
+template <bool CANON>
+__device__ __forceinline__ uint64_t global_window_key(const uint8_t *b, uint64_t p, int k) {
+  if (CANON) {
+    uint64_t fwd = 0, rev = 0;
+    for (int i = 0; i < k; ++i) {
+      fwd = (fwd << 2) | code_of(b[p + i]);
+      rev |= (uint64_t)comp_of(b[p + i]) << (2 * i);
+    }
+    return fwd < rev ? fwd : rev;
+  } else {
+    uint64_t pk = 0;
+    for (int i = 0; i < k; ++i) {
+      uint8_t bb = b[p + i];
+      if (valid_byte(bb)) pk = (pk << 2) | code_of(bb);
+    }
+    return pk;
+  }
+}
+
+}  // namespace nk
