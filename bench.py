@@ -121,7 +121,7 @@ def main() -> int:
 
     def step():
         s = torch.cuda.current_stream().cuda_stream
-        ctr.reset()
+        ctr.reset(s, blocking=False)
         if world == 1:
             ctr.process_parallel_device(d_bases.data_ptr(), d_offs.data_ptr(), RECS, bases.size, s)
             return

@@ -136,6 +136,9 @@ int nk_copy_refractory(nk_counter *c, uint32_t *out, size_t n);
 uint64_t *nk_device_currents(nk_counter *c);
 /* Resets neurons, currents and energy to the state nk_new() left them in. */
 int nk_reset(nk_counter *c);
+/* Same, enqueued on `stream` (hipStream_t or NULL for the handle's stream)
+ * without waiting for it. */
+int nk_reset_async(nk_counter *c, void *stream);
 
 /* Per-stage device timings of the last process/finalize call, milliseconds
  * (hipEvents on the stream the kernels ran on).  Returns the number of stages

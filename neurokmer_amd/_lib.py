@@ -30,7 +30,8 @@ EXPORTS = (
     "nk_merge_top_kmers", "nk_top_abundant_neurons", "nk_get_count", "nk_total_spikes",
     "nk_energy_used", "nk_set_steps", "nk_get_steps", "nk_pool_size", "nk_k",
     "nk_use_canonical", "nk_copy_currents", "nk_copy_spike_counts", "nk_copy_voltages",
-    "nk_copy_refractory", "nk_device_currents", "nk_reset", "nk_last_timings", "nk_last_error",
+    "nk_copy_refractory", "nk_device_currents", "nk_reset", "nk_reset_async", "nk_last_timings",
+    "nk_last_error",
     "nk_version",
 )
 
@@ -103,6 +104,7 @@ def load(share_torch: bool = True):
         "nk_copy_refractory": (C.c_int, [vp, vp, sz]),
         "nk_device_currents": (vp, [vp]),
         "nk_reset": (C.c_int, [vp]),
+        "nk_reset_async": (C.c_int, [vp, vp]),
         "nk_last_timings": (C.c_int, [vp, P(C.c_char_p), P(C.c_float), C.c_int]),
         "nk_last_error": (C.c_char_p, []),
         "nk_version": (C.c_char_p, []),

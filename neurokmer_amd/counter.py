@@ -121,8 +121,13 @@ class SpikingKmerCounter:
     def device_currents_ptr(self) -> int:
         return self._L.nk_device_currents(self._h) or 0
 
-    def reset(self) -> None:
-        check(self._L.nk_reset(self._h))
+    def reset(self, stream: int = 0, blocking: bool = True) -> None:
+        """Fresh neuron pool (the state new() leaves).  blocking=False enqueues
+        the reset on `stream` and returns at once."""
+        if blocking:
+            check(self._L.nk_reset(self._h))
+        else:
+            check(self._L.nk_reset_async(self._h, stream or None))
 
     # ---- results -----------------------------------------------------------
     def top_abundant_neurons(self, n: int):

@@ -96,8 +96,16 @@ struct nk_counter {
   DevBuf<uint64_t> top_keys;
   DevBuf<unsigned long long> top_keys_n;
   DevBuf<uint32_t> radix_h;
-  uint64_t set_cap = 0;
+  uint64_t set_cap = 0;     // capacity used by the last uniques pass
+  uint64_t set_alloc = 0;   // allocated capacity of set_keys
   size_t n_top_keys = 0;
+  DevBuf<uint64_t> set_mask_d, set_need_d;
+  DevBuf<unsigned long long> hits, n_hits;  // uniques hit records (cap = set_alloc / 2)
+  DevBuf<uint32_t> post_flags;  // [0] set too small [1] top bucket overflowed [2] top buckets
+  // packed finalize results: ResultHdr | cand[m] | uniq[m]
+  static constexpr size_t kResBytes = sizeof(ResultHdr) + kMaxTopN * (sizeof(TopCand) + 4);
+  DevBuf<uint8_t> res_d;
+  uint8_t *res_h = nullptr;  // pinned
   // host copies of input (host-array entry points)
   DevBuf<uint8_t> in_bases;
   DevBuf<uint64_t> in_offs;
@@ -111,7 +119,6 @@ struct nk_counter {
   DevBuf<uint32_t> p_over, partials, tbuckets;
   PartArgs last_pa{};
   bool part_used = false;
-  bool part_overflow_top = false;
   // input of the last accumulate (for the uniques pass)
   KmerInput last_in{};
   bool have_input = false;
@@ -119,7 +126,6 @@ struct nk_counter {
   uint64_t total_spikes = 0, total_energy = 0;
   // top rows of the last finalize
   std::vector<nk_top_row> top;
-  std::vector<uint64_t> top_cur_h;
   bool top_valid = false;
   // timings
   hipEvent_t ev[kStages + 1] = {};  // see collect_timings
@@ -138,12 +144,24 @@ static hipStream_t pick_stream(nk_counter *c, void *s) {
   return s ? (hipStream_t)s : c->own_stream;
 }
 
-static int zero_state(nk_counter *c) {
+static int zero_state_on(nk_counter *c, hipStream_t s) {
+  c->total_spikes = c->total_energy = 0;
+  c->top_valid = false;
+  c->have_input = false;
   if (!c->pool) return NK_OK;
-  HIPCHK(hipMemsetAsync(c->cur.p, 0, c->pool * 8, c->own_stream));
-  HIPCHK(hipMemsetAsync(c->sc.p, 0, c->pool * 8, c->own_stream));
-  HIPCHK(hipMemsetAsync(c->v.p, 0, c->pool * 4, c->own_stream));
-  HIPCHK(hipMemsetAsync(c->r.p, 0, c->pool * 4, c->own_stream));
+  ZeroList z{};
+  z.ptr[0] = c->cur.p; z.bytes[0] = c->pool * 8;
+  z.ptr[1] = c->sc.p;  z.bytes[1] = c->pool * 8;
+  z.ptr[2] = c->v.p;   z.bytes[2] = c->pool * 4;
+  z.ptr[3] = c->r.p;   z.bytes[3] = c->pool * 4;
+  z.n = 4;
+  HIPCHK(launch_zero(z, s));
+  return NK_OK;
+}
+
+static int zero_state(nk_counter *c) {
+  int rc = zero_state_on(c, c->own_stream);
+  if (rc) return rc;
   HIPCHK(hipStreamSynchronize(c->own_stream));
   c->total_spikes = c->total_energy = 0;
   c->top_valid = false;
@@ -228,7 +246,12 @@ nk_counter *nk_new(size_t k, float threshold, float leak, uint32_t refractory, d
        !c->hist.ensure(kHistBins) && !c->stats.ensure(2) && !c->topst.ensure(1) &&
        !c->cand.ensure(kMaxTopN) && !c->top_cur.ensure(kMaxTopN) &&
        !c->uniq.ensure(kMaxTopN) && !c->special.ensure(kMaxTopN) &&
-       !c->top_keys_n.ensure(1) && !c->radix_h.ensure(256);
+       !c->top_keys_n.ensure(1) && !c->radix_h.ensure(256) && !c->set_mask_d.ensure(1) &&
+       !c->set_need_d.ensure(1) && !c->post_flags.ensure(4) && !c->set_keys.ensure(1 << 20) &&
+       !c->hits.ensure(1 << 19) && !c->n_hits.ensure(1) &&
+       !c->res_d.ensure(nk_counter::kResBytes) &&
+       hipHostMalloc((void **)&c->res_h, nk_counter::kResBytes) == hipSuccess;
+  c->set_alloc = 1 << 20;
   if (!ok || zero_state(c) != NK_OK) {
     std::string e = g_err.empty() ? "device allocation failed" : g_err;
     nk_free(c);
@@ -248,7 +271,10 @@ void nk_free(nk_counter *c) {
   c->tile_rec.release(); c->hist.release(); c->tie_cnt.release(); c->uniq.release();
   c->special.release(); c->stats.release(); c->lif_tbl.release(); c->topst.release();
   c->cand.release(); c->top_cur.release(); c->set_keys.release(); c->top_keys.release();
-  c->top_keys_n.release(); c->radix_h.release(); c->in_bases.release(); c->in_offs.release();
+  c->top_keys_n.release(); c->radix_h.release(); c->set_mask_d.release();
+  c->set_need_d.release(); c->post_flags.release(); c->hits.release(); c->n_hits.release();
+  c->res_d.release();
+  if (c->res_h) (void)hipHostFree(c->res_h); c->in_bases.release(); c->in_offs.release();
   for (int i = 0; i <= kStages; ++i)
     if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -259,6 +285,12 @@ int nk_reset(nk_counter *c) {
   if (!c) return fail(NK_E_INVALID, "null counter");
   (void)hipSetDevice(c->device);
   return zero_state(c);
+}
+
+int nk_reset_async(nk_counter *c, void *stream) {
+  if (!c) return fail(NK_E_INVALID, "null counter");
+  (void)hipSetDevice(c->device);
+  return zero_state_on(c, pick_stream(c, stream));
 }
 
 // ---------------------------------------------------------------------------
@@ -287,7 +319,6 @@ int nk_accumulate_device(nk_counter *c, const uint8_t *d_bases, const uint64_t *
   if (rc) return rc;
   in.tile_rec = c->tile_rec.p;
   HIPCHK(hipEventRecord(c->ev[0], s));
-  if (c->pool) HIPCHK(hipMemsetAsync(c->cur.p, 0, c->pool * 8, s));
   HIPCHK(launch_tile_rec(in, tile, c->tile_rec.p, s));
   HIPCHK(hipEventRecord(c->ev[1], s));
   c->part_used = part && in.n_tiles > 0;
@@ -311,14 +342,19 @@ int nk_accumulate_device(nk_counter *c, const uint8_t *d_bases, const uint64_t *
     pa.max_segs = in.n_tiles;
     pa.overflow = c->p_over.p;
     pa.currents = (unsigned long long *)c->cur.p;
-    HIPCHK(hipMemsetAsync(c->p_fill.p, 0, B * 8, s));
-    HIPCHK(hipMemsetAsync(c->p_over.p, 0, B * 4, s));
+    ZeroList z{};
+    z.ptr[0] = c->cur.p;    z.bytes[0] = c->pool * 8;
+    z.ptr[1] = c->p_fill.p; z.bytes[1] = B * 8;
+    z.ptr[2] = c->p_over.p; z.bytes[2] = B * 4;
+    z.n = 3;
+    HIPCHK(launch_zero(z, s));
     HIPCHK(launch_part(in, (int)c->k, c->canonical, c->pool, pa, s));
     HIPCHK(hipEventRecord(c->ev[2], s));
     HIPCHK(launch_bucket_hist(pa, c->pool, slices, c->partials.p, s));
     HIPCHK(launch_partials_add(c->partials.p, slices, c->pool, c->cur.p, s));
     c->last_pa = pa;
   } else {
+    if (c->pool) HIPCHK(hipMemsetAsync(c->cur.p, 0, c->pool * 8, s));
     HIPCHK(launch_count(in, (int)c->k, c->canonical, c->pool, c->cur.p, s));
     HIPCHK(hipEventRecord(c->ev[2], s));
   }
@@ -362,115 +398,66 @@ static int refine_threshold(nk_counter *c, uint64_t want, uint64_t max_sc, TopSt
   return NK_OK;
 }
 
-static int lif_and_top(nk_counter *c, int streaming, hipStream_t s) {
-  const uint64_t P = c->pool;
+static int enqueue_lif(nk_counter *c, int streaming, hipStream_t s) {
   LifParams lp;
   lp.steps = c->steps;
   lp.thr = c->thr;
   lp.leak = c->leak;
   lp.refr = c->refr;
-  lp.skip_zero = streaming ? 0 : 1;
+  lp.skip_zero = streaming ? 0 : 1;  // process_parallel skips zero currents (:189-191)
   int rc;
   // closed-form results for fresh neurons with count < 65536, cached per params
-  if (!c->lif_valid || c->lif_key.steps != lp.steps || c->lif_key.thr != lp.thr ||
-      c->lif_key.leak != lp.leak || c->lif_key.refr != lp.refr ||
+  if (!c->lif_valid || c->lif_key.steps != lp.steps || c->lif_key.refr != lp.refr ||
       memcmp(&c->lif_key.thr, &lp.thr, 4) || memcmp(&c->lif_key.leak, &lp.leak, 4)) {
     if ((rc = c->lif_tbl.ensure(kLifTable))) return rc;
     HIPCHK(launch_lif_table(c->lif_tbl.p, kLifTable, lp, s));
     c->lif_key = lp;
     c->lif_valid = true;
   }
-  HIPCHK(hipMemsetAsync(c->hist.p, 0, kHistBins * 4, s));
-  HIPCHK(hipMemsetAsync(c->stats.p, 0, 16, s));
-  // streaming with steps == 0 returns before touching neurons (src/spiking_hash.rs:549-551)
-  LifParams run = lp;
-  HIPCHK(launch_lif_apply(c->cur.p, c->v.p, c->r.p, c->sc.p, P, run, c->lif_tbl.p, kLifTable,
+  ZeroList z{};
+  z.ptr[0] = c->hist.p;  z.bytes[0] = kHistBins * 4;
+  z.ptr[1] = c->stats.p; z.bytes[1] = 16;
+  z.n = 2;
+  HIPCHK(launch_zero(z, s));
+  // steps == 0: the kernel leaves every neuron as it is (streaming returns early,
+  // src/spiking_hash.rs:549-551; in-memory runs zero iterations)
+  HIPCHK(launch_lif_apply(c->cur.p, c->v.p, c->r.p, c->sc.p, c->pool, lp, c->lif_tbl.p, kLifTable,
                           c->hist.p, c->stats.p, s));
-  HIPCHK(hipEventRecord(c->ev[4], s));
-  // top-N
-  const uint64_t want = std::min<uint64_t>(c->opts.top_n, P);
-  HIPCHK(launch_topn_threshold(c->hist.p, want, P, c->topst.p, s));
-  TopState st;
-  uint64_t stats[2];
-  HIPCHK(hipMemcpyAsync(&st, c->topst.p, sizeof st, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(stats, c->stats.p, sizeof stats, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  c->total_spikes += stats[0];
-  c->total_energy += stats[0] * cost_fixed(c->cost);
-  c->top.clear();
-  if (want) {
-    if (st.refine) {
-      if ((rc = refine_threshold(c, want, stats[1], st, s))) return rc;
-      HIPCHK(hipMemcpyAsync(c->topst.p, &st, sizeof st, hipMemcpyHostToDevice, s));
-    }
-    const unsigned nb = (unsigned)((P + 2047) / 2048);
-    if ((rc = c->tie_cnt.ensure(nb))) return rc;
-    HIPCHK(launch_topn_count(c->sc.p, P, c->topst.p, c->tie_cnt.p, s));
-    HIPCHK(launch_topn_emit(c->sc.p, P, c->topst.p, c->tie_cnt.p, c->cand.p, s));
-    HIPCHK(launch_topn_sort(c->cand.p, (uint32_t)want, c->cur.p, c->top_cur.p, s));
-    std::vector<TopCand> h(want);
-    c->top_cur_h.resize(want);
-    HIPCHK(hipMemcpyAsync(h.data(), c->cand.p, want * sizeof(TopCand), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(c->top_cur_h.data(), c->top_cur.p, want * 8, hipMemcpyDeviceToHost, s));
-    std::vector<uint32_t> over;
-    if (c->part_used && c->have_input) {
-      over.resize(c->last_pa.n_buckets);
-      HIPCHK(hipMemcpyAsync(over.data(), c->p_over.p, over.size() * 4, hipMemcpyDeviceToHost, s));
-    }
-    HIPCHK(hipStreamSynchronize(s));
-    c->part_overflow_top = false;
-    for (uint64_t i = 0; i < want && !over.empty(); ++i)
-      if (over[h[i].idx >> kBinBits]) c->part_overflow_top = true;
-    c->top.resize(want);
-    for (uint64_t i = 0; i < want; ++i) {
-      c->top[i].idx = h[i].idx;
-      c->top[i].spikes = h[i].sc;
-      c->top[i].uniques = 0;
-      c->top[i]._pad = 0;
-    }
-  }
-  HIPCHK(hipEventRecord(c->ev[5], s));
   return NK_OK;
 }
 
-static int uniques_pass(nk_counter *c, hipStream_t s) {
-  const uint32_t m = (uint32_t)c->top.size();
-  if (!m || !c->have_input || !c->last_in.n_tiles) {
-    HIPCHK(hipEventRecord(c->ev[6], s));
-    return NK_OK;
-  }
-  // upper bound of distinct keys in the top rows = sum of their currents
-  uint64_t sum = 0;
-  for (uint32_t i = 0; i < m; ++i) sum += c->top_cur_h[i];
-  uint64_t cap = 64;
-  while (cap < 2 * sum + 2) cap <<= 1;
+static int enqueue_select(nk_counter *c, uint64_t want, hipStream_t s) {
+  const unsigned nb = (unsigned)((c->pool + 2047) / 2048);
   int rc;
-  if ((rc = c->set_keys.ensure(cap))) return rc;
-  c->set_cap = cap;
-  HIPCHK(launch_set_fill(c->set_keys.p, cap, s));
-  HIPCHK(hipMemsetAsync(c->uniq.p, 0, m * 4, s));
-  HIPCHK(hipMemsetAsync(c->special.p, 0, m * 4, s));
+  if ((rc = c->tie_cnt.ensure(nb))) return rc;
+  HIPCHK(launch_topn_count(c->sc.p, c->pool, c->topst.p, c->tie_cnt.p, s));
+  HIPCHK(launch_topn_emit(c->sc.p, c->pool, c->topst.p, c->tie_cnt.p, c->cand.p, s));
+  HIPCHK(launch_topn_sort(c->cand.p, (uint32_t)want, c->cur.p, c->top_cur.p, s));
+  return NK_OK;
+}
+
+static int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, hipStream_t s) {
+  const bool part = c->part_used && !rescan;
+  int rc;
+  if ((rc = c->tbuckets.ensure(m))) return rc;
+  HIPCHK(launch_top_post(c->cand.p, c->top_cur.p, m, c->set_alloc, part ? c->p_over.p : nullptr,
+                         part ? 1 : 0, c->set_mask_d.p, c->tbuckets.p, c->post_flags.p, c->uniq.p,
+                         c->special.p, c->n_hits.p, s));
+  HIPCHK(launch_set_fill(c->set_keys.p, c->set_mask_d.p, c->set_alloc, s));
   UniqArgs u{};
   u.top = c->cand.p;
   u.n_top = m;
   u.tbl_size = (uint32_t)top_tbl_size(m);
   u.set_keys = c->set_keys.p;
-  u.set_mask = cap - 1;
+  u.set_mask = c->set_mask_d.p;
   u.uniq = c->uniq.p;
   u.special = c->special.p;
-  if (c->part_used && !c->part_overflow_top) {
-    // scan only the buckets that hold top neurons
-    std::vector<uint32_t> tb;
-    for (uint32_t i = 0; i < m; ++i) tb.push_back((uint32_t)(c->top[i].idx >> kBinBits));
-    std::sort(tb.begin(), tb.end());
-    tb.erase(std::unique(tb.begin(), tb.end()), tb.end());
-    if ((rc = c->tbuckets.ensure(tb.size()))) return rc;
-    HIPCHK(hipMemcpyAsync(c->tbuckets.p, tb.data(), tb.size() * 4, hipMemcpyHostToDevice, s));
-    const uint32_t slices = (uint32_t)std::max<size_t>(1, (512 + tb.size() - 1) / tb.size());
+  if (part) {
+    const uint32_t slices = std::max<uint32_t>(1, 512 / m);
     HIPCHK(launch_part_uniques(c->last_in, (int)c->k, c->canonical, c->last_pa, u, c->tbuckets.p,
-                               (uint32_t)tb.size(), slices, s));
+                               c->post_flags.p + 2, m, slices, c->hits.p, c->n_hits.p, c->hits.n,
+                               s));
   } else {
-    // full rescan (k > 32, large pools, or a top bucket overflowed its region)
     KmerInput in = c->last_in;
     in.n_tiles = n_tiles_for(in.n_bases, kTile);
     if ((rc = c->tile_rec.ensure(std::max<uint64_t>(in.n_tiles, 1)))) return rc;
@@ -478,11 +465,81 @@ static int uniques_pass(nk_counter *c, hipStream_t s) {
     HIPCHK(launch_tile_rec(in, kTile, c->tile_rec.p, s));
     HIPCHK(launch_uniques(in, (int)c->k, c->canonical, c->pool, u, s));
   }
-  std::vector<uint32_t> un(m);
-  HIPCHK(hipMemcpyAsync(un.data(), c->uniq.p, m * 4, hipMemcpyDeviceToHost, s));
+  return NK_OK;
+}
+
+static int enqueue_readback(nk_counter *c, uint32_t m, bool uniq, hipStream_t s) {
+  HIPCHK(launch_gather(c->topst.p, c->stats.p, uniq ? c->set_mask_d.p : nullptr,
+                       uniq ? c->post_flags.p : nullptr, c->cand.p, uniq ? c->uniq.p : nullptr, m,
+                       c->res_d.p, s));
+  const size_t bytes = sizeof(ResultHdr) + (size_t)m * (sizeof(TopCand) + 4);
+  HIPCHK(hipMemcpyAsync(c->res_h, c->res_d.p, bytes, hipMemcpyDeviceToHost, s));
+  return NK_OK;
+}
+
+// LIF + exact top-N + uniques with ONE host synchronisation in the common
+// case; the rare corrections (spike counts past the histogram, a hash set too
+// small for the top rows, an overflowed top bucket) are redone after it.
+static int lif_top_uniques(nk_counter *c, int streaming, hipStream_t s) {
+  int rc;
+  if ((rc = enqueue_lif(c, streaming, s))) return rc;
+  HIPCHK(hipEventRecord(c->ev[4], s));
+  const uint64_t want = std::min<uint64_t>(c->opts.top_n, c->pool);
+  const bool uniq = want && c->have_input && c->last_in.n_tiles;
+  if (want) {
+    HIPCHK(launch_topn_threshold(c->hist.p, want, c->pool, c->topst.p, s));
+    if ((rc = enqueue_select(c, want, s))) return rc;
+  }
+  HIPCHK(hipEventRecord(c->ev[5], s));
+  if (uniq && (rc = enqueue_uniques(c, (uint32_t)want, false, s))) return rc;
+  if ((rc = enqueue_readback(c, (uint32_t)want, uniq, s))) return rc;
   HIPCHK(hipEventRecord(c->ev[6], s));
   HIPCHK(hipStreamSynchronize(s));
-  for (uint32_t i = 0; i < m; ++i) c->top[i].uniques = un[i];
+  const ResultHdr *h = reinterpret_cast<const ResultHdr *>(c->res_h);
+  const TopCand *hc = reinterpret_cast<const TopCand *>(c->res_h + sizeof(ResultHdr));
+  const uint32_t *hu =
+      reinterpret_cast<const uint32_t *>(c->res_h + sizeof(ResultHdr) + want * sizeof(TopCand));
+  c->total_spikes += h->stats[0];
+  c->total_energy += h->stats[0] * cost_fixed(c->cost);
+  if (want && h->st.refine) {  // spike counts >= 4095: exact radix refine, redo
+    TopState st = h->st;
+    if ((rc = refine_threshold(c, want, h->stats[1], st, s))) return rc;
+    HIPCHK(hipMemcpyAsync(c->topst.p, &st, sizeof st, hipMemcpyHostToDevice, s));
+    if ((rc = enqueue_select(c, want, s))) return rc;
+    if (uniq && (rc = enqueue_uniques(c, (uint32_t)want, false, s))) return rc;
+    if ((rc = enqueue_readback(c, (uint32_t)want, uniq, s))) return rc;
+    HIPCHK(hipStreamSynchronize(s));
+  }
+  if (uniq) {
+    // set too small: grow to the capacity the top rows need, redo the pass
+    if (h->flags[0]) {
+      uint64_t cap = c->set_alloc;
+      uint64_t sum = 0;
+      std::vector<uint64_t> tc(want);
+      HIPCHK(hipMemcpyAsync(tc.data(), c->top_cur.p, want * 8, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      for (uint64_t x : tc) sum += x;
+      while (cap < 2 * sum + 2) cap <<= 1;
+      if ((rc = c->set_keys.ensure(cap))) return rc;
+      if ((rc = c->hits.ensure(cap / 2))) return rc;
+      c->set_alloc = cap;
+    }
+    if (h->flags[0] || h->flags[1]) {
+      if ((rc = enqueue_uniques(c, (uint32_t)want, h->flags[1] != 0, s))) return rc;
+      if ((rc = enqueue_readback(c, (uint32_t)want, uniq, s))) return rc;
+      HIPCHK(hipStreamSynchronize(s));
+    }
+    c->set_cap = h->mask + 1;
+  } else {
+    c->set_cap = 0;
+  }
+  c->top.resize(want);
+  for (uint64_t i = 0; i < want; ++i) {
+    c->top[i].idx = hc[i].idx;
+    c->top[i].spikes = hc[i].sc;
+    c->top[i].uniques = uniq ? hu[i] : 0;
+    c->top[i]._pad = 0;
+  }
   return NK_OK;
 }
 
@@ -509,9 +566,7 @@ int nk_finalize(nk_counter *c, int streaming, void *stream) {
   (void)hipSetDevice(c->device);
   hipStream_t s = pick_stream(c, stream);
   HIPCHK(hipEventRecord(c->ev[7], s));
-  int rc = lif_and_top(c, streaming, s);
-  if (rc) return rc;
-  rc = uniques_pass(c, s);
+  int rc = lif_top_uniques(c, streaming, s);
   if (rc) return rc;
   c->top_valid = true;
   collect_timings(c, false);
@@ -523,8 +578,7 @@ static int process_device(nk_counter *c, const uint8_t *d_bases, const uint64_t 
   int rc = nk_accumulate_device(c, d_bases, d_offs, n_recs, n_bases, stream);
   if (rc) return rc;
   hipStream_t s = pick_stream(c, stream);
-  if ((rc = lif_and_top(c, streaming, s))) return rc;
-  if ((rc = uniques_pass(c, s))) return rc;
+  if ((rc = lif_top_uniques(c, streaming, s))) return rc;
   c->top_valid = true;
   collect_timings(c, true);
   return NK_OK;
@@ -618,9 +672,13 @@ int nk_merge_top_kmers(nk_counter *c, const uint64_t *d_keys, size_t n_keys, voi
   uint64_t cap = 64;
   while (cap < 2 * (uint64_t)n_keys + 2) cap <<= 1;
   int rc;
-  if ((rc = c->set_keys.ensure(cap))) return rc;
+  if (cap > c->set_alloc) {
+    if ((rc = c->set_keys.ensure(cap))) return rc;
+    c->set_alloc = cap;
+  }
   c->set_cap = cap;
-  HIPCHK(launch_set_fill(c->set_keys.p, cap, s));
+  HIPCHK(launch_set_word(c->set_mask_d.p, cap - 1, s));
+  HIPCHK(launch_set_fill(c->set_keys.p, c->set_mask_d.p, c->set_alloc, s));
   HIPCHK(hipMemsetAsync(c->uniq.p, 0, m * 4, s));
   HIPCHK(hipMemsetAsync(c->special.p, 0, m * 4, s));
   UniqArgs u{};
@@ -628,14 +686,14 @@ int nk_merge_top_kmers(nk_counter *c, const uint64_t *d_keys, size_t n_keys, voi
   u.n_top = m;
   u.tbl_size = (uint32_t)top_tbl_size(m);
   u.set_keys = c->set_keys.p;
-  u.set_mask = cap - 1;
+  u.set_mask = c->set_mask_d.p;
   u.uniq = c->uniq.p;
   u.special = c->special.p;
   HIPCHK(launch_set_merge(d_keys, n_keys, c->pool, u, s));
-  std::vector<uint32_t> un(m);
-  HIPCHK(hipMemcpyAsync(un.data(), c->uniq.p, m * 4, hipMemcpyDeviceToHost, s));
+  uint32_t *hu = reinterpret_cast<uint32_t *>(c->res_h);
+  HIPCHK(hipMemcpyAsync(hu, c->uniq.p, m * 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  for (uint32_t i = 0; i < m; ++i) c->top[i].uniques = un[i];
+  for (uint32_t i = 0; i < m; ++i) c->top[i].uniques = hu[i];
   return NK_OK;
 }
 

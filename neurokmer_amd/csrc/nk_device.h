@@ -12,16 +12,25 @@
 
 namespace nk {
 
-__device__ __forceinline__ uint64_t rotl64(uint64_t x, int b) {
-  return (x << b) | (x >> (64 - b));
+// Cost model measured on gfx950 (tools/isabench.hip): VOP2 xor/add and
+// v_bitop3 issue at ~2.4 clk per wave64 instruction; v_alignbit, 64-bit ops
+// (v_lshl_add_u64), carry adds and multiplies at ~4.2.  So a 64-bit add is one
+// v_lshl_add_u64, a rotate is two v_alignbit on the 32-bit halves (a rotate by
+// 32 is a free register swap), and xors stay 32-bit VOP2: 70 clk per SipRound.
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  const uint32_t nlo = __builtin_amdgcn_alignbit(lo, hi, 32 - r);
+  const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 32 - r);
+  return ((uint64_t)nhi << 32) | nlo;
 }
+__device__ __forceinline__ uint64_t swap32(uint64_t x) { return (x << 32) | (x >> 32); }
 
 #define NK_SIPROUND                                                  \
   do {                                                               \
-    v0 += v1; v1 = rotl64(v1, 13); v1 ^= v0; v0 = rotl64(v0, 32);    \
+    v0 += v1; v1 = rotl64(v1, 13); v1 ^= v0; v0 = swap32(v0);        \
     v2 += v3; v3 = rotl64(v3, 16); v3 ^= v2;                         \
     v0 += v3; v3 = rotl64(v3, 21); v3 ^= v0;                         \
-    v2 += v1; v1 = rotl64(v1, 17); v1 ^= v2; v2 = rotl64(v2, 32);    \
+    v2 += v1; v1 = rotl64(v1, 17); v1 ^= v2; v2 = swap32(v2);        \
   } while (0)
 
 // SipHash-1-3 with key (0,0) of one u64 written as 8 LE bytes:

@@ -45,6 +45,20 @@ struct TopCand {
   uint64_t sc;
 };
 
+constexpr int kZeroMax = 8;
+struct ZeroList {
+  void *ptr[kZeroMax];
+  uint64_t bytes[kZeroMax];
+  int n;
+};
+
+struct ResultHdr {  // header of the packed finalize results (one D2H copy)
+  TopState st;
+  uint64_t stats[2];
+  uint64_t mask;
+  uint32_t flags[4];
+};
+
 // input description shared by the k-mer kernels
 struct KmerInput {
   const uint8_t *bases;
@@ -72,7 +86,7 @@ struct UniqArgs {
   uint32_t n_top;
   uint32_t tbl_size;   // LDS probe table size (pow2 >= 2*n_top)
   unsigned long long *set_keys;  // global hash set of k-mer keys
-  uint64_t set_mask;
+  const uint64_t *set_mask;      // device word: capacity - 1
   uint32_t *uniq;      // per top row: distinct keys
   uint32_t *special;   // per top row: key == ~0 seen
 };
@@ -97,7 +111,18 @@ hipError_t launch_topn_emit(const uint64_t *sc, uint64_t pool, TopState *st,
                             const uint32_t *tie_cnt, TopCand *cand, hipStream_t s);
 hipError_t launch_topn_sort(TopCand *cand, uint32_t m, const uint64_t *currents,
                             uint64_t *top_cur, hipStream_t s);
-hipError_t launch_set_fill(unsigned long long *keys, uint64_t cap, hipStream_t s);
+hipError_t launch_set_fill(unsigned long long *keys, const uint64_t *mask, uint64_t max_cap,
+                           hipStream_t s);
+hipError_t launch_top_post(const TopCand *top, const uint64_t *top_cur, uint32_t m,
+                           uint64_t set_alloc, const uint32_t *overflow, int part,
+                           uint64_t *set_mask, uint32_t *tbuckets, uint32_t *flags,
+                           uint32_t *uniq, uint32_t *special, unsigned long long *n_hits,
+                           hipStream_t s);
+hipError_t launch_set_word(uint64_t *w, uint64_t v, hipStream_t s);
+hipError_t launch_zero(const ZeroList &z, hipStream_t s);
+hipError_t launch_gather(const TopState *st, const uint64_t *stats, const uint64_t *mask,
+                         const uint32_t *flags, const TopCand *cand, const uint32_t *uniq,
+                         uint32_t m, uint8_t *out, hipStream_t s);
 hipError_t launch_set_compact(const unsigned long long *keys, uint64_t cap, const uint32_t *special,
                               uint32_t n_top, const TopCand *top, uint64_t pool,
                               uint64_t *out, unsigned long long *count, hipStream_t s);
@@ -111,8 +136,9 @@ hipError_t launch_bucket_hist(const PartArgs &pa, uint64_t pool, uint32_t slices
 hipError_t launch_partials_add(const uint32_t *partials, uint32_t slices, uint64_t pool,
                                uint64_t *currents, hipStream_t s);
 hipError_t launch_part_uniques(const KmerInput &in, int k, int canonical, const PartArgs &pa,
-                               const UniqArgs &u, const uint32_t *tbuckets, uint32_t n_tb,
-                               uint32_t slices, hipStream_t s);
+                               const UniqArgs &u, const uint32_t *tbuckets, const uint32_t *n_tb,
+                               uint32_t max_tb, uint32_t slices, unsigned long long *hits,
+                               unsigned long long *n_hits, uint64_t hit_cap, hipStream_t s);
 
 uint64_t top_tbl_size(uint32_t n_top);
 uint64_t n_tiles_for(uint64_t n_bases, uint64_t tile);

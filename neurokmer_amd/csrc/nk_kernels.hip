@@ -53,20 +53,51 @@ __global__ void k_tile_rec(const uint64_t *__restrict__ offsets, uint64_t n_recs
 // ---------------------------------------------------------------------------
 // top-N membership table in LDS (MODE 1)
 // ---------------------------------------------------------------------------
+// Per-workgroup filter in front of the global set: a key this workgroup has
+// already inserted is dropped in LDS.  Hot neurons (repeats) otherwise send
+// thousands of identical inserts to one global slot, which serialise at the
+// memory side.  Returns true when the key was seen before by this workgroup.
+constexpr int kSeen = 1024;
+__device__ __forceinline__ void seen_init(unsigned long long *seen) {
+  for (int i = threadIdx.x; i < kSeen; i += blockDim.x) seen[i] = kEmpty;
+}
+__device__ __forceinline__ bool seen_before(unsigned long long *seen, uint64_t key) {
+  uint32_t h = (uint32_t)mix64(key) & (kSeen - 1);
+  for (int probe = 0; probe < 16; ++probe) {
+    unsigned long long v = seen[h];
+    if (v == key) return true;
+    if (v == kEmpty) {
+      unsigned long long prev = atomicCAS(&seen[h], kEmpty, (unsigned long long)key);
+      if (prev == kEmpty) return false;
+      if (prev == key) return true;
+    }
+    h = (h + 1) & (kSeen - 1);
+  }
+  return false;  // table crowded: let the global set decide
+}
+
 __device__ __forceinline__ void set_insert(const UniqArgs &u, uint32_t slot, uint64_t key) {
   if (key == kEmpty) {
     if (atomicCAS(&u.special[slot], 0u, 1u) == 0u) atomicAdd(&u.uniq[slot], 1u);
     return;
   }
-  uint64_t h = mix64(key) & u.set_mask;
+  const uint64_t mask = *u.set_mask;
+  uint64_t h = mix64(key) & mask;
   for (;;) {
-    unsigned long long prev = atomicCAS(&u.set_keys[h], kEmpty, (unsigned long long)key);
-    if (prev == kEmpty) {
-      atomicAdd(&u.uniq[slot], 1u);
-      return;
+    // read first: repeated k-mers (the hot neurons) find their key without
+    // serialising on one address; a stale kEmpty only costs an extra CAS
+    unsigned long long cur = __hip_atomic_load(&u.set_keys[h], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == key) return;
+    if (cur == kEmpty) {
+      unsigned long long prev = atomicCAS(&u.set_keys[h], kEmpty, (unsigned long long)key);
+      if (prev == kEmpty) {
+        atomicAdd(&u.uniq[slot], 1u);
+        return;
+      }
+      if (prev == key) return;
     }
-    if (prev == key) return;
-    h = (h + 1) & u.set_mask;
+    h = (h + 1) & mask;
   }
 }
 
@@ -105,10 +136,14 @@ __global__ __launch_bounds__(kBlock) void k_kmers(KmerInput in, int k, FastMod f
                                                   unsigned long long *__restrict__ currents,
                                                   UniqArgs u) {
   __shared__ TileLds<kTile, !CANON> L;
+  __shared__ unsigned long long seen[MODE == 1 ? kSeen : 1];
   extern __shared__ uint64_t dyn[];  // MODE 1: probe table
   uint64_t *tbl_idx = dyn;
   uint32_t *tbl_slot = reinterpret_cast<uint32_t *>(dyn + (MODE == 1 ? u.tbl_size : 0));
-  if (MODE == 1) build_top_tbl(u, tbl_idx, tbl_slot);  // contains __syncthreads
+  if (MODE == 1) {
+    seen_init(seen);
+    build_top_tbl(u, tbl_idx, tbl_slot);  // contains __syncthreads
+  }
   const uint64_t T0 = (uint64_t)blockIdx.x * kTile;
   stage_tile<kTile, kBlock, !CANON>(L, in, blockIdx.x, k);
 #pragma unroll 4
@@ -122,7 +157,7 @@ __global__ __launch_bounds__(kBlock) void k_kmers(KmerInput in, int k, FastMod f
       atomicAdd(&currents[idx], 1ULL);
     } else {
       int slot = probe_top(tbl_idx, tbl_slot, u.tbl_size - 1, idx);
-      if (slot >= 0) set_insert(u, (uint32_t)slot, key);
+      if (slot >= 0 && (key == kEmpty || !seen_before(seen, key))) set_insert(u, (uint32_t)slot, key);
     }
   }
 }
@@ -139,9 +174,13 @@ __global__ __launch_bounds__(kBlock) void k_kmers_compat(KmerInput in, int k, Fa
                                                          unsigned long long *__restrict__ currents,
                                                          UniqArgs u) {
   extern __shared__ uint64_t dyn[];
+  __shared__ unsigned long long seen[MODE == 1 ? kSeen : 1];
   uint64_t *tbl_idx = dyn;
   uint32_t *tbl_slot = reinterpret_cast<uint32_t *>(dyn + (MODE == 1 ? u.tbl_size : 0));
-  if (MODE == 1) build_top_tbl(u, tbl_idx, tbl_slot);
+  if (MODE == 1) {
+    seen_init(seen);
+    build_top_tbl(u, tbl_idx, tbl_slot);
+  }
 
   const uint64_t T0 = (uint64_t)blockIdx.x * kTile;
   const uint32_t sh = (uint32_t)((2 * (k - 1)) & 63);
@@ -183,7 +222,7 @@ __global__ __launch_bounds__(kBlock) void k_kmers_compat(KmerInput in, int k, Fa
       atomicAdd(&currents[idx], 1ULL);
     } else {
       int slot = probe_top(tbl_idx, tbl_slot, u.tbl_size - 1, idx);
-      if (slot >= 0) set_insert(u, (uint32_t)slot, key);
+      if (slot >= 0 && (key == kEmpty || !seen_before(seen, key))) set_insert(u, (uint32_t)slot, key);
     }
   }
 }
@@ -320,7 +359,21 @@ __global__ __launch_bounds__(kHistBlock) void k_bucket_hist(PartArgs pa, uint64_
   for (; i < hi && (i & 7); ++i)
     if (threadIdx.x == 0) atomicAdd(&h[src[i]], 1u);
   const uint64_t hi8 = i + ((hi - i) & ~7ull);
-  for (uint64_t j = i + 8ull * threadIdx.x; j < hi8; j += 8ull * kHistBlock) {
+  const uint64_t step = 8ull * kHistBlock;
+  uint64_t j = i + 8ull * threadIdx.x;
+  for (; j + 3 * step < hi8; j += 4 * step) {  // four 16-B loads in flight
+    uint4 v[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) v[t] = *reinterpret_cast<const uint4 *>(src + j + t * step);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      atomicAdd(&h[v[t].x & 0xFFFFu], 1u); atomicAdd(&h[v[t].x >> 16], 1u);
+      atomicAdd(&h[v[t].y & 0xFFFFu], 1u); atomicAdd(&h[v[t].y >> 16], 1u);
+      atomicAdd(&h[v[t].z & 0xFFFFu], 1u); atomicAdd(&h[v[t].z >> 16], 1u);
+      atomicAdd(&h[v[t].w & 0xFFFFu], 1u); atomicAdd(&h[v[t].w >> 16], 1u);
+    }
+  }
+  for (; j < hi8; j += step) {
     const uint4 v = *reinterpret_cast<const uint4 *>(src + j);
     atomicAdd(&h[v.x & 0xFFFFu], 1u); atomicAdd(&h[v.x >> 16], 1u);
     atomicAdd(&h[v.y & 0xFFFFu], 1u); atomicAdd(&h[v.y >> 16], 1u);
@@ -345,19 +398,90 @@ __global__ void k_partials_add(const uint32_t *__restrict__ partials, uint32_t s
   }
 }
 
-// Uniques from the kept records: scan only the buckets holding top-N neurons.
+// Key of the k-mer at absolute position p (k <= 32) from three 16-B loads,
+// through the same conversion as the tile staging.
 template <bool CANON>
-__global__ __launch_bounds__(kHistBlock) void k_part_uniq(KmerInput in, int k, PartArgs pa,
-                                                          UniqArgs u,
+__device__ __forceinline__ uint64_t vec_window_key(const uint8_t *bases, uint64_t n_bases,
+                                                   uint64_t p, int k) {
+  const uint64_t a = p & ~15ull;
+  uint32_t F[3], R[3], INV[3];
+  for (int c = 0; c < 3; ++c) {
+    const uint64_t g = a + 16ull * c;
+    uint4 v;
+    if (g + 16 <= n_bases) {
+      v = *reinterpret_cast<const uint4 *>(bases + g);
+    } else {
+      uint32_t w[4] = {0, 0, 0, 0};
+      for (int j = 0; j < 16; ++j)
+        if (g + j < n_bases) w[j >> 2] |= (uint32_t)bases[g + j] << (8 * (j & 3));
+      v = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    Conv4 x = conv4(v.x), y = conv4(v.y), z = conv4(v.z), t = conv4(v.w);
+    F[c] = (x.fnib << 24) | (y.fnib << 16) | (z.fnib << 8) | t.fnib;
+    R[c] = x.rnib | (y.rnib << 8) | (z.rnib << 16) | (t.rnib << 24);
+    INV[c] = x.inv | (y.inv << 4) | (z.inv << 8) | (t.inv << 12);
+  }
+  const int q = (int)(p - a), s = 2 * q, twok = 2 * k;
+  const uint64_t hi64 = ((uint64_t)F[0] << 32) | F[1];
+  const uint64_t fwd = ((hi64 << s) | (((uint64_t)F[2] << s) >> 32)) >> (64 - twok);
+  if (CANON) {
+    const uint64_t mask2k = (k >= 32) ? ~0ULL : ((1ULL << twok) - 1ULL);
+    const uint64_t lo64 = ((uint64_t)R[1] << 32) | R[0];
+    const uint64_t rev = ((lo64 >> s) | (((uint64_t)R[2] << 32) << (32 - s))) & mask2k;
+    return fwd < rev ? fwd : rev;
+  }
+  const uint64_t inv = ((uint64_t)INV[0] | ((uint64_t)INV[1] << 16) | ((uint64_t)INV[2] << 32)) >> q;
+  const uint64_t kmask = (1ull << k) - 1ull;
+  if (!(inv & kmask)) return fwd;
+  return global_window_key<false>(bases, p, k);
+}
+
+// Last index a in [0, n) with d[a].y <= x (d sorted by .y, d[0].y <= x), found
+// by one wave with 64-ary steps: 2-4 dependent loads instead of ~log2(n).
+__device__ uint64_t wave_search_le(const uint2 *d, uint64_t n, uint64_t x) {
+  const int lane = threadIdx.x & 63;
+  uint64_t lo = 0, hi = n;
+  while (hi - lo > 1) {
+    const uint64_t step = (hi - lo + 63) / 64;
+    const uint64_t idx = lo + (uint64_t)lane * step;
+    const bool ok = idx < hi && d[idx].y <= x;
+    const uint64_t mask = __ballot(ok);
+    const int last = 63 - __clzll((long long)mask);  // lane 0 always ok
+    lo = lo + (uint64_t)last * step;
+    const uint64_t nh = lo + step;
+    hi = nh < hi ? nh : hi;
+  }
+  return lo;
+}
+
+// Uniques from the kept records, in two flat kernels:
+//   U1 k_uniq_scan: stream the records of the buckets holding top-N neurons
+//      (16-B loads), test each bin offset against an LDS bitmap of the
+//      bucket's top bins, collect hits {bucket, top row, record index} in LDS
+//      and publish them with one global reservation per workgroup;
+//   U2 k_uniq_hits: one lane per hit: record -> segment -> tile (binary
+//      search of the segment descriptors), recompute the key from the bases,
+//      per-workgroup dedup in LDS, insert into the global hash set.
+// Hits never serialise inside a wave and no lane waits on another's latency.
+constexpr int kScanBuf = 4096;
+
+__global__ __launch_bounds__(kHistBlock) void k_uniq_scan(PartArgs pa, UniqArgs u,
                                                           const uint32_t *__restrict__ tbuckets,
-                                                          uint32_t slices) {
+                                                          const uint32_t *__restrict__ n_tb,
+                                                          uint32_t slices,
+                                                          unsigned long long *__restrict__ hits,
+                                                          unsigned long long *__restrict__ n_hits,
+                                                          uint64_t hit_cap) {
   __shared__ uint32_t bits[kBinsPerBucket / 32];
   __shared__ uint32_t t_off[kMaxTopN];
   __shared__ uint32_t t_slot[kMaxTopN];
-  __shared__ uint32_t t_n;
+  __shared__ unsigned long long buf[kScanBuf];
+  __shared__ uint32_t t_n, s_nh;
+  __shared__ unsigned long long s_base;
+  if (blockIdx.y >= *n_tb) return;
   const uint32_t b = tbuckets[blockIdx.y], r = blockIdx.x;
   for (int i = threadIdx.x; i < kBinsPerBucket / 32; i += kHistBlock) bits[i] = 0;
-  if (threadIdx.x == 0) t_n = 0;
+  if (threadIdx.x == 0) { t_n = 0; s_nh = 0; }
   __syncthreads();
   for (uint32_t s = threadIdx.x; s < u.n_top; s += kHistBlock) {
     const uint64_t idx = u.top[s].idx;
@@ -372,25 +496,89 @@ __global__ __launch_bounds__(kHistBlock) void k_part_uniq(KmerInput in, int k, P
   __syncthreads();
   uint64_t n = pa.fill[b] & ((1ull << 40) - 1);
   if (n > pa.cap) n = pa.cap;
-  const uint64_t nseg = pa.fill[b] >> 40;
   const uint64_t lo = n * r / slices, hi = n * (r + 1) / slices;
+  const uint32_t tn = t_n;
   const uint16_t *src = pa.off + (uint64_t)b * pa.cap;
-  for (uint64_t i = lo + threadIdx.x; i < hi; i += kHistBlock) {
-    const uint32_t off = src[i];
-    if (!((bits[off >> 5] >> (off & 31)) & 1u)) continue;
+  // one hit record: bucket | top row | record index (< 2^38)
+  auto push = [&](uint64_t i, uint32_t off) {
     uint32_t slot = 0;
-    for (uint32_t t = 0; t < t_n; ++t)
+    for (uint32_t t = 0; t < tn; ++t)
       if (t_off[t] == off) slot = t_slot[t];
-    // segment holding record i: last descriptor with base <= i
+    const unsigned long long e = ((unsigned long long)b << 48) |
+                                 ((unsigned long long)slot << 38) | i;
+    const uint32_t at = atomicAdd(&s_nh, 1u);
+    if (at < kScanBuf) {
+      buf[at] = e;
+    } else {  // LDS list full (very hit-dense slice): publish this one directly
+      const unsigned long long g = atomicAdd(n_hits, 1ull);
+      if (g < hit_cap) hits[g] = e;
+    }
+  };
+  // 8 records per 16-B load, two loads in flight per lane, no barrier in the loop
+  const uint64_t lo8 = lo & ~7ull;
+  const uint64_t step = 8ull * kHistBlock;
+  for (uint64_t c0 = lo8 + 8ull * threadIdx.x; c0 < hi; c0 += 2 * step) {
+    const uint64_t c1 = c0 + step;
+    const uint4 v0 = *reinterpret_cast<const uint4 *>(src + c0);
+    uint4 v1 = make_uint4(0, 0, 0, 0);
+    if (c1 < hi) v1 = *reinterpret_cast<const uint4 *>(src + c1);
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const uint4 v = half ? v1 : v0;
+      const uint64_t base = half ? c1 : c0;
+      const uint64_t w01 = ((uint64_t)v.y << 32) | v.x, w23 = ((uint64_t)v.w << 32) | v.z;
+      uint32_t hm = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t off = (uint32_t)(((j < 4 ? w01 : w23) >> (16 * (j & 3))) & 0xFFFFu);
+        const uint64_t i = base + j;
+        if (i >= lo && i < hi && ((bits[off >> 5] >> (off & 31)) & 1u)) hm |= 1u << j;
+      }
+#pragma unroll 1
+      while (hm) {
+        const int j = __ffs(hm) - 1;
+        hm &= hm - 1;
+        push(base + j, (uint32_t)(((j < 4 ? w01 : w23) >> (16 * (j & 3))) & 0xFFFFu));
+      }
+    }
+  }
+  __syncthreads();
+  const uint32_t nh = s_nh < (uint32_t)kScanBuf ? s_nh : (uint32_t)kScanBuf;
+  if (nh) {
+    if (threadIdx.x == 0) s_base = atomicAdd(n_hits, (unsigned long long)nh);
+    __syncthreads();
+    const unsigned long long gb = s_base;
+    for (uint32_t h = threadIdx.x; h < nh; h += kHistBlock)
+      if (gb + h < hit_cap) hits[gb + h] = buf[h];
+  }
+}
+
+template <bool CANON>
+__global__ __launch_bounds__(256) void k_uniq_hits(KmerInput in, int k, PartArgs pa, UniqArgs u,
+                                                   const unsigned long long *__restrict__ hits,
+                                                   const unsigned long long *__restrict__ n_hits,
+                                                   uint64_t hit_cap) {
+  __shared__ unsigned long long seen[kSeen];
+  seen_init(seen);
+  __syncthreads();
+  uint64_t nh = *n_hits;
+  if (nh > hit_cap) nh = hit_cap;
+  for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < nh;
+       h += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long e = hits[h];
+    const uint32_t b = (uint32_t)(e >> 48);
+    const uint32_t slot = (uint32_t)((e >> 38) & 0x3FFu);
+    const uint64_t i = e & ((1ull << 38) - 1);
     const uint2 *d = pa.desc + (uint64_t)b * pa.max_segs;
-    uint64_t a = 0, z = nseg;  // d[a].y <= i < d[z].y
+    uint64_t a = 0, z = pa.fill[b] >> 40;  // last segment with first record <= i
     while (z - a > 1) {
-      uint64_t m = (a + z) >> 1;
+      const uint64_t m = (a + z) >> 1;
       if (d[m].y <= i) a = m;
       else z = m;
     }
     const uint64_t p = (uint64_t)d[a].x * kPartTile + pa.pos[(uint64_t)b * pa.cap + i];
-    set_insert(u, slot, global_window_key<CANON>(in.bases, p, k));
+    const uint64_t key = vec_window_key<CANON>(in.bases, in.n_bases, p, k);
+    if (key == kEmpty || !seen_before(seen, key)) set_insert(u, slot, key);
   }
 }
 
@@ -643,7 +831,8 @@ __global__ __launch_bounds__(1024) void k_topn_sort(TopCand *__restrict__ cand, 
 // ---------------------------------------------------------------------------
 // device hash set helpers (uniques of the top-N neurons)
 // ---------------------------------------------------------------------------
-__global__ void k_set_fill(unsigned long long *__restrict__ keys, uint64_t cap) {
+__global__ void k_set_fill(unsigned long long *__restrict__ keys, const uint64_t *__restrict__ mask) {
+  const uint64_t cap = *mask + 1;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap;
        i += (uint64_t)gridDim.x * blockDim.x)
     keys[i] = kEmpty;
@@ -666,15 +855,17 @@ __global__ void k_set_compact(const unsigned long long *__restrict__ keys, uint6
 
 __global__ void k_set_merge(const uint64_t *__restrict__ keys, uint64_t n, FastMod fm, UniqArgs u) {
   extern __shared__ uint64_t dyn[];
+  __shared__ unsigned long long seen[kSeen];
   uint64_t *tbl_idx = dyn;
   uint32_t *tbl_slot = reinterpret_cast<uint32_t *>(dyn + u.tbl_size);
+  seen_init(seen);
   build_top_tbl(u, tbl_idx, tbl_slot);
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * blockDim.x) {
     uint64_t key = keys[i];
     uint64_t idx = fastmod(sip13_u64(key), fm);
     int slot = probe_top(tbl_idx, tbl_slot, u.tbl_size - 1, idx);
-    if (slot >= 0) set_insert(u, (uint32_t)slot, key);
+    if (slot >= 0 && (key == kEmpty || !seen_before(seen, key))) set_insert(u, (uint32_t)slot, key);
   }
 }
 
@@ -793,11 +984,12 @@ hipError_t launch_topn_sort(TopCand *cand, uint32_t m, const uint64_t *currents,
   return hipGetLastError();
 }
 
-hipError_t launch_set_fill(unsigned long long *keys, uint64_t cap, hipStream_t s) {
-  unsigned g = (unsigned)((cap + 255) / 256);
-  if (g > 4096) g = 4096;
+hipError_t launch_set_fill(unsigned long long *keys, const uint64_t *mask, uint64_t max_cap,
+                           hipStream_t s) {
+  unsigned g = (unsigned)((max_cap + 255) / 256);
+  if (g > 2048) g = 2048;
   if (!g) return hipSuccess;
-  hipLaunchKernelGGL(k_set_fill, dim3(g), dim3(256), 0, s, keys, cap);
+  hipLaunchKernelGGL(k_set_fill, dim3(g), dim3(256), 0, s, keys, mask);
   return hipGetLastError();
 }
 
@@ -851,14 +1043,131 @@ hipError_t launch_partials_add(const uint32_t *partials, uint32_t slices, uint64
 }
 
 hipError_t launch_part_uniques(const KmerInput &in, int k, int canonical, const PartArgs &pa,
-                               const UniqArgs &u, const uint32_t *tbuckets, uint32_t n_tb,
-                               uint32_t slices, hipStream_t s) {
-  if (!n_tb) return hipSuccess;
-  dim3 g(slices, n_tb);
+                               const UniqArgs &u, const uint32_t *tbuckets, const uint32_t *n_tb,
+                               uint32_t max_tb, uint32_t slices, unsigned long long *hits,
+                               unsigned long long *n_hits, uint64_t hit_cap, hipStream_t s) {
+  if (!max_tb) return hipSuccess;
+  hipLaunchKernelGGL(k_uniq_scan, dim3(slices, max_tb), dim3(kHistBlock), 0, s, pa, u, tbuckets,
+                     n_tb, slices, hits, n_hits, hit_cap);
+  const unsigned g = 1024;
   if (canonical)
-    hipLaunchKernelGGL(k_part_uniq<true>, g, dim3(kHistBlock), 0, s, in, k, pa, u, tbuckets, slices);
+    hipLaunchKernelGGL(k_uniq_hits<true>, dim3(g), dim3(256), 0, s, in, k, pa, u, hits, n_hits,
+                       hit_cap);
   else
-    hipLaunchKernelGGL(k_part_uniq<false>, g, dim3(kHistBlock), 0, s, in, k, pa, u, tbuckets, slices);
+    hipLaunchKernelGGL(k_uniq_hits<false>, dim3(g), dim3(256), 0, s, in, k, pa, u, hits, n_hits,
+                       hit_cap);
+  return hipGetLastError();
+}
+
+// After the top-N sort: size the uniques hash set from the top rows' currents
+// (distinct keys <= their sum), list the distinct buckets holding top rows and
+// flag the rare cases the host must redo (set too small, a top bucket whose
+// region overflowed).  One block.
+__global__ __launch_bounds__(1024) void k_top_post(const TopCand *__restrict__ top,
+                                                   const uint64_t *__restrict__ top_cur,
+                                                   uint32_t m, uint64_t set_alloc,
+                                                   const uint32_t *__restrict__ overflow,
+                                                   int part, uint64_t *__restrict__ set_mask,
+                                                   uint32_t *__restrict__ tbuckets,
+                                                   uint32_t *__restrict__ flags,
+                                                   uint32_t *__restrict__ uniq,
+                                                   uint32_t *__restrict__ special,
+                                                   unsigned long long *__restrict__ n_hits) {
+  __shared__ unsigned long long s_sum;
+  __shared__ uint32_t s_nb, s_over;
+  if (threadIdx.x == 0) { s_sum = 0; s_nb = 0; s_over = 0; *n_hits = 0; }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+    uniq[i] = 0;
+    special[i] = 0;
+    atomicAdd(&s_sum, (unsigned long long)top_cur[i]);
+    if (part) {
+      const uint32_t b = (uint32_t)(top[i].idx >> kBinBits);
+      if (overflow[b]) s_over = 1;
+      bool first = true;  // first row of its bucket in the list
+      for (uint32_t j = 0; j < i; ++j)
+        if ((uint32_t)(top[j].idx >> kBinBits) == b) { first = false; break; }
+      if (first) tbuckets[atomicAdd(&s_nb, 1u)] = b;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t cap = 64;
+    while (cap < 2 * (uint64_t)s_sum + 2) cap <<= 1;
+    flags[0] = cap > set_alloc ? 1u : 0u;  // set too small
+    flags[1] = s_over;                     // a top bucket overflowed
+    flags[2] = s_nb;                       // distinct top buckets
+    flags[3] = 0;
+    *set_mask = (cap > set_alloc ? set_alloc : cap) - 1;
+  }
+}
+
+hipError_t launch_top_post(const TopCand *top, const uint64_t *top_cur, uint32_t m,
+                           uint64_t set_alloc, const uint32_t *overflow, int part,
+                           uint64_t *set_mask, uint32_t *tbuckets, uint32_t *flags,
+                           uint32_t *uniq, uint32_t *special, unsigned long long *n_hits,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(k_top_post, dim3(1), dim3(1024), 0, s, top, top_cur, m, set_alloc, overflow,
+                     part, set_mask, tbuckets, flags, uniq, special, n_hits);
+  return hipGetLastError();
+}
+
+__global__ void k_set_word(uint64_t *__restrict__ w, uint64_t v) { *w = v; }
+hipError_t launch_set_word(uint64_t *w, uint64_t v, hipStream_t s) {
+  hipLaunchKernelGGL(k_set_word, dim3(1), dim3(1), 0, s, w, v);
+  return hipGetLastError();
+}
+
+// One launch zeroes up to kZeroMax buffers (16-B stores for the bulk).
+__global__ void k_zero(ZeroList z) {
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (int b = 0; b < z.n; ++b) {
+    uint8_t *p = (uint8_t *)z.ptr[b];
+    const uint64_t n = z.bytes[b];
+    const uint64_t n16 = ((uintptr_t)p & 15) ? 0 : n / 16;
+    for (uint64_t i = tid; i < n16; i += stride) reinterpret_cast<uint4 *>(p)[i] = make_uint4(0, 0, 0, 0);
+    for (uint64_t i = n16 * 16 + tid; i < n; i += stride) p[i] = 0;
+  }
+}
+
+hipError_t launch_zero(const ZeroList &z, hipStream_t s) {
+  uint64_t tot = 0;
+  for (int b = 0; b < z.n; ++b) tot += z.bytes[b];
+  if (!tot) return hipSuccess;
+  unsigned g = (unsigned)((tot / 16 + 255) / 256);
+  if (g > 2048) g = 2048;
+  if (!g) g = 1;
+  hipLaunchKernelGGL(k_zero, dim3(g), dim3(256), 0, s, z);
+  return hipGetLastError();
+}
+
+// Everything the host needs after a finalize, packed for ONE D2H copy:
+// [TopState | stats[2] | set mask | flags[4] | cand[m] | uniq[m]]
+__global__ void k_gather(const TopState *__restrict__ st, const uint64_t *__restrict__ stats,
+                         const uint64_t *__restrict__ mask, const uint32_t *__restrict__ flags,
+                         const TopCand *__restrict__ cand, const uint32_t *__restrict__ uniq,
+                         uint32_t m, uint8_t *__restrict__ out) {
+  ResultHdr *h = reinterpret_cast<ResultHdr *>(out);
+  TopCand *c = reinterpret_cast<TopCand *>(out + sizeof(ResultHdr));
+  uint32_t *u = reinterpret_cast<uint32_t *>(out + sizeof(ResultHdr) + (size_t)m * sizeof(TopCand));
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    h->st = *st;
+    h->stats[0] = stats[0];
+    h->stats[1] = stats[1];
+    h->mask = mask ? *mask : 0;
+    for (int i = 0; i < 4; ++i) h->flags[i] = flags ? flags[i] : 0;
+  }
+  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+    c[i] = cand[i];
+    u[i] = uniq ? uniq[i] : 0;
+  }
+}
+
+hipError_t launch_gather(const TopState *st, const uint64_t *stats, const uint64_t *mask,
+                         const uint32_t *flags, const TopCand *cand, const uint32_t *uniq,
+                         uint32_t m, uint8_t *out, hipStream_t s) {
+  hipLaunchKernelGGL(k_gather, dim3(1), dim3(1024), 0, s, st, stats, mask, flags, cand, uniq, m, out);
   return hipGetLastError();
 }
 
