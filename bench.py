@@ -61,32 +61,26 @@ def load_pmc_traffic():
         return None, None
 
 
-def cpu_baseline(bases: np.ndarray, offsets: np.ndarray, target_s: float = 12.0):
-    """The C restatement of process_parallel (oracle/, 'port') on a bounded
-    prefix of every record of the same workload: parallel over records like
-    rayon, exact k-mer map, serial merge + LIF, as in src/spiking_hash.rs:84-201."""
+def cpu_baseline(bases: np.ndarray, offsets: np.ndarray, per_record: int = 2_000_000):
+    """The C restatement of process_parallel (oracle/nk_oracle.c, 'port') on a
+    bounded sample of the same workload: the first `per_record` bases of each
+    of the 7 records, parallel over records like rayon (src/spiking_hash.rs:
+    94-95; 7 threads), exact k-mer map, serial merge, serial 2M-neuron LIF
+    (:157-200).  About 10 s of CPU work."""
     from oracle import cbind
-
-    def sample(per_rec):
-        segs = [bases[int(offsets[i]):int(offsets[i]) + per_rec] for i in range(offsets.size - 1)]
-        offs = np.zeros(len(segs) + 1, np.uint64)
-        np.cumsum([s.size for s in segs], out=offs[1:])
-        return np.concatenate(segs), offs
-
+    per = int(min(per_record, np.diff(offsets.astype(np.int64)).min()))
+    segs = [bases[int(offsets[i]):int(offsets[i]) + per] for i in range(offsets.size - 1)]
+    offs = np.zeros(len(segs) + 1, np.uint64)
+    np.cumsum([x.size for x in segs], out=offs[1:])
+    b = np.concatenate(segs)
     threads = offsets.size - 1  # one rayon work unit per record
-    per = 200_000
-    while True:
-        b, o = sample(per)
-        ref = cbind.OracleCounter(K, 1.0, 0.95, 2, 1.0, POOL, True)
-        t0 = time.perf_counter()
-        ref.process_parallel_arrays(b, o, threads)
-        dt = time.perf_counter() - t0
-        nk = n_kmers(o, K)
-        if dt >= target_s / 4 or per * 4 > int(np.diff(offsets).min()):
-            break
-        per = min(int(per * max(2.0, target_s / max(dt, 1e-3))), int(np.diff(offsets).min()))
-    return {"rate": nk / dt / 1e6, "seconds": dt, "kmers": nk, "bases": int(o[-1]),
-            "per_record": per, "threads": threads, "ref": ref, "sample": (b, o)}
+    ref = cbind.OracleCounter(K, 1.0, 0.95, 2, 1.0, POOL, True)
+    t0 = time.perf_counter()
+    ref.process_parallel_arrays(b, offs, threads)
+    dt = time.perf_counter() - t0
+    nk = n_kmers(offs, K)
+    return {"rate": nk / dt / 1e6, "seconds": dt, "kmers": nk, "bases": int(offs[-1]),
+            "per_record": per, "threads": threads, "ref": ref, "sample": (b, offs)}
 
 
 def main() -> int:
@@ -96,17 +90,26 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--bases", type=int, default=BASES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    # test-only: rehearse the multi-rank path on a 1-GPU box (gloo, all ranks on cuda:0)
+    ap.add_argument("--dist-backend", default="nccl")
+    ap.add_argument("--same-device", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.same_device:
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
     dev = torch.device("cuda", local)
 
     from neurokmer_amd import SpikingKmerCounter, synth
+    from neurokmer_amd import dist as nkdist
 
     # ---- this rank's shard of the synthetic input (resident in HBM) --------
     bases, offsets = synth.make_records(args.bases, RECS, seed=synth.SEED ^ (rank * 0x9E37),
@@ -126,19 +129,12 @@ def main() -> int:
             ctr.process_parallel_device(d_bases.data_ptr(), d_offs.data_ptr(), RECS, bases.size, s)
             return
         ctr.accumulate_device(d_bases.data_ptr(), d_offs.data_ptr(), RECS, bases.size, s)
-        dist.all_reduce(cur_t)  # RCCL over xGMI: u64 currents (as int64, same bits)
+        nkdist.allreduce_currents_(cur_t)  # RCCL over xGMI: u64 currents (int64, same bits)
         ctr.finalize(False, s)
         ptr, n = ctr.top_kmers_device()
-        mine = (torch.as_tensor(_CAI(ptr, n), device=dev).clone() if n
+        mine = (torch.as_tensor(_CAI(ptr, n), device=dev) if n
                 else torch.zeros(0, dtype=torch.int64, device=dev))
-        sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-        dist.all_gather(sizes, torch.tensor([n], dtype=torch.int64, device=dev))
-        mx = int(max(int(x.item()) for x in sizes))
-        pad = torch.full((mx,), -1, dtype=torch.int64, device=dev)
-        pad[:n] = mine
-        parts = [torch.empty(mx, dtype=torch.int64, device=dev) for _ in range(world)]
-        dist.all_gather(parts, pad)
-        allk = torch.cat([p[:int(sz.item())] for p, sz in zip(parts, sizes)])
+        allk = nkdist.gather_union(mine)  # union of every shard's top-N k-mers
         ctr.merge_top_kmers(allk.data_ptr(), allk.numel(), s)
 
     for _ in range(args.warmup):
@@ -151,7 +147,7 @@ def main() -> int:
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        count_ms.append(ctr.last_timings().get("count", float("nan")) if world == 1 else None)
+        count_ms.append(ctr.last_timings().get("count", float("nan")))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -216,9 +212,10 @@ def main() -> int:
                 "value": round(cb["rate"], 4), "unit": "Mk-mers/s", "cores": cb["threads"],
                 "kind": "port",
                 "sample": f"first {cb['per_record']} bases of each of the {RECS} records of "
-                          f"rank 0's workload ({cb['bases']} bases, {cb['kmers']} k-mers), "
-                          f"{cb['seconds']:.2f} s, oracle/nk_oracle.c process_parallel "
-                          f"(parallel over records, exact k-mer map)"}
+                          f"rank 0's workload ({cb['bases']} bases, {cb['kmers']} k-mers, "
+                          f"pool 2M, k=31, canonical) in {cb['seconds']:.2f} s: oracle/nk_oracle.c "
+                          f"process_parallel restatement (parallel over records, exact k-mer "
+                          f"map, serial merge and 2M x 1000-step LIF)"}
             out["parity_on_cpu_sample"] = parity
         print(json.dumps(out), flush=True)
     ctr.close()

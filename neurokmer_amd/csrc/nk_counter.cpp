@@ -243,7 +243,7 @@ nk_counter *nk_new(size_t k, float threshold, float leak, uint32_t refractory, d
   for (int i = 0; ok && i <= kStages; ++i) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
   size_t P = pool_size ? pool_size : 1;
   ok = ok && !c->cur.ensure(P) && !c->sc.ensure(P) && !c->v.ensure(P) && !c->r.ensure(P) &&
-       !c->hist.ensure(kHistBins) && !c->stats.ensure(2) && !c->topst.ensure(1) &&
+       !c->hist.ensure(kHistBins * kHistCopies) && !c->stats.ensure(2) && !c->topst.ensure(1) &&
        !c->cand.ensure(kMaxTopN) && !c->top_cur.ensure(kMaxTopN) &&
        !c->uniq.ensure(kMaxTopN) && !c->special.ensure(kMaxTopN) &&
        !c->top_keys_n.ensure(1) && !c->radix_h.ensure(256) && !c->set_mask_d.ensure(1) &&
@@ -327,7 +327,8 @@ int nk_accumulate_device(nk_counter *c, const uint8_t *d_bases, const uint64_t *
     // still exact: the excess is counted with direct atomics)
     uint64_t cap = n_bases / B * 5 / 4 + kPartTile;
     cap = (cap + 63) & ~63ull;
-    const uint32_t slices = (uint32_t)std::max<uint64_t>(1, (256 + B - 1) / B);
+    // one round of 1-per-CU workgroups (128 KiB LDS each) on 256 CUs
+    const uint32_t slices = (uint32_t)std::max<uint64_t>(1, 256 / B);
     if ((rc = c->p_off.ensure(B * cap)) || (rc = c->p_pos.ensure(B * cap)) ||
         (rc = c->p_fill.ensure(B)) || (rc = c->p_desc.ensure(B * in.n_tiles)) ||
         (rc = c->p_over.ensure(B)) || (rc = c->partials.ensure(slices * c->pool)))
@@ -415,7 +416,7 @@ static int enqueue_lif(nk_counter *c, int streaming, hipStream_t s) {
     c->lif_valid = true;
   }
   ZeroList z{};
-  z.ptr[0] = c->hist.p;  z.bytes[0] = kHistBins * 4;
+  z.ptr[0] = c->hist.p;  z.bytes[0] = kHistBins * kHistCopies * 4;
   z.ptr[1] = c->stats.p; z.bytes[1] = 16;
   z.n = 2;
   HIPCHK(launch_zero(z, s));
@@ -569,7 +570,8 @@ int nk_finalize(nk_counter *c, int streaming, void *stream) {
   int rc = lif_top_uniques(c, streaming, s);
   if (rc) return rc;
   c->top_valid = true;
-  collect_timings(c, false);
+  // an accumulate on this handle precedes: report its stages too
+  collect_timings(c, c->have_input);
   return NK_OK;
 }
 

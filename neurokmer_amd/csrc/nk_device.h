@@ -70,6 +70,25 @@ __device__ __forceinline__ uint64_t fastmod(uint64_t h, FastMod fm) {
   return r;
 }
 
+// Exact h % P for P < 2^30 in 32-bit arithmetic: r = h - q*P < 3P < 2^32, so
+// only the low word of q = mulhi64(h, magic) is needed (one mul_hi + two
+// v_mad_u64_u32 + one mul_lo), then r = h_lo - q_lo*P (mod 2^32) and two
+// branch-free corrections min(r, r - P).  Checked against % on 2.4e8 values
+// (tools/README).
+__device__ __forceinline__ uint32_t fastmod32(uint64_t h, FastMod fm) {
+  const uint32_t h0 = (uint32_t)h, h1 = (uint32_t)(h >> 32);
+  const uint32_t m0 = (uint32_t)fm.magic, m1 = (uint32_t)(fm.magic >> 32);
+  const uint32_t p = (uint32_t)fm.p;
+  const uint32_t ahi = __umulhi(h0, m0);
+  uint64_t mid = (uint64_t)h1 * m0 + ahi;
+  mid = (uint64_t)h0 * m1 + mid;
+  const uint32_t qlo = h1 * m1 + (uint32_t)(mid >> 32);
+  uint32_t r = h0 - qlo * p;
+  r = min(r, r - p);
+  r = min(r, r - p);
+  return r;
+}
+
 // ---- LIF -------------------------------------------------------------------
 // One LifNeuron::update with input c (src/models.rs:34-51); f32 ops rounded
 // separately (__fmul_rn/__fadd_rn are never contracted into an FMA).

@@ -8,6 +8,7 @@ namespace nk {
 constexpr int kTile = 4096;      // k-mer start positions per workgroup
 constexpr int kBlock = 256;      // threads per workgroup (4 waves)
 constexpr int kHistBins = 4096;  // spike-count histogram for top-N selection
+constexpr int kHistCopies = 8;   // one per XCD group of LIF blocks
 constexpr int kMaxTopN = 1024;
 // partitioned count
 constexpr int kPartTile = 8192;       // positions per K1a workgroup

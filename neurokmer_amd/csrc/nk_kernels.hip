@@ -249,7 +249,7 @@ constexpr int kPartPerThread = kPartTile / kPartBlock;  // 16
 template <bool CANON>
 __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMod fm, PartArgs pa) {
   __shared__ TileLds<kPartTile, !CANON> L;
-  __shared__ uint32_t s_cnt[kMaxBuckets];
+  __shared__ uint32_t s_cnt[kMaxBuckets + 1];  // + a dummy bucket for non-k-mer positions
   __shared__ uint32_t s_start[kMaxBuckets + 1];
   __shared__ uint32_t s_base[kMaxBuckets];
   __shared__ uint32_t s_fit[kMaxBuckets];
@@ -259,25 +259,73 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
   const uint64_t tile = blockIdx.x;
   const uint64_t T0 = tile * (uint64_t)kPartTile;
   const uint32_t B = pa.n_buckets;
-  for (uint32_t b = tid; b < B; b += kPartBlock) s_cnt[b] = 0;
+  for (uint32_t b = tid; b <= B; b += kPartBlock) s_cnt[b] = 0;
   stage_tile<kPartTile, kPartBlock, !CANON>(L, in, tile, k);  // syncs
 
-  // phase 1: key -> neuron -> (bucket, rank within the tile's bucket)
-  uint32_t E[kPartPerThread];  // bit31 valid | bucket << 13 | rank
+  // phase 1: this lane's 16 consecutive positions q0..q0+15.  The first
+  // window is extracted from the bit streams, the next 15 are rolled in from
+  // two 32-bit code words (forward MSB-first, complement LSB-first), exactly
+  // the reference's slide for k <= 32 (src/models.rs:254-269).  The body is
+  // branch-free: a position that starts no k-mer goes to a dummy bucket.
+  const int q0 = tid * kPartPerThread;
+  const uint64_t rem = in.n_bases - T0;  // >= 1
+  const uint64_t nrange = rem >= (uint64_t)k ? rem - (uint64_t)k + 1 : 0;
+  uint32_t ok = ~(L.WIN[q0 >> 5] >> (q0 & 31)) & 0xFFFFu;
+  if (nrange < (uint64_t)q0 + kPartPerThread)
+    ok &= nrange > (uint64_t)q0 ? (1u << (uint32_t)(nrange - q0)) - 1u : 0u;
+  const int twok = 2 * k;
+  const uint64_t mask2k = (k >= 32) ? ~0ULL : ((1ULL << twok) - 1ULL);
+  uint64_t fwd, rev;
+  {
+    const int w = q0 >> 4;  // q0 is 16-aligned: shift 0
+    const uint64_t x = ((uint64_t)L.F[w] << 32) | L.F[w + 1];
+    fwd = x >> (64 - twok);
+    rev = (((uint64_t)L.R[w + 1] << 32) | L.R[w]) & mask2k;
+  }
+  uint32_t inF, inR;  // codes of the 15 bases rolled in: positions q0+k .. q0+k+14
+  {
+    const int s0 = q0 + k;
+    const int w = s0 >> 4, sh = 2 * (s0 & 15);
+    inF = (uint32_t)(((((uint64_t)L.F[w] << 32) | L.F[w + 1]) << sh) >> 32);
+    inR = (uint32_t)((((uint64_t)L.R[w + 1] << 32) | L.R[w]) >> sh);
+  }
+  uint64_t invz = 0;  // non-canonical: invalid-byte bits of positions q0 .. q0+47
+  if (!CANON) {
+    const int iw = q0 >> 4;
+    invz = (uint64_t)L.INV[iw] | ((uint64_t)L.INV[iw + 1] << 16) | ((uint64_t)L.INV[iw + 2] << 32);
+  }
+  const uint32_t kmask = (k >= 32) ? 0xFFFFFFFFu : ((1u << k) - 1u);
+  const int topsh = twok - 2;
+  uint32_t E[kPartPerThread];  // bucket << 16 | rank
   uint32_t O[kPartPerThread];  // bin offset within the bucket
 #pragma unroll
   for (int j = 0; j < kPartPerThread; ++j) {
-    const int q = j * kPartBlock + tid;
-    E[j] = 0;
-    O[j] = 0;
-    if (window_valid(L, T0, q, k, in.n_bases)) {
-      const uint64_t key = window_key<kPartTile, !CANON, CANON>(L, q, k);
-      const uint32_t idx = (uint32_t)fastmod(sip13_u64(key), fm);
-      const uint32_t b = idx >> kBinBits;
-      const uint32_t rank = atomicAdd(&s_cnt[b], 1u);
-      E[j] = 0x80000000u | (b << 13) | rank;
-      O[j] = idx & (kBinsPerBucket - 1);
+    if (j) {
+      const uint32_t c = (inF >> (32 - 2 * j)) & 3u;
+      const uint32_t cc = (inR >> (2 * (j - 1))) & 3u;
+      fwd = ((fwd << 2) | c) & mask2k;
+      rev = (rev >> 2) | ((uint64_t)cc << topsh);
     }
+    uint64_t key;
+    if (CANON) {
+      key = fwd < rev ? fwd : rev;
+    } else {
+      key = fwd;
+      if (((uint32_t)(invz >> j)) & kmask) {  // pack_kmer skips non-ACGT bytes (rare)
+        const uint8_t *raw = reinterpret_cast<const uint8_t *>(L.RAWB);
+        uint64_t pk = 0;
+        for (int i = 0; i < k; ++i) {
+          const uint8_t bb = raw[q0 + j + i];
+          if (valid_byte(bb)) pk = (pk << 2) | code_of(bb);
+        }
+        key = pk;
+      }
+    }
+    const uint32_t idx = fastmod32(sip13_u64(key), fm);
+    const uint32_t b = ((ok >> j) & 1u) ? (idx >> kBinBits) : B;
+    const uint32_t rank = atomicAdd(&s_cnt[b], 1u);
+    E[j] = (b << 16) | rank;
+    O[j] = idx & (kBinsPerBucket - 1);
   }
   __syncthreads();
   // exclusive scan of the bucket counts (one wave) + HBM reservation (one
@@ -316,12 +364,8 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
   // phase 2: counting-sort the records in LDS
 #pragma unroll
   for (int j = 0; j < kPartPerThread; ++j) {
-    if (E[j] & 0x80000000u) {
-      const uint32_t b = (E[j] >> 13) & 0x3FFFFu;
-      const uint32_t rank = E[j] & 0x1FFFu;
-      const uint32_t q = (uint32_t)(j * kPartBlock + tid);
-      s_sorted[s_start[b] + rank] = O[j] | (q << 16);
-    }
+    const uint32_t b = E[j] >> 16;
+    if (b < B) s_sorted[s_start[b] + (E[j] & 0xFFFFu)] = O[j] | ((uint32_t)(q0 + j) << 16);
   }
   __syncthreads();
   // phase 3: one wave per bucket segment -> coalesced writes into the bucket array
@@ -599,7 +643,8 @@ __global__ void k_lif_table(LifEntry *__restrict__ tbl, int n, LifParams lp) {
 
 constexpr int kLifPerThread = 8;
 
-__global__ __launch_bounds__(kBlock) void k_lif_apply(const uint64_t *__restrict__ currents,
+constexpr int kLifBlock = 1024;
+__global__ __launch_bounds__(kLifBlock) void k_lif_apply(const uint64_t *__restrict__ currents,
                                                       float *__restrict__ V,
                                                       uint32_t *__restrict__ R,
                                                       uint64_t *__restrict__ SC, uint64_t pool,
@@ -608,14 +653,14 @@ __global__ __launch_bounds__(kBlock) void k_lif_apply(const uint64_t *__restrict
                                                       uint32_t *__restrict__ hist,
                                                       unsigned long long *__restrict__ stats) {
   __shared__ uint32_t sh[kHistBins];
-  __shared__ unsigned long long s_sp[kBlock / 64];
-  __shared__ unsigned long long s_mx[kBlock / 64];
-  for (int i = threadIdx.x; i < kHistBins; i += kBlock) sh[i] = 0;
+  __shared__ unsigned long long s_sp[kLifBlock / 64];
+  __shared__ unsigned long long s_mx[kLifBlock / 64];
+  for (int i = threadIdx.x; i < kHistBins; i += kLifBlock) sh[i] = 0;
   __syncthreads();
-  const uint64_t base = (uint64_t)blockIdx.x * kBlock * kLifPerThread;
+  const uint64_t base = (uint64_t)blockIdx.x * kLifBlock * kLifPerThread;
   unsigned long long my_sp = 0, my_mx = 0;
   for (int j = 0; j < kLifPerThread; ++j) {
-    uint64_t i = base + (uint64_t)j * kBlock + threadIdx.x;
+    uint64_t i = base + (uint64_t)j * kLifBlock + threadIdx.x;
     if (i >= pool) break;
     uint64_t cnt = currents[i];
     uint64_t sc = SC[i];
@@ -650,12 +695,15 @@ __global__ __launch_bounds__(kBlock) void k_lif_apply(const uint64_t *__restrict
   __syncthreads();
   if (threadIdx.x == 0) {
     unsigned long long a = 0, m = 0;
-    for (int w = 0; w < kBlock / 64; ++w) { a += s_sp[w]; m = s_mx[w] > m ? s_mx[w] : m; }
+    for (int w = 0; w < kLifBlock / 64; ++w) { a += s_sp[w]; m = s_mx[w] > m ? s_mx[w] : m; }
     if (a) atomicAdd(&stats[0], a);
     atomicMax(&stats[1], m);
   }
-  for (int i = threadIdx.x; i < kHistBins; i += kBlock)
-    if (sh[i]) atomicAdd(&hist[i], sh[i]);
+  // 8 copies of the global histogram (blocks b, b+8, ... share one), summed by
+  // the threshold kernel: the hot spike-count bins see 8x fewer atomics each
+  uint32_t *hc = hist + (size_t)(blockIdx.x & (kHistCopies - 1)) * kHistBins;
+  for (int i = threadIdx.x; i < kHistBins; i += kLifBlock)
+    if (sh[i]) atomicAdd(&hc[i], sh[i]);
 }
 
 // ---------------------------------------------------------------------------
@@ -670,7 +718,8 @@ __global__ __launch_bounds__(1024) void k_topn_threshold(const uint32_t *__restr
   const int t = threadIdx.x;
   // thread t owns bins [4095-4t-3, 4095-4t] i.e. counting from the top
   unsigned long long loc = 0;
-  for (int j = 0; j < 4; ++j) loc += hist[kHistBins - 1 - (4 * t + j)];
+  for (int j = 0; j < 4; ++j)
+    for (int c = 0; c < kHistCopies; ++c) loc += hist[c * kHistBins + kHistBins - 1 - (4 * t + j)];
   part[t] = loc;
   __syncthreads();
   // inclusive scan over threads (Hillis-Steele; 10 steps)
@@ -690,7 +739,8 @@ __global__ __launch_bounds__(1024) void k_topn_threshold(const uint32_t *__restr
     unsigned long long cum = before;
     for (int j = 0; j < 4; ++j) {
       int bin = kHistBins - 1 - (4 * t + j);
-      unsigned long long h = hist[bin];
+      unsigned long long h = 0;
+      for (int c = 0; c < kHistCopies; ++c) h += hist[c * kHistBins + bin];
       if (cum + h >= want) {
         st->T = (uint64_t)bin;
         st->n_above = cum;
@@ -935,9 +985,9 @@ hipError_t launch_lif_apply(const uint64_t *currents, float *v, uint32_t *r, uin
                             uint64_t pool, LifParams lp, const LifEntry *tbl, int tbl_n,
                             uint32_t *hist, uint64_t *stats, hipStream_t s) {
   if (!pool) return hipSuccess;
-  uint64_t per = (uint64_t)kBlock * kLifPerThread;
+  uint64_t per = (uint64_t)kLifBlock * kLifPerThread;
   unsigned g = (unsigned)((pool + per - 1) / per);
-  hipLaunchKernelGGL(k_lif_apply, dim3(g), dim3(kBlock), 0, s, currents, v, r, sc, pool, lp, tbl,
+  hipLaunchKernelGGL(k_lif_apply, dim3(g), dim3(kLifBlock), 0, s, currents, v, r, sc, pool, lp, tbl,
                      tbl_n, hist, (unsigned long long *)stats);
   return hipGetLastError();
 }

@@ -1,0 +1,101 @@
+"""CPU multi-process test (gloo, world_size 2) of the multi-GPU protocol in
+neurokmer_amd/dist.py: shard the records (with in-record splits + k-1 halo),
+accumulate per shard, all-reduce the u64 currents, LIF/top-N on the sum, and
+union the shards' distinct top-N k-mers.  The per-shard work is done by the C
+oracle here (no GPU); on the GPU box the same protocol drives the HIP path
+(bench.py, tests/test_gpu_parity.py::test_split_phase_two_shards_equals_whole).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from neurokmer_amd import dist as nkdist
+from neurokmer_amd import synth
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, k, pool, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import cbind
+        bases, offs = synth.make_records(90_000, 3, seed=7, repeats_per_mb=30000, motif_len=50,
+                                         n_rate=0.002)
+        lo, hi, soffs = nkdist.shard_records(offs, world, k)[rank]
+        shard = bases[lo:hi]
+        ctr = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, True)
+        ctr.process_parallel_arrays(shard, soffs, 1)
+        cur = torch.from_numpy(ctr.currents().view(np.int64).copy())
+        nkdist.allreduce_currents_(cur)
+        # identical LIF + top-N on every rank: reuse the oracle on the summed
+        # currents by comparing against a whole-input run below
+        whole = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, True)
+        whole.process_parallel_arrays(bases, offs, 1)
+        ok_cur = np.array_equal(cur.numpy().view(np.uint64), whole.currents())
+        top = whole.top_abundant_neurons(20)
+        top_idx = {t[0] for t in top}
+        # this shard's distinct keys of the top neurons
+        mine = set()
+        for i in range(soffs.size - 1):
+            rec = shard[int(soffs[i]):int(soffs[i + 1])].tobytes()
+            for key in cbind.kmer_keys(rec, k, True):
+                if int(cbind.lib().nko_map_kmer(int(key), pool)) in top_idx:
+                    mine.add(int(key))
+        t = torch.tensor(sorted(mine), dtype=torch.int64)
+        allk = nkdist.gather_union(t)
+        per = {}
+        for key in set(allk.tolist()):
+            n = int(cbind.lib().nko_map_kmer(key & (2**64 - 1), pool))
+            per[n] = per.get(n, 0) + 1
+        ok_uniq = all(per.get(i, 0) == u for i, _, u in top)
+        q.put((rank, ok_cur, ok_uniq, int(hi - lo)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("k,pool", [(21, 5003), (31, 777)])
+def test_gloo_two_ranks_match_whole_input(k, pool):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, k, pool, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok_cur, ok_uniq, nbytes in res:
+        assert ok_cur, f"rank {rank}: all-reduced currents differ from the whole input"
+        assert ok_uniq, f"rank {rank}: union of shard top k-mers differs"
+        assert nbytes > 0
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("k", [5, 31, 40])
+def test_shard_records_cover_every_window_once(world, k):
+    from oracle import cbind
+    bases, offs = synth.make_records(20_000, 3, seed=world * 100 + k, n_rate=0.01)
+    want = []
+    for i in range(offs.size - 1):
+        want += [int(x) for x in cbind.kmer_keys(bases[int(offs[i]):int(offs[i + 1])].tobytes(),
+                                                 k, False)]
+    got = []
+    for lo, hi, so in nkdist.shard_records(offs, world, k):
+        sh = bases[lo:hi]
+        for i in range(so.size - 1):
+            got += [int(x) for x in cbind.kmer_keys(sh[int(so[i]):int(so[i + 1])].tobytes(), k,
+                                                    False)]
+    assert sorted(got) == sorted(want)

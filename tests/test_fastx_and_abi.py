@@ -1,0 +1,127 @@
+"""CPU tests of the host side: the FASTA/FASTQ reader (native, via the
+fastx_dump harness, and the Python mirror) and the C ABI library (loads,
+exports every symbol include/neurokmer.h declares, fails loudly without a GPU).
+"""
+import gzip
+import json
+import os
+import re
+import subprocess
+
+import pytest
+
+from neurokmer_amd import _lib, synth
+from neurokmer_amd.fastx import stream_sequences
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DUMP = os.path.join(ROOT, "neurokmer_amd", "bin", "fastx_dump")
+
+
+def native(path, batch=1 << 20):
+    out = subprocess.run([DUMP, str(path), str(batch)], capture_output=True, check=True).stdout
+    d = json.loads(out)
+    return d["rc"], [bytes.fromhex(h) for h in d["records"]], d["truncated"]
+
+
+def both(path, batch=1 << 20):
+    rc, recs, _ = native(path, batch)
+    assert rc == 0
+    py = list(stream_sequences(str(path)))
+    assert recs == py
+    return recs
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _built():
+    if not os.path.exists(DUMP):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "neurokmer_amd", "csrc"),
+                        os.path.join("..", "bin", "fastx_dump")], check=True)
+
+
+def test_fasta_multiline_crlf_blank(tmp_path):
+    p = tmp_path / "a.fa"
+    p.write_bytes(b">r1 desc\nACGT\r\nNNac\n\n>r2\n>r3\nTTTT\nG")
+    assert both(p) == [b"ACGTNNac", b"", b"TTTTG"]
+
+
+@pytest.mark.parametrize("batch", [1, 7, 1 << 20])
+def test_fasta_synthetic_roundtrip(tmp_path, batch):
+    bases, offs = synth.make_records(50_000, 9, n_rate=0.01, mixed_case=True)
+    p = tmp_path / "s.fa"
+    synth.write_fasta(str(p), bases, offs, width=61)
+    assert both(p, batch) == synth.records_list(bases, offs)
+
+
+def test_fastq_and_gzip(tmp_path):
+    bases, offs = synth.make_reads(300, 150, seed=3)
+    p = tmp_path / "r.fq"
+    synth.write_fastq(str(p), bases, offs)
+    assert both(p) == synth.records_list(bases, offs)
+    gz = tmp_path / "r.fq.gz"
+    gz.write_bytes(gzip.compress(p.read_bytes()))
+    assert both(gz) == synth.records_list(bases, offs)
+
+
+def test_fastq_stops_at_first_malformed_record(tmp_path):
+    # src/utils.rs:16-20: a parse error ends the stream; earlier records are kept
+    p = tmp_path / "bad.fq"
+    p.write_bytes(b"@a\nACGT\n+\nIIII\n@b\nACG\n+\nII\n@c\nTTTT\n+\nIIII\n")
+    rc, recs, truncated = native(p)
+    assert rc == 0 and recs == [b"ACGT"] and truncated
+    assert list(stream_sequences(str(p))) == [b"ACGT"]
+
+
+def test_empty_and_unknown_format_are_errors(tmp_path):
+    e = tmp_path / "empty.fa"
+    e.write_bytes(b"")
+    assert native(e)[0] == _lib.NK_E_PARSE
+    with pytest.raises(ValueError):
+        stream_sequences(str(e))
+    u = tmp_path / "u.txt"
+    u.write_bytes(b"ACGT\n")
+    assert native(u)[0] == _lib.NK_E_PARSE
+    with pytest.raises(ValueError):
+        stream_sequences(str(u))
+    assert native(tmp_path / "missing.fa")[0] == _lib.NK_E_IO
+
+
+def header_functions():
+    text = open(os.path.join(ROOT, "include", "neurokmer.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(nk_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol():
+    L = _lib.load(share_torch=False)
+    names = header_functions()
+    assert len(names) >= 25
+    assert sorted(_lib.EXPORTS) == names
+    for n in names:
+        assert hasattr(L, n), n
+    nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                        text=True, check=True).stdout
+    for n in names:
+        assert re.search(rf"\bT {n}$", nm, re.M), n
+
+
+def test_no_cpu_fallback_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from neurokmer_amd import SpikingKmerCounter
+    with pytest.raises(_lib.NeuroKmerError) as e:
+        SpikingKmerCounter(31, 1.0, 0.95, 2, 1.0, 1000, True)
+    assert e.value.code == _lib.NK_E_NO_DEVICE
+    assert "no CPU fallback" in str(e.value)
+    L = _lib.load()
+    assert L.nk_version().decode().startswith("neurokmer-mi355x")
+
+
+def test_cli_rejects_bad_usage():
+    cli = _lib.CLI_PATH
+    r = subprocess.run([cli], capture_output=True, text=True)
+    assert r.returncode == 2 and "--input" in r.stderr
+    r = subprocess.run([cli, "--help"], capture_output=True, text=True)
+    assert r.returncode == 0 and "--pool-size" in r.stderr
+    r = subprocess.run([cli, "-i", "x.fa", "-k", "abc"], capture_output=True, text=True)
+    assert r.returncode == 2

@@ -1,6 +1,7 @@
 #!/bin/bash
-# One GPU session: parity tests, then a short bench.  Stops at the first
-# fault / abort / timeout (exit codes other than 0 and 1 from pytest).
+# One GPU session: parity tests, then a short bench (+ optional 2-rank rehearsal
+# on the single GPU with gloo).  Stops at the first fault / abort / timeout
+# (exit codes other than 0 and 1 from pytest).
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -13,4 +14,13 @@ timeout -k 10 600 python bench.py --steps ${STEPS:-5} --warmup 2 > gpurun_out/be
 rc=$?
 echo "bench rc=$rc"
 tail -5 gpurun_out/bench.log
+[ $rc -ne 0 ] && exit $rc
+if [ -n "${DIST2:-}" ]; then
+  timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --bases 30000000 --dist-backend gloo \
+    --same-device --no-cpu-baseline > gpurun_out/bench_dist2.log 2>&1
+  rc=$?
+  echo "dist2 rc=$rc"
+  tail -3 gpurun_out/bench_dist2.log
+fi
 exit $rc
