@@ -48,7 +48,11 @@ typedef struct nk_opts {
   int32_t kmer_width;    /* NK_KMER_COMPAT */
   uint32_t top_n;        /* neurons whose "unique k-mers colliding" are tracked
                             by every process call (default 20 = src/main.rs:50) */
-  uint32_t reserved[13];
+  uint32_t stage_timing; /* 0 (default): HIP events around the count kernel only
+                            (nk_last_timings: index, count, post, total);
+                            1: an event between every stage (each costs ~6 us
+                            of GPU idle time on MI355X) */
+  uint32_t reserved[12];
 } nk_opts;
 
 /* Fills *o with the defaults above. */

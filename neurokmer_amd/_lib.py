@@ -38,7 +38,7 @@ EXPORTS = (
 
 class NkOpts(C.Structure):
     _fields_ = [("device", C.c_int32), ("kmer_width", C.c_int32), ("top_n", C.c_uint32),
-                ("reserved", C.c_uint32 * 13)]
+                ("stage_timing", C.c_uint32), ("reserved", C.c_uint32 * 12)]
 
 
 class NkTopRow(C.Structure):

@@ -50,12 +50,13 @@ class EnergyTracker:
 class SpikingKmerCounter:
     def __init__(self, k: int, threshold: float, leak: float, refractory: int,
                  spike_cost: float, pool_size: int, use_canonical: bool, *,
-                 device: int = 0, top_n: int = 20):
+                 device: int = 0, top_n: int = 20, stage_timing: bool = False):
         self._L = _lib.load()
         o = NkOpts()
         self._L.nk_opts_default(C.byref(o))
         o.device = device
         o.top_n = top_n
+        o.stage_timing = 1 if stage_timing else 0
         self._h = None
         h = self._L.nk_new(k, threshold, leak, refractory, spike_cost, pool_size,
                            1 if use_canonical else 0, C.byref(o))

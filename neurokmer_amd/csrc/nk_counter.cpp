@@ -67,6 +67,10 @@ struct DevBuf {
 constexpr int kLifTable = 1 << 16;
 constexpr int kStages = 7;
 const char *kStageNames[kStages] = {"index", "count", "hist", "lif", "topn", "uniques", "total"};
+// default (opts.stage_timing == 0): events only around the count kernel and at
+// both ends; an event between two kernels idles the GPU for ~6 us on MI355X
+constexpr int kStagesLight = 4;
+const char *kStageNamesLight[kStagesLight] = {"index", "count", "post", "total"};
 
 }  // namespace
 
@@ -104,8 +108,8 @@ struct nk_counter {
   DevBuf<uint32_t> post_flags;  // [0] set too small [1] top bucket overflowed [2] top buckets
   // packed finalize results: ResultHdr | cand[m] | uniq[m]
   static constexpr size_t kResBytes = sizeof(ResultHdr) + kMaxTopN * (sizeof(TopCand) + 4);
-  DevBuf<uint8_t> res_d;
-  uint8_t *res_h = nullptr;  // pinned
+  uint8_t *res_h = nullptr;   // pinned, mapped: written by k_gather
+  uint8_t *res_hd = nullptr;  // its device-side address
   // host copies of input (host-array entry points)
   DevBuf<uint8_t> in_bases;
   DevBuf<uint64_t> in_offs;
@@ -118,6 +122,13 @@ struct nk_counter {
   DevBuf<uint2> p_desc;
   DevBuf<uint32_t> p_over, partials, tbuckets;
   PartArgs last_pa{};
+  uint32_t pend_slices = 0;  // K1b partials not yet folded into cur (fused into LIF)
+  bool lif_zeroed = false;   // hist/stats already zeroed by this call's prep kernel
+  bool state_fresh = true;   // spikes/v/r are logically zero (lazy reset)
+  bool cur_fresh = true;     // currents are logically zero (lazy reset)
+  // top-N selection fused into the LIF kernel (TopFuse)
+  DevBuf<TopCand> bcand;
+  DevBuf<uint32_t> bcnt;
   bool part_used = false;
   // input of the last accumulate (for the uniques pass)
   KmerInput last_in{};
@@ -133,6 +144,13 @@ struct nk_counter {
   int n_stage = 0;
 };
 
+// ev[i] for the stage timings; the inner stage boundaries only in full mode
+static hipError_t mark(nk_counter *c, int i, hipStream_t s) {
+  if (c->opts.stage_timing || i == 0 || i == 1 || i == 2 || i == 6 || i == 7)
+    return hipEventRecord(c->ev[i], s);
+  return hipSuccess;
+}
+
 static uint64_t cost_fixed(double cost) {  // Rust `(cost * 1000.0) as u64`
   double x = cost * 1000.0;
   if (!(x > 0.0)) return 0;
@@ -144,18 +162,33 @@ static hipStream_t pick_stream(nk_counter *c, void *s) {
   return s ? (hipStream_t)s : c->own_stream;
 }
 
-static int zero_state_on(nk_counter *c, hipStream_t s) {
+// Reset is lazy: the neuron state (spikes, v, r) and the currents are only
+// marked fresh.  The next LIF takes fresh state as zero without reading it and
+// writes every neuron; the next accumulate zeroes the currents in its prep
+// kernel; the copy-out / pointer entry points materialise zeros on demand.
+static int zero_state_on(nk_counter *c, hipStream_t) {
   c->total_spikes = c->total_energy = 0;
   c->top_valid = false;
   c->have_input = false;
-  if (!c->pool) return NK_OK;
+  c->state_fresh = true;
+  c->cur_fresh = true;
+  return NK_OK;
+}
+
+// materialise the lazily-zero buffers (what != 0: currents; what == 0: state)
+static int materialize(nk_counter *c, bool currents, hipStream_t s) {
   ZeroList z{};
-  z.ptr[0] = c->cur.p; z.bytes[0] = c->pool * 8;
-  z.ptr[1] = c->sc.p;  z.bytes[1] = c->pool * 8;
-  z.ptr[2] = c->v.p;   z.bytes[2] = c->pool * 4;
-  z.ptr[3] = c->r.p;   z.bytes[3] = c->pool * 4;
-  z.n = 4;
-  HIPCHK(launch_zero(z, s));
+  if (currents && c->cur_fresh) {
+    z.ptr[z.n] = c->cur.p; z.bytes[z.n++] = c->pool * 8;
+    c->cur_fresh = false;
+  }
+  if (!currents && c->state_fresh) {
+    z.ptr[z.n] = c->sc.p; z.bytes[z.n++] = c->pool * 8;
+    z.ptr[z.n] = c->v.p;  z.bytes[z.n++] = c->pool * 4;
+    z.ptr[z.n] = c->r.p;  z.bytes[z.n++] = c->pool * 4;
+    c->state_fresh = false;
+  }
+  if (z.n && c->pool) HIPCHK(launch_zero(z, s));
   return NK_OK;
 }
 
@@ -175,6 +208,8 @@ static int copy_out(nk_counter *c, const DevBuf<T> &b, T *out, size_t n) {
   if (n != c->pool) return fail(NK_E_INVALID, "n (%zu) must equal pool_size (%zu)", n, c->pool);
   if (!n) return NK_OK;
   (void)hipSetDevice(c->device);
+  int rc = materialize(c, (const void *)&b == (const void *)&c->cur, c->own_stream);
+  if (rc) return rc;
   HIPCHK(hipStreamSynchronize(c->own_stream));
   HIPCHK(hipMemcpy(out, b.p, n * sizeof(T), hipMemcpyDeviceToHost));
   return NK_OK;
@@ -249,8 +284,9 @@ nk_counter *nk_new(size_t k, float threshold, float leak, uint32_t refractory, d
        !c->top_keys_n.ensure(1) && !c->radix_h.ensure(256) && !c->set_mask_d.ensure(1) &&
        !c->set_need_d.ensure(1) && !c->post_flags.ensure(4) && !c->set_keys.ensure(1 << 20) &&
        !c->hits.ensure(1 << 19) && !c->n_hits.ensure(1) &&
-       !c->res_d.ensure(nk_counter::kResBytes) &&
-       hipHostMalloc((void **)&c->res_h, nk_counter::kResBytes) == hipSuccess;
+       hipHostMalloc((void **)&c->res_h, nk_counter::kResBytes,
+                     hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+       hipHostGetDevicePointer((void **)&c->res_hd, c->res_h, 0) == hipSuccess;
   c->set_alloc = 1 << 20;
   if (!ok || zero_state(c) != NK_OK) {
     std::string e = g_err.empty() ? "device allocation failed" : g_err;
@@ -268,12 +304,12 @@ void nk_free(nk_counter *c) {
   c->cur.release(); c->sc.release(); c->v.release(); c->r.release();
   c->p_off.release(); c->p_pos.release(); c->p_fill.release(); c->p_desc.release();
   c->p_over.release(); c->partials.release(); c->tbuckets.release();
+  c->bcand.release(); c->bcnt.release();
   c->tile_rec.release(); c->hist.release(); c->tie_cnt.release(); c->uniq.release();
   c->special.release(); c->stats.release(); c->lif_tbl.release(); c->topst.release();
   c->cand.release(); c->top_cur.release(); c->set_keys.release(); c->top_keys.release();
   c->top_keys_n.release(); c->radix_h.release(); c->set_mask_d.release();
   c->set_need_d.release(); c->post_flags.release(); c->hits.release(); c->n_hits.release();
-  c->res_d.release();
   if (c->res_h) (void)hipHostFree(c->res_h); c->in_bases.release(); c->in_offs.release();
   for (int i = 0; i <= kStages; ++i)
     if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
@@ -296,8 +332,10 @@ int nk_reset_async(nk_counter *c, void *stream) {
 // ---------------------------------------------------------------------------
 // accumulate: currents = histogram of H(kmer) % pool over this input
 // ---------------------------------------------------------------------------
-int nk_accumulate_device(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_offs,
-                         size_t n_recs, size_t n_bases, void *stream) {
+// defer_partials: leave K1c (currents += partials) to the LIF kernel of the
+// same process call instead of a separate pass
+static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_offs,
+                      size_t n_recs, size_t n_bases, void *stream, bool defer_partials) {
   if (!c) return fail(NK_E_INVALID, "null counter");
   if (n_bases && ((uintptr_t)d_bases & 15))
     return fail(NK_E_INVALID, "device bases must be 16-byte aligned");
@@ -318,22 +356,24 @@ int nk_accumulate_device(nk_counter *c, const uint8_t *d_bases, const uint64_t *
   int rc = c->tile_rec.ensure(std::max<uint64_t>(in.n_tiles, 1));
   if (rc) return rc;
   in.tile_rec = c->tile_rec.p;
-  HIPCHK(hipEventRecord(c->ev[0], s));
-  HIPCHK(launch_tile_rec(in, tile, c->tile_rec.p, s));
-  HIPCHK(hipEventRecord(c->ev[1], s));
   c->part_used = part && in.n_tiles > 0;
+  // one prep kernel: tile -> first record index, and every buffer the count
+  // (and, for a process call, the LIF) accumulates into zeroed
+  ZeroList z{};
+  z.ptr[z.n] = c->cur.p; z.bytes[z.n++] = c->pool * 8;
+  PartArgs pa{};
+  uint32_t slices = 0;
   if (c->part_used) {
     // bucket regions: 1.25x the fair share + one tile of slack (overflow is
     // still exact: the excess is counted with direct atomics)
     uint64_t cap = n_bases / B * 5 / 4 + kPartTile;
     cap = (cap + 63) & ~63ull;
     // one round of 1-per-CU workgroups (128 KiB LDS each) on 256 CUs
-    const uint32_t slices = (uint32_t)std::max<uint64_t>(1, 256 / B);
+    slices = (uint32_t)std::max<uint64_t>(1, 256 / B);
     if ((rc = c->p_off.ensure(B * cap)) || (rc = c->p_pos.ensure(B * cap)) ||
         (rc = c->p_fill.ensure(B)) || (rc = c->p_desc.ensure(B * in.n_tiles)) ||
         (rc = c->p_over.ensure(B)) || (rc = c->partials.ensure(slices * c->pool)))
       return rc;
-    PartArgs pa{};
     pa.n_buckets = (uint32_t)B;
     pa.cap = cap;
     pa.off = c->p_off.p;
@@ -343,27 +383,41 @@ int nk_accumulate_device(nk_counter *c, const uint8_t *d_bases, const uint64_t *
     pa.max_segs = in.n_tiles;
     pa.overflow = c->p_over.p;
     pa.currents = (unsigned long long *)c->cur.p;
-    ZeroList z{};
-    z.ptr[0] = c->cur.p;    z.bytes[0] = c->pool * 8;
-    z.ptr[1] = c->p_fill.p; z.bytes[1] = B * 8;
-    z.ptr[2] = c->p_over.p; z.bytes[2] = B * 4;
-    z.n = 3;
-    HIPCHK(launch_zero(z, s));
+    z.ptr[z.n] = c->p_fill.p; z.bytes[z.n++] = B * 8;
+    z.ptr[z.n] = c->p_over.p; z.bytes[z.n++] = B * 4;
+  }
+  if (defer_partials) {  // the LIF of this process call accumulates into these
+    z.ptr[z.n] = c->hist.p;  z.bytes[z.n++] = kHistBins * kHistCopies * 4;
+    z.ptr[z.n] = c->stats.p; z.bytes[z.n++] = 16;
+    c->lif_zeroed = true;
+  }
+  HIPCHK(mark(c, 0, s));
+  HIPCHK(launch_prep(in, tile, c->tile_rec.p, z, s));
+  c->cur_fresh = false;
+  HIPCHK(mark(c, 1, s));
+  if (c->part_used) {
     HIPCHK(launch_part(in, (int)c->k, c->canonical, c->pool, pa, s));
-    HIPCHK(hipEventRecord(c->ev[2], s));
+    HIPCHK(mark(c, 2, s));
     HIPCHK(launch_bucket_hist(pa, c->pool, slices, c->partials.p, s));
-    HIPCHK(launch_partials_add(c->partials.p, slices, c->pool, c->cur.p, s));
+    if (defer_partials)
+      c->pend_slices = slices;
+    else
+      HIPCHK(launch_partials_add(c->partials.p, slices, c->pool, c->cur.p, s));
     c->last_pa = pa;
   } else {
-    if (c->pool) HIPCHK(hipMemsetAsync(c->cur.p, 0, c->pool * 8, s));
     HIPCHK(launch_count(in, (int)c->k, c->canonical, c->pool, c->cur.p, s));
-    HIPCHK(hipEventRecord(c->ev[2], s));
+    HIPCHK(mark(c, 2, s));
   }
-  HIPCHK(hipEventRecord(c->ev[3], s));
+  HIPCHK(mark(c, 3, s));
   c->last_in = in;
   c->have_input = true;
   c->top_valid = false;
   return NK_OK;
+}
+
+int nk_accumulate_device(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_offs,
+                         size_t n_recs, size_t n_bases, void *stream) {
+  return accumulate(c, d_bases, d_offs, n_recs, n_bases, stream, false);
 }
 
 // ---------------------------------------------------------------------------
@@ -399,7 +453,10 @@ static int refine_threshold(nk_counter *c, uint64_t want, uint64_t max_sc, TopSt
   return NK_OK;
 }
 
-static int enqueue_lif(nk_counter *c, int streaming, hipStream_t s) {
+// fuse_want > 0: the LIF kernel also selects the top rows and runs the
+// uniques post step (part: the partitioned count's records are used)
+static int enqueue_lif(nk_counter *c, int streaming, uint32_t fuse_want, bool part,
+                       hipStream_t s) {
   LifParams lp;
   lp.steps = c->steps;
   lp.thr = c->thr;
@@ -415,15 +472,37 @@ static int enqueue_lif(nk_counter *c, int streaming, hipStream_t s) {
     c->lif_key = lp;
     c->lif_valid = true;
   }
-  ZeroList z{};
-  z.ptr[0] = c->hist.p;  z.bytes[0] = kHistBins * kHistCopies * 4;
-  z.ptr[1] = c->stats.p; z.bytes[1] = 16;
-  z.n = 2;
-  HIPCHK(launch_zero(z, s));
+  if (!c->lif_zeroed) {
+    ZeroList z{};
+    z.ptr[0] = c->hist.p;  z.bytes[0] = kHistBins * kHistCopies * 4;
+    z.ptr[1] = c->stats.p; z.bytes[1] = 16;
+    z.n = 2;
+    HIPCHK(launch_zero(z, s));
+  }
+  TopFuse tf{};
+  if (fuse_want) {
+    const uint32_t nb = lif_blocks(c->pool);
+    if ((rc = c->bcand.ensure((uint64_t)nb * fuse_want)) || (rc = c->bcnt.ensure(nb)) ||
+        (rc = c->tbuckets.ensure(fuse_want)))
+      return rc;
+    tf.want = fuse_want;
+    tf.bcand = c->bcand.p;
+    tf.bcnt = c->bcnt.p;
+    tf.st = c->topst.p;
+    tf.cand = c->cand.p;
+    tf.top_cur = c->top_cur.p;
+    tf.post = PostArgs{c->set_alloc, part ? c->p_over.p : nullptr, part ? 1 : 0, c->set_mask_d.p,
+                       c->tbuckets.p, c->post_flags.p, c->uniq.p, c->special.p, c->n_hits.p};
+  }
+  c->lif_zeroed = false;
   // steps == 0: the kernel leaves every neuron as it is (streaming returns early,
   // src/spiking_hash.rs:549-551; in-memory runs zero iterations)
-  HIPCHK(launch_lif_apply(c->cur.p, c->v.p, c->r.p, c->sc.p, c->pool, lp, c->lif_tbl.p, kLifTable,
-                          c->hist.p, c->stats.p, s));
+  if ((rc = materialize(c, true, s))) return rc;  // finalize right after a reset
+  HIPCHK(launch_lif_apply(c->cur.p, c->partials.p, c->pend_slices, c->state_fresh ? 1 : 0, c->v.p,
+                          c->r.p, c->sc.p, c->pool, lp, c->lif_tbl.p, kLifTable, c->hist.p,
+                          c->stats.p, tf, s));
+  c->pend_slices = 0;
+  if (c->pool) c->state_fresh = false;
   return NK_OK;
 }
 
@@ -437,14 +516,15 @@ static int enqueue_select(nk_counter *c, uint64_t want, hipStream_t s) {
   return NK_OK;
 }
 
-static int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, hipStream_t s) {
+static int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, bool post_done,
+                           hipStream_t s) {
   const bool part = c->part_used && !rescan;
   int rc;
   if ((rc = c->tbuckets.ensure(m))) return rc;
-  HIPCHK(launch_top_post(c->cand.p, c->top_cur.p, m, c->set_alloc, part ? c->p_over.p : nullptr,
+  if (!post_done) HIPCHK(launch_top_post(c->cand.p, c->top_cur.p, m, c->set_alloc, part ? c->p_over.p : nullptr,
                          part ? 1 : 0, c->set_mask_d.p, c->tbuckets.p, c->post_flags.p, c->uniq.p,
                          c->special.p, c->n_hits.p, s));
-  HIPCHK(launch_set_fill(c->set_keys.p, c->set_mask_d.p, c->set_alloc, s));
+  if (!part) HIPCHK(launch_set_fill(c->set_keys.p, c->set_mask_d.p, c->set_alloc, s));
   UniqArgs u{};
   u.top = c->cand.p;
   u.n_top = m;
@@ -453,7 +533,7 @@ static int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, hipStream_t s
   u.set_mask = c->set_mask_d.p;
   u.uniq = c->uniq.p;
   u.special = c->special.p;
-  if (part) {
+  if (part) {  // the scan kernel also empties the set
     const uint32_t slices = std::max<uint32_t>(1, 512 / m);
     HIPCHK(launch_part_uniques(c->last_in, (int)c->k, c->canonical, c->last_pa, u, c->tbuckets.p,
                                c->post_flags.p + 2, m, slices, c->hits.p, c->n_hits.p, c->hits.n,
@@ -472,9 +552,7 @@ static int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, hipStream_t s
 static int enqueue_readback(nk_counter *c, uint32_t m, bool uniq, hipStream_t s) {
   HIPCHK(launch_gather(c->topst.p, c->stats.p, uniq ? c->set_mask_d.p : nullptr,
                        uniq ? c->post_flags.p : nullptr, c->cand.p, uniq ? c->uniq.p : nullptr, m,
-                       c->res_d.p, s));
-  const size_t bytes = sizeof(ResultHdr) + (size_t)m * (sizeof(TopCand) + 4);
-  HIPCHK(hipMemcpyAsync(c->res_h, c->res_d.p, bytes, hipMemcpyDeviceToHost, s));
+                       c->res_hd, s));  // straight into pinned host memory: no copy
   return NK_OK;
 }
 
@@ -483,18 +561,21 @@ static int enqueue_readback(nk_counter *c, uint32_t m, bool uniq, hipStream_t s)
 // small for the top rows, an overflowed top bucket) are redone after it.
 static int lif_top_uniques(nk_counter *c, int streaming, hipStream_t s) {
   int rc;
-  if ((rc = enqueue_lif(c, streaming, s))) return rc;
-  HIPCHK(hipEventRecord(c->ev[4], s));
   const uint64_t want = std::min<uint64_t>(c->opts.top_n, c->pool);
   const bool uniq = want && c->have_input && c->last_in.n_tiles;
-  if (want) {
+  // top-N selection (and the uniques post step) inside the LIF kernel
+  const bool fused = want && want <= kFuseMaxTopN && lif_blocks(c->pool) <= kFuseMaxBlocks;
+  if ((rc = enqueue_lif(c, streaming, fused ? (uint32_t)want : 0u, uniq && c->part_used, s)))
+    return rc;
+  HIPCHK(mark(c, 4, s));
+  if (want && !fused) {
     HIPCHK(launch_topn_threshold(c->hist.p, want, c->pool, c->topst.p, s));
     if ((rc = enqueue_select(c, want, s))) return rc;
   }
-  HIPCHK(hipEventRecord(c->ev[5], s));
-  if (uniq && (rc = enqueue_uniques(c, (uint32_t)want, false, s))) return rc;
+  HIPCHK(mark(c, 5, s));
+  if (uniq && (rc = enqueue_uniques(c, (uint32_t)want, false, fused, s))) return rc;
   if ((rc = enqueue_readback(c, (uint32_t)want, uniq, s))) return rc;
-  HIPCHK(hipEventRecord(c->ev[6], s));
+  HIPCHK(mark(c, 6, s));
   HIPCHK(hipStreamSynchronize(s));
   const ResultHdr *h = reinterpret_cast<const ResultHdr *>(c->res_h);
   const TopCand *hc = reinterpret_cast<const TopCand *>(c->res_h + sizeof(ResultHdr));
@@ -507,7 +588,7 @@ static int lif_top_uniques(nk_counter *c, int streaming, hipStream_t s) {
     if ((rc = refine_threshold(c, want, h->stats[1], st, s))) return rc;
     HIPCHK(hipMemcpyAsync(c->topst.p, &st, sizeof st, hipMemcpyHostToDevice, s));
     if ((rc = enqueue_select(c, want, s))) return rc;
-    if (uniq && (rc = enqueue_uniques(c, (uint32_t)want, false, s))) return rc;
+    if (uniq && (rc = enqueue_uniques(c, (uint32_t)want, false, false, s))) return rc;
     if ((rc = enqueue_readback(c, (uint32_t)want, uniq, s))) return rc;
     HIPCHK(hipStreamSynchronize(s));
   }
@@ -526,7 +607,7 @@ static int lif_top_uniques(nk_counter *c, int streaming, hipStream_t s) {
       c->set_alloc = cap;
     }
     if (h->flags[0] || h->flags[1]) {
-      if ((rc = enqueue_uniques(c, (uint32_t)want, h->flags[1] != 0, s))) return rc;
+      if ((rc = enqueue_uniques(c, (uint32_t)want, h->flags[1] != 0, false, s))) return rc;
       if ((rc = enqueue_readback(c, (uint32_t)want, uniq, s))) return rc;
       HIPCHK(hipStreamSynchronize(s));
     }
@@ -552,6 +633,14 @@ static void collect_timings(nk_counter *c, bool with_count) {
     float ms = 0;
     return hipEventElapsedTime(&ms, a, b) == hipSuccess ? ms : 0.0f;
   };
+  if (!c->opts.stage_timing) {
+    c->stage_ms[0] = with_count ? el(c->ev[0], c->ev[1]) : 0.0f;
+    c->stage_ms[1] = with_count ? el(c->ev[1], c->ev[2]) : 0.0f;
+    c->stage_ms[2] = el(with_count ? c->ev[2] : c->ev[7], c->ev[6]);
+    c->stage_ms[3] = el(with_count ? c->ev[0] : c->ev[7], c->ev[6]);
+    c->n_stage = kStagesLight;
+    return;
+  }
   c->stage_ms[0] = with_count ? el(c->ev[0], c->ev[1]) : 0.0f;
   c->stage_ms[1] = with_count ? el(c->ev[1], c->ev[2]) : 0.0f;
   c->stage_ms[2] = with_count ? el(c->ev[2], c->ev[3]) : 0.0f;
@@ -566,7 +655,7 @@ int nk_finalize(nk_counter *c, int streaming, void *stream) {
   if (!c) return fail(NK_E_INVALID, "null counter");
   (void)hipSetDevice(c->device);
   hipStream_t s = pick_stream(c, stream);
-  HIPCHK(hipEventRecord(c->ev[7], s));
+  HIPCHK(mark(c, 7, s));
   int rc = lif_top_uniques(c, streaming, s);
   if (rc) return rc;
   c->top_valid = true;
@@ -577,8 +666,12 @@ int nk_finalize(nk_counter *c, int streaming, void *stream) {
 
 static int process_device(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_offs,
                           size_t n_recs, size_t n_bases, void *stream, int streaming) {
-  int rc = nk_accumulate_device(c, d_bases, d_offs, n_recs, n_bases, stream);
-  if (rc) return rc;
+  int rc = accumulate(c, d_bases, d_offs, n_recs, n_bases, stream, true);
+  if (rc) {
+    c->pend_slices = 0;
+    c->lif_zeroed = false;
+    return rc;
+  }
   hipStream_t s = pick_stream(c, stream);
   if ((rc = lif_top_uniques(c, streaming, s))) return rc;
   c->top_valid = true;
@@ -734,7 +827,16 @@ uint64_t nk_get_steps(const nk_counter *c) { return c ? c->steps : 0; }
 size_t nk_pool_size(const nk_counter *c) { return c ? c->pool : 0; }
 size_t nk_k(const nk_counter *c) { return c ? c->k : 0; }
 int nk_use_canonical(const nk_counter *c) { return c ? c->canonical : 0; }
-uint64_t *nk_device_currents(nk_counter *c) { return c ? c->cur.p : nullptr; }
+uint64_t *nk_device_currents(nk_counter *c) {
+  if (!c) return nullptr;
+  if (c->cur_fresh) {  // lazily-reset currents: zero them before handing them out
+    (void)hipSetDevice(c->device);
+    if (materialize(c, true, c->own_stream) ||
+        hipStreamSynchronize(c->own_stream) != hipSuccess)
+      return nullptr;
+  }
+  return c->cur.p;
+}
 
 int nk_copy_currents(nk_counter *c, uint64_t *out, size_t n) { return copy_out(c, c->cur, out, n); }
 int nk_copy_spike_counts(nk_counter *c, uint64_t *out, size_t n) {
@@ -749,7 +851,7 @@ int nk_last_timings(const nk_counter *c, const char **names, float *ms, int cap)
   if (!c) return 0;
   int n = std::min(cap, c->n_stage);
   for (int i = 0; i < n; ++i) {
-    if (names) names[i] = kStageNames[i];
+    if (names) names[i] = c->opts.stage_timing ? kStageNames[i] : kStageNamesLight[i];
     if (ms) ms[i] = c->stage_ms[i];
   }
   return n;

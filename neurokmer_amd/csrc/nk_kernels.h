@@ -46,6 +46,35 @@ struct TopCand {
   uint64_t sc;
 };
 
+// What k_top_post derives from the final top rows (set sizing for uniques).
+struct PostArgs {
+  uint64_t set_alloc;
+  const uint32_t *overflow;  // per bucket (partitioned count) or null
+  int part;
+  uint64_t *set_mask;
+  uint32_t *tbuckets;
+  uint32_t *flags;
+  uint32_t *uniq;
+  uint32_t *special;
+  unsigned long long *n_hits;
+};
+
+// Top-N selection fused into the LIF kernel (want <= kFuseMaxTopN): every LIF
+// block keeps its own top `want` rows by (spikes desc, index asc) -- a superset
+// of its share of the global top rows -- and one small kernel after it selects,
+// sorts and post-processes the global rows.
+constexpr uint32_t kFuseMaxTopN = 64;
+constexpr uint32_t kFuseMaxBlocks = 1024;
+struct TopFuse {
+  uint32_t want;      // 0: not fused
+  TopCand *bcand;     // [blocks * want]
+  uint32_t *bcnt;     // [blocks]
+  TopState *st;
+  TopCand *cand;      // final rows, sorted
+  uint64_t *top_cur;  // currents of the final rows
+  PostArgs post;
+};
+
 constexpr int kZeroMax = 8;
 struct ZeroList {
   void *ptr[kZeroMax];
@@ -99,9 +128,14 @@ hipError_t launch_count(const KmerInput &in, int k, int canonical, uint64_t pool
 hipError_t launch_uniques(const KmerInput &in, int k, int canonical, uint64_t pool,
                           const UniqArgs &u, hipStream_t s);
 hipError_t launch_lif_table(LifEntry *tbl, int n, LifParams lp, hipStream_t s);
-hipError_t launch_lif_apply(const uint64_t *currents, float *v, uint32_t *r, uint64_t *sc,
-                            uint64_t pool, LifParams lp, const LifEntry *tbl, int tbl_n,
-                            uint32_t *hist, uint64_t *stats, hipStream_t s);
+// partials/slices: when slices > 0, currents[i] += sum of the K1b partials
+// first (the fused K1c of a single-device process call) and is written back.
+// fresh: v/r/sc are taken as 0 (lazy reset) and every neuron is written.
+hipError_t launch_lif_apply(uint64_t *currents, const uint32_t *partials, uint32_t slices,
+                            int fresh, float *v, uint32_t *r, uint64_t *sc, uint64_t pool, LifParams lp,
+                            const LifEntry *tbl, int tbl_n, uint32_t *hist, uint64_t *stats,
+                            const TopFuse &tf, hipStream_t s);
+uint32_t lif_blocks(uint64_t pool);  // grid size of the LIF kernel
 hipError_t launch_topn_threshold(const uint32_t *hist, uint64_t n, uint64_t pool, TopState *st,
                                  hipStream_t s);
 hipError_t launch_radix_hist(const uint64_t *sc, uint64_t pool, int shift, uint64_t prefix,
@@ -120,6 +154,9 @@ hipError_t launch_top_post(const TopCand *top, const uint64_t *top_cur, uint32_t
                            uint32_t *uniq, uint32_t *special, unsigned long long *n_hits,
                            hipStream_t s);
 hipError_t launch_set_word(uint64_t *w, uint64_t v, hipStream_t s);
+// tile -> first record index for the count kernels, fused with a zero list
+hipError_t launch_prep(const KmerInput &in, uint64_t tile_size, uint32_t *tile_rec,
+                       const ZeroList &z, hipStream_t s);
 hipError_t launch_zero(const ZeroList &z, hipStream_t s);
 hipError_t launch_gather(const TopState *st, const uint64_t *stats, const uint64_t *mask,
                          const uint32_t *flags, const TopCand *cand, const uint32_t *uniq,
@@ -136,6 +173,7 @@ hipError_t launch_bucket_hist(const PartArgs &pa, uint64_t pool, uint32_t slices
                               uint32_t *partials, hipStream_t s);
 hipError_t launch_partials_add(const uint32_t *partials, uint32_t slices, uint64_t pool,
                                uint64_t *currents, hipStream_t s);
+// (also empties the uniques hash set u.set_keys[0 .. *u.set_mask])
 hipError_t launch_part_uniques(const KmerInput &in, int k, int canonical, const PartArgs &pa,
                                const UniqArgs &u, const uint32_t *tbuckets, const uint32_t *n_tb,
                                uint32_t max_tb, uint32_t slices, unsigned long long *hits,

@@ -236,7 +236,8 @@ __global__ __launch_bounds__(kBlock) void k_kmers_compat(KmerInput in, int k, Fa
 //                  tile's (bin offset u16, tile position u16) records by bucket
 //                  (bucket = neuron >> 15) in LDS, reserve room in each bucket's
 //                  HBM array with ONE atomic per (tile, bucket), and write the
-//                  segments out coalesced.
+//                  segments out as 16-B stores: each segment is padded to a
+//                  multiple of 8 records with the sentinel bin kPadOff.
 //   K1b k_bucket_hist  one workgroup per (bucket, slice): 32768-bin u32
 //                  histogram in LDS over a contiguous slice of the bucket's
 //                  records, written once as a partial.
@@ -245,6 +246,10 @@ __global__ __launch_bounds__(kBlock) void k_kmers_compat(KmerInput in, int k, Fa
 // instead of re-hashing the input.
 // ---------------------------------------------------------------------------
 constexpr int kPartPerThread = kPartTile / kPartBlock;  // 16
+constexpr uint32_t kPadOff = 0xFFFFu;                    // sentinel bin of a pad record
+constexpr int kSortSlots = kPartTile + 7 * kMaxBuckets;  // records + worst-case padding
+constexpr int kGroups = kSortSlots / 8;                  // 8-record store groups
+constexpr int kGroupIters = (kGroups + kPartBlock - 1) / kPartBlock;
 
 template <bool CANON>
 __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMod fm, PartArgs pa) {
@@ -253,7 +258,8 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
   __shared__ uint32_t s_start[kMaxBuckets + 1];
   __shared__ uint32_t s_base[kMaxBuckets];
   __shared__ uint32_t s_fit[kMaxBuckets];
-  __shared__ uint32_t s_sorted[kPartTile];
+  __shared__ __align__(16) uint32_t s_sorted[kSortSlots];
+  __shared__ uint8_t s_gmap[kGroups];  // store group -> bucket
 
   const int tid = threadIdx.x;
   const uint64_t tile = blockIdx.x;
@@ -328,13 +334,15 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
     O[j] = idx & (kBinsPerBucket - 1);
   }
   __syncthreads();
-  // exclusive scan of the bucket counts (one wave) + HBM reservation (one
-  // atomic per non-empty bucket: entries in the low 40 bits, segments above)
+  // exclusive scan of the padded bucket counts (one wave) + HBM reservation
+  // (one atomic per non-empty bucket: entries in the low 40 bits, segments
+  // above).  Reservations are multiples of 8 records, so every segment starts
+  // 16-B aligned in the bucket array (cap is a multiple of 64).
   if (tid < 64) {
     uint32_t carry = 0;
     for (uint32_t b0 = 0; b0 < B; b0 += 64) {
       uint32_t b = b0 + tid;
-      uint32_t c = b < B ? s_cnt[b] : 0;
+      uint32_t c = b < B ? (s_cnt[b] + 7u) & ~7u : 0;
       uint32_t x = c;
       for (int o = 1; o < 64; o <<= 1) {
         uint32_t y = __shfl_up(x, o, 64);
@@ -346,7 +354,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
     if (tid == 0) s_start[B] = carry;
   }
   for (uint32_t b = tid; b < B; b += kPartBlock) {
-    uint32_t c = s_cnt[b];
+    const uint32_t c = (s_cnt[b] + 7u) & ~7u;
     uint32_t fit = 0, base = 0;
     if (c) {
       unsigned long long ret = atomicAdd(&pa.fill[b], (unsigned long long)c | (1ull << 40));
@@ -361,28 +369,52 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
     s_fit[b] = fit;
   }
   __syncthreads();
-  // phase 2: counting-sort the records in LDS
+  // phase 2: counting-sort the records in LDS (positions that start no k-mer
+  // land in the dummy bucket's region after the last group and are dropped);
+  // one thread per bucket writes its pad records and its group map entries
+  {
+    uint32_t st[kPartPerThread];
 #pragma unroll
-  for (int j = 0; j < kPartPerThread; ++j) {
-    const uint32_t b = E[j] >> 16;
-    if (b < B) s_sorted[s_start[b] + (E[j] & 0xFFFFu)] = O[j] | ((uint32_t)(q0 + j) << 16);
+    for (int j = 0; j < kPartPerThread; ++j) st[j] = s_start[E[j] >> 16];
+#pragma unroll
+    for (int j = 0; j < kPartPerThread; ++j)
+      s_sorted[st[j] + (E[j] & 0xFFFFu)] = O[j] | ((uint32_t)(q0 + j) << 16);
+  }
+  for (uint32_t b = tid; b < B; b += kPartBlock) {
+    const uint32_t c = s_cnt[b], st = s_start[b], cp = (c + 7u) & ~7u;
+    for (uint32_t i = c; i < cp; ++i) s_sorted[st + i] = 0xFFFFFFFFu;
+    for (uint32_t g = st >> 3; g < (st + cp) >> 3; ++g) s_gmap[g] = (uint8_t)b;
   }
   __syncthreads();
-  // phase 3: one wave per bucket segment -> coalesced writes into the bucket array
-  const int wave = tid >> 6, lane = tid & 63;
-  for (uint32_t b = wave; b < B; b += kPartBlock / 64) {
-    const uint32_t c = s_cnt[b];
-    if (!c) continue;
-    const uint32_t src = s_start[b], fit = s_fit[b];
-    const uint64_t dst = (uint64_t)b * pa.cap + s_base[b];
-    for (uint32_t t = lane; t < c; t += 64) {
-      const uint32_t v = s_sorted[src + t];
-      if (t < fit) {
-        pa.off[dst + t] = (uint16_t)(v & 0xFFFFu);
-        pa.pos[dst + t] = (uint16_t)(v >> 16);
-      } else {  // bucket region full: count directly (correct, slow, rare)
-        atomicAdd(&pa.currents[((uint64_t)b << kBinBits) | (v & 0xFFFFu)], 1ULL);
-      }
+  // phase 3: each thread moves 8-record groups -> one 16-B store into the
+  // offset array and one into the position array
+  const uint32_t n_groups = s_start[B] >> 3;
+#pragma unroll
+  for (int it = 0; it < kGroupIters; ++it) {
+    const uint32_t g = (uint32_t)tid + (uint32_t)it * kPartBlock;
+    if (g >= n_groups) break;
+    const uint32_t b = s_gmap[g];
+    const uint32_t j8 = g * 8 - s_start[b];
+    const uint4 w0 = *reinterpret_cast<const uint4 *>(&s_sorted[g * 8]);
+    const uint4 w1 = *reinterpret_cast<const uint4 *>(&s_sorted[g * 8 + 4]);
+    if (j8 < s_fit[b]) {
+      const uint64_t dst = (uint64_t)b * pa.cap + s_base[b] + j8;
+      // v_perm: bytes {lo16(a), lo16(b)} and {hi16(a), hi16(b)}
+      const uint4 off = make_uint4(__builtin_amdgcn_perm(w0.y, w0.x, 0x05040100u),
+                                   __builtin_amdgcn_perm(w0.w, w0.z, 0x05040100u),
+                                   __builtin_amdgcn_perm(w1.y, w1.x, 0x05040100u),
+                                   __builtin_amdgcn_perm(w1.w, w1.z, 0x05040100u));
+      const uint4 pos = make_uint4(__builtin_amdgcn_perm(w0.y, w0.x, 0x07060302u),
+                                   __builtin_amdgcn_perm(w0.w, w0.z, 0x07060302u),
+                                   __builtin_amdgcn_perm(w1.y, w1.x, 0x07060302u),
+                                   __builtin_amdgcn_perm(w1.w, w1.z, 0x07060302u));
+      *reinterpret_cast<uint4 *>(pa.off + dst) = off;
+      *reinterpret_cast<uint4 *>(pa.pos + dst) = pos;
+    } else {  // bucket region full: count directly (correct, slow, rare)
+      const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      for (int i = 0; i < 8; ++i)
+        if ((w[i] & 0xFFFFu) != kPadOff)
+          atomicAdd(&pa.currents[((uint64_t)b << kBinBits) | (w[i] & 0xFFFFu)], 1ULL);
     }
   }
 }
@@ -390,9 +422,10 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
 __global__ __launch_bounds__(kHistBlock) void k_bucket_hist(PartArgs pa, uint64_t pool,
                                                             uint32_t slices,
                                                             uint32_t *__restrict__ partials) {
-  __shared__ uint32_t h[kBinsPerBucket];
+  __shared__ uint32_t h[kBinsPerBucket + 1];  // + a spill bin for pad records
   const uint32_t b = blockIdx.y, r = blockIdx.x;
-  for (int i = threadIdx.x; i < kBinsPerBucket; i += kHistBlock) h[i] = 0;
+  for (int i = threadIdx.x; i <= kBinsPerBucket; i += kHistBlock) h[i] = 0;
+  auto bin = [](uint32_t off) { return off < (uint32_t)kBinsPerBucket ? off : (uint32_t)kBinsPerBucket; };
   __syncthreads();
   uint64_t n = pa.fill[b] & ((1ull << 40) - 1);
   if (n > pa.cap) n = pa.cap;
@@ -401,30 +434,39 @@ __global__ __launch_bounds__(kHistBlock) void k_bucket_hist(PartArgs pa, uint64_
   // 8 records (16 B) per lane per step where aligned
   uint64_t i = lo;
   for (; i < hi && (i & 7); ++i)
-    if (threadIdx.x == 0) atomicAdd(&h[src[i]], 1u);
+    if (threadIdx.x == 0) atomicAdd(&h[bin(src[i])], 1u);
   const uint64_t hi8 = i + ((hi - i) & ~7ull);
   const uint64_t step = 8ull * kHistBlock;
   uint64_t j = i + 8ull * threadIdx.x;
-  for (; j + 3 * step < hi8; j += 4 * step) {  // four 16-B loads in flight
-    uint4 v[4];
+  // four 16-B loads per lane per round, software-pipelined: the next round's
+  // loads are in flight while this round's 32 LDS atomics issue
+  auto hist8 = [&](const uint4 &v) {
+    atomicAdd(&h[bin(v.x & 0xFFFFu)], 1u); atomicAdd(&h[bin(v.x >> 16)], 1u);
+    atomicAdd(&h[bin(v.y & 0xFFFFu)], 1u); atomicAdd(&h[bin(v.y >> 16)], 1u);
+    atomicAdd(&h[bin(v.z & 0xFFFFu)], 1u); atomicAdd(&h[bin(v.z >> 16)], 1u);
+    atomicAdd(&h[bin(v.w & 0xFFFFu)], 1u); atomicAdd(&h[bin(v.w >> 16)], 1u);
+  };
+  if (j + 3 * step < hi8) {
+    uint4 cur[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) v[t] = *reinterpret_cast<const uint4 *>(src + j + t * step);
+    for (int t = 0; t < 4; ++t) cur[t] = *reinterpret_cast<const uint4 *>(src + j + t * step);
+    for (;;) {
+      const uint64_t jn = j + 4 * step;
+      const bool more = jn + 3 * step < hi8;
+      uint4 nxt[4];  // unconditional (clamped) loads keep the wait counts static
+      const uint64_t jl = more ? jn : j;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      atomicAdd(&h[v[t].x & 0xFFFFu], 1u); atomicAdd(&h[v[t].x >> 16], 1u);
-      atomicAdd(&h[v[t].y & 0xFFFFu], 1u); atomicAdd(&h[v[t].y >> 16], 1u);
-      atomicAdd(&h[v[t].z & 0xFFFFu], 1u); atomicAdd(&h[v[t].z >> 16], 1u);
-      atomicAdd(&h[v[t].w & 0xFFFFu], 1u); atomicAdd(&h[v[t].w >> 16], 1u);
+      for (int t = 0; t < 4; ++t) nxt[t] = *reinterpret_cast<const uint4 *>(src + jl + t * step);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) hist8(cur[t]);
+      j = jn;
+      if (!more) break;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) cur[t] = nxt[t];
     }
   }
-  for (; j < hi8; j += step) {
-    const uint4 v = *reinterpret_cast<const uint4 *>(src + j);
-    atomicAdd(&h[v.x & 0xFFFFu], 1u); atomicAdd(&h[v.x >> 16], 1u);
-    atomicAdd(&h[v.y & 0xFFFFu], 1u); atomicAdd(&h[v.y >> 16], 1u);
-    atomicAdd(&h[v.z & 0xFFFFu], 1u); atomicAdd(&h[v.z >> 16], 1u);
-    atomicAdd(&h[v.w & 0xFFFFu], 1u); atomicAdd(&h[v.w >> 16], 1u);
-  }
-  for (uint64_t j = hi8 + threadIdx.x; j < hi; j += kHistBlock) atomicAdd(&h[src[j]], 1u);
+  for (; j < hi8; j += step) hist8(*reinterpret_cast<const uint4 *>(src + j));
+  for (uint64_t j = hi8 + threadIdx.x; j < hi; j += kHistBlock) atomicAdd(&h[bin(src[j])], 1u);
   __syncthreads();
   const uint64_t nb0 = (uint64_t)b << kBinBits;
   const uint64_t nbins = pool - nb0 < (uint64_t)kBinsPerBucket ? pool - nb0 : kBinsPerBucket;
@@ -515,16 +557,25 @@ __global__ __launch_bounds__(kHistBlock) void k_uniq_scan(PartArgs pa, UniqArgs 
                                                           uint32_t slices,
                                                           unsigned long long *__restrict__ hits,
                                                           unsigned long long *__restrict__ n_hits,
-                                                          uint64_t hit_cap) {
-  __shared__ uint32_t bits[kBinsPerBucket / 32];
+                                                          uint64_t hit_cap,
+                                                          unsigned long long *__restrict__ set_keys,
+                                                          const uint64_t *__restrict__ set_mask) {
+  __shared__ uint32_t bits[65536 / 32];  // covers the pad sentinel bin (never set)
   __shared__ uint32_t t_off[kMaxTopN];
   __shared__ uint32_t t_slot[kMaxTopN];
   __shared__ unsigned long long buf[kScanBuf];
   __shared__ uint32_t t_n, s_nh;
   __shared__ unsigned long long s_base;
+  {  // every block first empties its share of the uniques hash set (k_uniq_hits fills it)
+    const uint64_t cap = *set_mask + 1;
+    const uint64_t nthr = (uint64_t)gridDim.x * gridDim.y * kHistBlock;
+    for (uint64_t i = ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * kHistBlock + threadIdx.x;
+         i < cap; i += nthr)
+      set_keys[i] = kEmpty;
+  }
   if (blockIdx.y >= *n_tb) return;
   const uint32_t b = tbuckets[blockIdx.y], r = blockIdx.x;
-  for (int i = threadIdx.x; i < kBinsPerBucket / 32; i += kHistBlock) bits[i] = 0;
+  for (int i = threadIdx.x; i < 65536 / 32; i += kHistBlock) bits[i] = 0;
   if (threadIdx.x == 0) { t_n = 0; s_nh = 0; }
   __syncthreads();
   for (uint32_t s = threadIdx.x; s < u.n_top; s += kHistBlock) {
@@ -641,32 +692,346 @@ __global__ void k_lif_table(LifEntry *__restrict__ tbl, int n, LifParams lp) {
   tbl[i].r = r;
 }
 
+__device__ __forceinline__ bool cand_before(const TopCand &a, const TopCand &b) {
+  return a.sc != b.sc ? a.sc > b.sc : a.idx < b.idx;
+}
+
+// Bitonic sort of one row per lane across a wave64 (registers + shuffles, no
+// LDS, no barriers): lane 0 ends with the first row by cand_before.  Empty
+// lanes carry {idx ~0, sc 0}, which sorts last.
+__device__ __forceinline__ TopCand wave_sort64(TopCand x) {
+  const int lane = threadIdx.x & 63;
+  for (int size = 2; size <= 64; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      TopCand y;
+      y.idx = __shfl_xor(x.idx, stride, 64);
+      y.sc = __shfl_xor(x.sc, stride, 64);
+      const bool up = (lane & size) == 0, lower = (lane & stride) == 0;
+      if (lower == up ? cand_before(y, x) : cand_before(x, y)) x = y;
+    }
+  }
+  return x;
+}
+
+// Exclusive prefix sum over the threads of a block (blockDim.x <= 1024, a
+// multiple of 64); *total gets the block sum.  Two barriers.
+template <typename T>
+__device__ __forceinline__ T block_excl_scan(T x, T *s_w, T *total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  T incl = x;
+  for (int o = 1; o < 64; o <<= 1) {
+    const T y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) s_w[w] = incl;
+  __syncthreads();
+  T pre = 0, tot = 0;
+  for (int i = 0; i < nw; ++i) {
+    const T v = s_w[i];
+    pre += i < w ? v : (T)0;
+    tot += v;
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + incl - x;
+}
+
+// Set sizing and bookkeeping for the uniques pass from the final top rows
+// (one block of 1024 threads).
+__device__ void top_post_block(const TopCand *top, const uint64_t *top_cur, uint32_t m,
+                               const PostArgs &pa) {
+  __shared__ unsigned long long s_sum;
+  __shared__ uint32_t s_nb, s_over;
+  __shared__ uint32_t s_bk[kMaxTopN];
+  if (threadIdx.x == 0) { s_sum = 0; s_nb = 0; s_over = 0; *pa.n_hits = 0; }
+  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x)
+    s_bk[i] = (uint32_t)(top[i].idx >> kBinBits);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+    pa.uniq[i] = 0;
+    pa.special[i] = 0;
+    atomicAdd(&s_sum, (unsigned long long)top_cur[i]);
+    if (pa.part) {
+      const uint32_t b = s_bk[i];
+      if (pa.overflow[b]) s_over = 1;
+      bool first = true;  // first row of its bucket in the list
+      for (uint32_t j = 0; j < i; ++j)
+        if (s_bk[j] == b) { first = false; break; }
+      if (first) pa.tbuckets[atomicAdd(&s_nb, 1u)] = b;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t cap = 64;
+    while (cap < 2 * (uint64_t)s_sum + 2) cap <<= 1;
+    pa.flags[0] = cap > pa.set_alloc ? 1u : 0u;  // set too small
+    pa.flags[1] = s_over;                        // a top bucket overflowed
+    pa.flags[2] = s_nb;                          // distinct top buckets
+    pa.flags[3] = 0;
+    *pa.set_mask = (cap > pa.set_alloc ? pa.set_alloc : cap) - 1;
+  }
+}
+
 constexpr int kLifPerThread = 8;
 
 constexpr int kLifBlock = 1024;
-__global__ __launch_bounds__(kLifBlock) void k_lif_apply(const uint64_t *__restrict__ currents,
+constexpr int kLifWaves = kLifBlock / 64;
+
+// Block-local top `want` rows of this LIF block (want <= kFuseMaxTopN) from its
+// spike histogram `sh` (bin = min(spikes, 4095)): rows above the block
+// threshold in any order, then the threshold ties in index order.  Returns
+// false when the threshold falls in the clamp bin (exact refine on the host).
+__device__ bool block_top(const uint32_t *sh, const uint64_t *scv, uint64_t base, uint64_t pool,
+                          uint32_t want, TopCand *out, TopCand *gout, uint32_t *gcnt) {
+  __shared__ uint32_t s_w[kLifWaves];
+  __shared__ uint32_t s_T, s_above, s_need, s_n;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  // thread t owns bins 4095-4t .. 4092-4t (counted from the top)
+  uint32_t loc = 0;
+  for (int j = 0; j < 4; ++j) loc += sh[kHistBins - 1 - (4 * t + j)];
+  uint32_t total;
+  const uint32_t before = block_excl_scan(loc, s_w, &total);
+  if (t == 0) {  // fewer rows than `want` in this block: take everything
+    s_T = 0;
+    s_above = total - sh[0];
+    s_need = want - s_above;
+    s_n = 0;
+  }
+  __syncthreads();
+  if (total >= want && before < want && before + loc >= want) {
+    uint32_t cum = before;
+    for (int j = 0; j < 4; ++j) {
+      const int bin = kHistBins - 1 - (4 * t + j);
+      const uint32_t h = sh[bin];
+      if (cum + h >= want) {
+        s_T = (uint32_t)bin;
+        s_above = cum;
+        s_need = want - cum;
+        break;
+      }
+      cum += h;
+    }
+  }
+  __syncthreads();
+  const uint64_t T = s_T;
+  const uint32_t above = s_above, need = s_need;
+  if (T == (uint64_t)(kHistBins - 1)) return false;
+  for (int j = 0; j < kLifPerThread; ++j) {
+    const uint64_t i = base + (uint64_t)j * kLifBlock + t;
+    if (i < pool && scv[j] > T) {
+      const uint32_t at = atomicAdd(&s_n, 1u);
+      out[at].idx = i;
+      out[at].sc = scv[j];
+    }
+  }
+  // ties: index order is (row j, thread t)
+  uint32_t run = 0;
+  for (int j = 0; j < kLifPerThread && run < need; ++j) {
+    const uint64_t i = base + (uint64_t)j * kLifBlock + t;
+    const bool tie = i < pool && scv[j] == T;
+    const uint64_t bal = __ballot(tie);
+    if (lane == 0) s_w[w] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t pre = run, row = 0;
+    for (int q = 0; q < kLifWaves; ++q) {
+      pre += q < w ? s_w[q] : 0u;
+      row += s_w[q];
+    }
+    const uint32_t r = pre + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+    if (tie && r < need) {
+      out[above + r].idx = i;
+      out[above + r].sc = T;
+    }
+    run += row;
+    __syncthreads();
+  }
+  __syncthreads();
+  // this block's rows, sorted, to its candidate slot (wave 0)
+  if (t < 64) {
+    const uint32_t n = above + (run < need ? run : need);
+    TopCand x;
+    if ((uint32_t)t < n) x = out[t];
+    else { x.idx = ~0ULL; x.sc = 0; }
+    x = wave_sort64(x);
+    if ((uint32_t)t < n) gout[t] = x;
+    if (t == 0) *gcnt = n;
+  }
+  return true;
+}
+
+// Selection left to the host's exact path: flag it, and leave the uniques pass
+// that is already queued with no work (no top buckets, no hits).
+__device__ void defer_to_host(const TopFuse &tf, uint64_t T, uint64_t n_above, uint64_t need) {
+  tf.st->T = T;
+  tf.st->n_above = n_above;
+  tf.st->need = need;
+  tf.st->emit_above = 0;
+  tf.st->refine = 1u;
+  for (int i = 0; i < 4; ++i) tf.post.flags[i] = 0;
+  *tf.post.n_hits = 0;
+}
+
+// The final selection: global threshold from the spike histogram copies, the
+// exact global rows from the block candidates, sort, post-processing.
+__device__ void final_top(const uint32_t *hist, uint64_t pool, const uint64_t *currents,
+                          uint32_t nb, const TopFuse &tf) {
+  __shared__ unsigned long long s_w64[kLifWaves];
+  __shared__ uint32_t s_w32[kLifWaves];
+  __shared__ unsigned long long s_T, s_above, s_need;
+  __shared__ uint32_t s_na, s_bad;
+  __shared__ uint32_t s_ab[kFuseMaxBlocks], s_tb[kFuseMaxBlocks];
+  __shared__ TopCand s_fin[kFuseMaxTopN];
+  const int t = threadIdx.x;
+  const uint64_t want = tf.want < pool ? tf.want : pool;
+  // (1) global threshold, as k_topn_threshold: 32 independent loads per thread
+  unsigned long long h4[4] = {0, 0, 0, 0};
+  {
+    uint4 hv[kHistCopies];  // bins 4092-4t .. 4095-4t of every copy: one round trip
+#pragma unroll
+    for (int c = 0; c < kHistCopies; ++c)
+      hv[c] = *reinterpret_cast<const uint4 *>(hist + c * kHistBins + kHistBins - 4 - 4 * t);
+#pragma unroll
+    for (int c = 0; c < kHistCopies; ++c) {
+      h4[0] += hv[c].w;
+      h4[1] += hv[c].z;
+      h4[2] += hv[c].y;
+      h4[3] += hv[c].x;
+    }
+  }
+  const unsigned long long loc = h4[0] + h4[1] + h4[2] + h4[3];
+  unsigned long long total;
+  const unsigned long long before = block_excl_scan(loc, s_w64, &total);
+  if (t == 0) { s_T = 0; s_above = total; s_need = 0; s_na = 0; s_bad = 0; }
+  if ((uint32_t)t < nb) { s_ab[t] = 0; s_tb[t] = 0; }
+  __syncthreads();
+  if (before < want && before + loc >= want) {
+    unsigned long long cum = before;
+    for (int j = 0; j < 4; ++j) {
+      if (cum + h4[j] >= want) {
+        s_T = (unsigned long long)(kHistBins - 1 - (4 * t + j));
+        s_above = cum;
+        s_need = want - cum;
+        break;
+      }
+      cum += h4[j];
+    }
+  }
+  __syncthreads();
+  const uint64_t T = s_T, n_above = s_above, need = s_need;
+  if (T == (uint64_t)(kHistBins - 1)) {  // spike counts >= 4095: host radix refine
+    if (t == 0) defer_to_host(tf, T, n_above, need);
+    return;
+  }
+  // (2) every block's sorted candidate list: rows above T (any order is fine,
+  // the final sort orders them) and the number of ties at T per block
+  const uint32_t W = tf.want, M = nb * W;
+  constexpr int U = 8;
+  TopCand cv[U];
+  uint32_t cn[U];
+  // unconditional loads at clamped indices: the U loads of a chunk are in
+  // flight together (one round trip); masked afterwards
+  auto load_chunk = [&](uint32_t c0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      uint32_t id = c0 + u * kLifBlock + t;
+      id = id < M ? id : M - 1;
+      cn[u] = tf.bcnt[id / W];
+      cv[u] = tf.bcand[id];
+    }
+  };
+  for (uint32_t c0 = 0; c0 < M; c0 += U * kLifBlock) {
+    load_chunk(c0);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t id = c0 + u * kLifBlock + t;
+      if (id >= M || id % W >= cn[u]) continue;
+      if (cv[u].sc > T) {
+        atomicAdd(&s_ab[id / W], 1u);
+        const uint32_t at = atomicAdd(&s_na, 1u);
+        if (at < kFuseMaxTopN) s_fin[at] = cv[u];
+      } else if (cv[u].sc == T) {
+        atomicAdd(&s_tb[id / W], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  // ties: block order is index order, and each list holds its ties in index
+  // order right after its rows above T
+  uint32_t ttot;
+  const uint32_t tpre = block_excl_scan((uint32_t)t < nb ? s_tb[t] : 0u, s_w32, &ttot);
+  if ((uint32_t)t < nb) s_tb[t] = tpre;
+  if (t == 0 && (s_na != n_above || ttot < need)) s_bad = 1;  // cannot happen; be safe
+  __syncthreads();
+  if (s_bad) {
+    if (t == 0) defer_to_host(tf, T, n_above, need);
+    return;
+  }
+  for (uint32_t c0 = 0; c0 < M; c0 += U * kLifBlock) {
+    if (M > U * kLifBlock) load_chunk(c0);  // one chunk: still in registers
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t id = c0 + u * kLifBlock + t;
+      if (id >= M || id % W >= cn[u] || cv[u].sc != T) continue;
+      const uint32_t b = id / W;
+      const uint64_t r = (uint64_t)s_tb[b] + (id % W - s_ab[b]);
+      if (r < need) s_fin[n_above + r] = cv[u];
+    }
+  }
+  __syncthreads();
+  // (3) exact order (wave 0), rows and their currents out
+  const uint32_t m = (uint32_t)want;
+  if (t < 64) {
+    TopCand x;
+    if ((uint32_t)t < m) x = s_fin[t];
+    else { x.idx = ~0ULL; x.sc = 0; }
+    x = wave_sort64(x);
+    if ((uint32_t)t < m) {
+      tf.cand[t] = x;
+      tf.top_cur[t] = currents[x.idx];
+    }
+    if (t == 0) { tf.st->T = T; tf.st->n_above = n_above; tf.st->need = need;
+                  tf.st->emit_above = n_above; tf.st->refine = 0u; }
+  }
+  __syncthreads();
+  // (4) uniques bookkeeping on the final rows
+  top_post_block(tf.cand, tf.top_cur, m, tf.post);
+}
+
+__global__ __launch_bounds__(kLifBlock) void k_lif_apply(uint64_t *__restrict__ currents,
+                                                      const uint32_t *__restrict__ partials,
+                                                      uint32_t slices, int fresh,
                                                       float *__restrict__ V,
                                                       uint32_t *__restrict__ R,
                                                       uint64_t *__restrict__ SC, uint64_t pool,
                                                       LifParams lp,
                                                       const LifEntry *__restrict__ tbl, int tbl_n,
                                                       uint32_t *__restrict__ hist,
-                                                      unsigned long long *__restrict__ stats) {
+                                                      unsigned long long *__restrict__ stats,
+                                                      TopFuse tf) {
   __shared__ uint32_t sh[kHistBins];
-  __shared__ unsigned long long s_sp[kLifBlock / 64];
-  __shared__ unsigned long long s_mx[kLifBlock / 64];
+  __shared__ unsigned long long s_sp[kLifWaves];
+  __shared__ unsigned long long s_mx[kLifWaves];
+  __shared__ TopCand s_cand[kFuseMaxTopN];
   for (int i = threadIdx.x; i < kHistBins; i += kLifBlock) sh[i] = 0;
   __syncthreads();
   const uint64_t base = (uint64_t)blockIdx.x * kLifBlock * kLifPerThread;
   unsigned long long my_sp = 0, my_mx = 0;
+  uint64_t scv[kLifPerThread];
   for (int j = 0; j < kLifPerThread; ++j) {
+    scv[j] = 0;
     uint64_t i = base + (uint64_t)j * kLifBlock + threadIdx.x;
     if (i >= pool) break;
     uint64_t cnt = currents[i];
-    uint64_t sc = SC[i];
+    if (slices) {  // fused K1c: fold the bucket histograms' partials in first
+      for (uint32_t r = 0; r < slices; ++r) cnt += partials[(uint64_t)r * pool + i];
+      currents[i] = cnt;
+    }
+    // fresh state (after nk_reset): v = r = spikes = 0 without reading them,
+    // and every neuron is written
+    uint64_t sc = fresh ? 0 : SC[i];
     if (!(lp.skip_zero && cnt == 0) && lp.steps != 0) {
-      float v = V[i];
-      uint32_t r = R[i];
+      float v = fresh ? 0.0f : V[i];
+      uint32_t r = fresh ? 0u : R[i];
       uint64_t sp;
       if (v == 0.0f && r == 0 && cnt < (uint64_t)tbl_n) {
         const LifEntry e = tbl[cnt];
@@ -681,7 +1046,12 @@ __global__ __launch_bounds__(kLifBlock) void k_lif_apply(const uint64_t *__restr
       sc += sp;
       SC[i] = sc;
       my_sp += sp;
+    } else if (fresh) {
+      V[i] = 0.0f;
+      R[i] = 0u;
+      SC[i] = 0;
     }
+    scv[j] = sc;
     my_mx = sc > my_mx ? sc : my_mx;
     atomicAdd(&sh[sc < (uint64_t)(kHistBins - 1) ? (uint32_t)sc : (uint32_t)(kHistBins - 1)], 1u);
   }
@@ -695,15 +1065,30 @@ __global__ __launch_bounds__(kLifBlock) void k_lif_apply(const uint64_t *__restr
   __syncthreads();
   if (threadIdx.x == 0) {
     unsigned long long a = 0, m = 0;
-    for (int w = 0; w < kLifBlock / 64; ++w) { a += s_sp[w]; m = s_mx[w] > m ? s_mx[w] : m; }
+    for (int w = 0; w < kLifWaves; ++w) { a += s_sp[w]; m = s_mx[w] > m ? s_mx[w] : m; }
     if (a) atomicAdd(&stats[0], a);
     atomicMax(&stats[1], m);
   }
   // 8 copies of the global histogram (blocks b, b+8, ... share one), summed by
-  // the threshold kernel: the hot spike-count bins see 8x fewer atomics each
+  // the threshold step: the hot spike-count bins see 8x fewer atomics each
   uint32_t *hc = hist + (size_t)(blockIdx.x & (kHistCopies - 1)) * kHistBins;
   for (int i = threadIdx.x; i < kHistBins; i += kLifBlock)
     if (sh[i]) atomicAdd(&hc[i], sh[i]);
+  if (!tf.want) return;
+  // fused top-N: this block's candidates (the final step is k_top_final)
+  if (!block_top(sh, scv, base, pool, tf.want, s_cand, tf.bcand + (uint64_t)blockIdx.x * tf.want,
+                 tf.bcnt + blockIdx.x) &&
+      threadIdx.x == 0)
+    tf.bcnt[blockIdx.x] = 0;  // the final step sees the clamp bin and defers to the host
+}
+
+// After the LIF kernel (the kernel boundary makes every block's candidates,
+// histogram and currents visible): one block of kLifBlock threads.
+__global__ __launch_bounds__(kLifBlock) void k_top_final(const uint32_t *__restrict__ hist,
+                                                      uint64_t pool,
+                                                      const uint64_t *__restrict__ currents,
+                                                      uint32_t nb, TopFuse tf) {
+  final_top(hist, pool, currents, nb, tf);
 }
 
 // ---------------------------------------------------------------------------
@@ -842,9 +1227,6 @@ __global__ __launch_bounds__(kBlock) void k_topn_emit(const uint64_t *__restrict
   }
 }
 
-__device__ __forceinline__ bool cand_before(const TopCand &a, const TopCand &b) {
-  return a.sc != b.sc ? a.sc > b.sc : a.idx < b.idx;
-}
 
 // exact final order of the <= kMaxTopN candidates: bitonic sort in LDS
 __global__ __launch_bounds__(1024) void k_topn_sort(TopCand *__restrict__ cand, uint32_t m,
@@ -981,14 +1363,22 @@ hipError_t launch_lif_table(LifEntry *tbl, int n, LifParams lp, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_lif_apply(const uint64_t *currents, float *v, uint32_t *r, uint64_t *sc,
-                            uint64_t pool, LifParams lp, const LifEntry *tbl, int tbl_n,
-                            uint32_t *hist, uint64_t *stats, hipStream_t s) {
+uint32_t lif_blocks(uint64_t pool) {
+  const uint64_t per = (uint64_t)kLifBlock * kLifPerThread;
+  return (uint32_t)((pool + per - 1) / per);
+}
+
+hipError_t launch_lif_apply(uint64_t *currents, const uint32_t *partials, uint32_t slices,
+                            int fresh, float *v, uint32_t *r, uint64_t *sc, uint64_t pool, LifParams lp,
+                            const LifEntry *tbl, int tbl_n, uint32_t *hist, uint64_t *stats,
+                            const TopFuse &tf, hipStream_t s) {
   if (!pool) return hipSuccess;
-  uint64_t per = (uint64_t)kLifBlock * kLifPerThread;
-  unsigned g = (unsigned)((pool + per - 1) / per);
-  hipLaunchKernelGGL(k_lif_apply, dim3(g), dim3(kLifBlock), 0, s, currents, v, r, sc, pool, lp, tbl,
-                     tbl_n, hist, (unsigned long long *)stats);
+  const unsigned g = lif_blocks(pool);
+  if (tf.want && (tf.want > kFuseMaxTopN || g > kFuseMaxBlocks)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_lif_apply, dim3(g), dim3(kLifBlock), 0, s, currents, partials, slices, fresh,
+                     v, r, sc, pool, lp, tbl, tbl_n, hist, (unsigned long long *)stats, tf);
+  if (tf.want)
+    hipLaunchKernelGGL(k_top_final, dim3(1), dim3(kLifBlock), 0, s, hist, pool, currents, g, tf);
   return hipGetLastError();
 }
 
@@ -1098,7 +1488,7 @@ hipError_t launch_part_uniques(const KmerInput &in, int k, int canonical, const 
                                unsigned long long *n_hits, uint64_t hit_cap, hipStream_t s) {
   if (!max_tb) return hipSuccess;
   hipLaunchKernelGGL(k_uniq_scan, dim3(slices, max_tb), dim3(kHistBlock), 0, s, pa, u, tbuckets,
-                     n_tb, slices, hits, n_hits, hit_cap);
+                     n_tb, slices, hits, n_hits, hit_cap, u.set_keys, u.set_mask);
   const unsigned g = 1024;
   if (canonical)
     hipLaunchKernelGGL(k_uniq_hits<true>, dim3(g), dim3(256), 0, s, in, k, pa, u, hits, n_hits,
@@ -1115,41 +1505,8 @@ hipError_t launch_part_uniques(const KmerInput &in, int k, int canonical, const 
 // region overflowed).  One block.
 __global__ __launch_bounds__(1024) void k_top_post(const TopCand *__restrict__ top,
                                                    const uint64_t *__restrict__ top_cur,
-                                                   uint32_t m, uint64_t set_alloc,
-                                                   const uint32_t *__restrict__ overflow,
-                                                   int part, uint64_t *__restrict__ set_mask,
-                                                   uint32_t *__restrict__ tbuckets,
-                                                   uint32_t *__restrict__ flags,
-                                                   uint32_t *__restrict__ uniq,
-                                                   uint32_t *__restrict__ special,
-                                                   unsigned long long *__restrict__ n_hits) {
-  __shared__ unsigned long long s_sum;
-  __shared__ uint32_t s_nb, s_over;
-  if (threadIdx.x == 0) { s_sum = 0; s_nb = 0; s_over = 0; *n_hits = 0; }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
-    uniq[i] = 0;
-    special[i] = 0;
-    atomicAdd(&s_sum, (unsigned long long)top_cur[i]);
-    if (part) {
-      const uint32_t b = (uint32_t)(top[i].idx >> kBinBits);
-      if (overflow[b]) s_over = 1;
-      bool first = true;  // first row of its bucket in the list
-      for (uint32_t j = 0; j < i; ++j)
-        if ((uint32_t)(top[j].idx >> kBinBits) == b) { first = false; break; }
-      if (first) tbuckets[atomicAdd(&s_nb, 1u)] = b;
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint64_t cap = 64;
-    while (cap < 2 * (uint64_t)s_sum + 2) cap <<= 1;
-    flags[0] = cap > set_alloc ? 1u : 0u;  // set too small
-    flags[1] = s_over;                     // a top bucket overflowed
-    flags[2] = s_nb;                       // distinct top buckets
-    flags[3] = 0;
-    *set_mask = (cap > set_alloc ? set_alloc : cap) - 1;
-  }
+                                                   uint32_t m, PostArgs pa) {
+  top_post_block(top, top_cur, m, pa);
 }
 
 hipError_t launch_top_post(const TopCand *top, const uint64_t *top_cur, uint32_t m,
@@ -1157,8 +1514,8 @@ hipError_t launch_top_post(const TopCand *top, const uint64_t *top_cur, uint32_t
                            uint64_t *set_mask, uint32_t *tbuckets, uint32_t *flags,
                            uint32_t *uniq, uint32_t *special, unsigned long long *n_hits,
                            hipStream_t s) {
-  hipLaunchKernelGGL(k_top_post, dim3(1), dim3(1024), 0, s, top, top_cur, m, set_alloc, overflow,
-                     part, set_mask, tbuckets, flags, uniq, special, n_hits);
+  PostArgs pa{set_alloc, overflow, part, set_mask, tbuckets, flags, uniq, special, n_hits};
+  hipLaunchKernelGGL(k_top_post, dim3(1), dim3(1024), 0, s, top, top_cur, m, pa);
   return hipGetLastError();
 }
 
@@ -1179,6 +1536,47 @@ __global__ void k_zero(ZeroList z) {
     for (uint64_t i = tid; i < n16; i += stride) reinterpret_cast<uint4 *>(p)[i] = make_uint4(0, 0, 0, 0);
     for (uint64_t i = n16 * 16 + tid; i < n; i += stride) p[i] = 0;
   }
+}
+
+// tile -> first record (blocks [0, tr_blocks)) + the zero list (the rest)
+__global__ void k_prep(const uint64_t *__restrict__ offsets, uint64_t n_recs, uint64_t n_tiles,
+                       uint64_t tile_size, uint32_t *__restrict__ tile_rec, unsigned tr_blocks,
+                       ZeroList z) {
+  if (blockIdx.x < tr_blocks) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_tiles) return;
+    const uint64_t pos = t * tile_size;
+    uint64_t lo = 0, hi = n_recs;
+    while (hi - lo > 1) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (offsets[mid] <= pos) lo = mid;
+      else hi = mid;
+    }
+    tile_rec[t] = (uint32_t)lo;
+    return;
+  }
+  const uint64_t tid = (uint64_t)(blockIdx.x - tr_blocks) * blockDim.x + threadIdx.x;
+  const uint64_t stride = (uint64_t)(gridDim.x - tr_blocks) * blockDim.x;
+  for (int b = 0; b < z.n; ++b) {
+    uint8_t *p = (uint8_t *)z.ptr[b];
+    const uint64_t n = z.bytes[b];
+    const uint64_t n16 = ((uintptr_t)p & 15) ? 0 : n / 16;
+    for (uint64_t i = tid; i < n16; i += stride) reinterpret_cast<uint4 *>(p)[i] = make_uint4(0, 0, 0, 0);
+    for (uint64_t i = n16 * 16 + tid; i < n; i += stride) p[i] = 0;
+  }
+}
+
+hipError_t launch_prep(const KmerInput &in, uint64_t tile_size, uint32_t *tile_rec,
+                       const ZeroList &z, hipStream_t s) {
+  uint64_t tot = 0;
+  for (int b = 0; b < z.n; ++b) tot += z.bytes[b];
+  const unsigned tr = (unsigned)((in.n_tiles + 255) / 256);
+  unsigned g = (unsigned)((tot / 16 + 255) / 256);
+  if (g > 1024) g = 1024;
+  if (!g) g = 1;
+  hipLaunchKernelGGL(k_prep, dim3(tr + g), dim3(256), 0, s, in.offsets, in.n_recs, in.n_tiles,
+                     tile_size, tile_rec, tr, z);
+  return hipGetLastError();
 }
 
 hipError_t launch_zero(const ZeroList &z, hipStream_t s) {

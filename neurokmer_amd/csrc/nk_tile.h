@@ -77,12 +77,24 @@ __device__ __forceinline__ void stage_tile(TileLds<TILE, RAW> &L, const KmerInpu
   const int tid = threadIdx.x;
   const uint64_t T0 = tile * (uint64_t)TILE;
   const uint64_t n_bases = in.n_bases;
-  for (int c = tid; c < kChunks; c += BLOCK) {
-    uint64_t g = T0 + 16ull * c;
-    uint4 v;
-    if (g + 16 <= n_bases) {
-      v = *reinterpret_cast<const uint4 *>(in.bases + g);
-    } else {
+  // all of this thread's 16-B loads are issued before any is consumed; the
+  // input's last partial chunk takes a byte path afterwards
+  constexpr int kIter = (kChunks + BLOCK - 1) / BLOCK;
+  uint4 vv[kIter];
+#pragma unroll
+  for (int i = 0; i < kIter; ++i) {
+    const int c = tid + i * BLOCK;
+    const uint64_t g = T0 + 16ull * c;
+    vv[i] = (c < kChunks && g + 16 <= n_bases) ? *reinterpret_cast<const uint4 *>(in.bases + g)
+                                               : make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < kIter; ++i) {
+    const int c = tid + i * BLOCK;
+    if (c >= kChunks) break;
+    const uint64_t g = T0 + 16ull * c;
+    uint4 v = vv[i];
+    if (g + 16 > n_bases) {
       uint32_t w[4] = {0, 0, 0, 0};
       for (int j = 0; j < 16; ++j)
         if (g + j < n_bases) w[j >> 2] |= (uint32_t)in.bases[g + j] << (8 * (j & 3));

@@ -145,6 +145,34 @@ def test_state_persists_across_calls():
     assert g.top_abundant_neurons(5) == [(i, 0, 0) for i in range(5)]
 
 
+def test_reset_is_lazy_and_exact():
+    """nk_reset only marks the state fresh; the next call must equal a fresh
+    counter, and the copy-outs right after a reset must read zeros."""
+    b1, o1 = synth.make_records(120_000, 3, repeats_per_mb=6000, motif_len=70, seed=4)
+    b2, o2 = synth.make_records(110_000, 4, repeats_per_mb=9000, motif_len=50, seed=5)
+    g = SpikingKmerCounter(21, 1.0, 0.95, 2, 1.0, 5003, True)
+    g.process_parallel_arrays(b1, o1)
+    g.reset()
+    for arr in (g.currents(), g.spike_counts(), g.refractory()):
+        assert not arr.any()
+    assert not g.voltages().view(np.uint32).any()
+    g.process_parallel_arrays(b1, o1)
+    g.reset()  # no copy-out in between: the LIF must not read the stale state
+    g.process_parallel_arrays(b2, o2)
+    r = cbind.OracleCounter(21, 1.0, 0.95, 2, 1.0, 5003, True)
+    r.process_parallel_arrays(b2, o2)
+    assert_same(g, r)
+
+
+@pytest.mark.parametrize("top_n", [1, 2, 63, 64, 65, 333])
+def test_top_n_selection_paths(top_n):
+    # <= 64 rows: selection fused into the LIF kernel; more: separate kernels.
+    # Saturated repeats make long runs of ties broken by index.
+    bases, offs = synth.make_records(300_000, 5, repeats_per_mb=20_000, motif_len=60, seed=17)
+    g, r = run_both(bases, offs, 21, 70_001, True, top_n=top_n)
+    assert_same(g, r, n=top_n)
+
+
 def test_python_restatement_agrees():
     # tiny case through the pure-Python restatement as a second, independent oracle
     bases, offs = ragged_records(total=6000, n_rate=0.01, mixed_case=True, seed=99, max_len=900)

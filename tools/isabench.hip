@@ -45,6 +45,15 @@ __global__ __launch_bounds__(256) void kop(uint32_t *out, uint64_t *clk) {
     if (OP == 19) { CHAIN8("v_pk_add_u16 %0, %0, %1") }
     if (OP == 20) { CHAIN8("v_and_or_b32 %0, %0, %1, %2") }
     if (OP == 21) { CHAIN8("v_mul_u32_u24 %0, %0, %1") }
+    if (OP == 22) { CHAIN8("v_mov_b32_e32 %0, %1") }
+    if (OP == 23) {
+#define SWP(A, B) asm volatile("v_swap_b32 %0, %1" : "+v"(A), "+v"(B));
+      SWP(a0, a1) SWP(a2, a3) SWP(a4, a5) SWP(a6, a7) SWP(a1, a2) SWP(a3, a4) SWP(a5, a6) SWP(a7, a0)
+    }
+    if (OP == 24) {  // 64-bit add as a VOP2 carry pair through VCC
+#define ADC(L, H) asm volatile("v_add_co_u32_e32 %0, vcc, %0, %2\n\tv_addc_co_u32_e32 %1, vcc, %1, %3, vcc" : "+v"(L), "+v"(H) : "v"(b0), "v"(c0) : "vcc");
+      ADC(a0, a1) ADC(a2, a3) ADC(a4, a5) ADC(a6, a7)
+    }
   }
   uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
   out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
@@ -72,6 +81,8 @@ __global__ __launch_bounds__(256) void kop64(uint64_t *out, uint64_t *clk) {
 #define MAD(A) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(A) : "v"(bl), "v"(bh) : "vcc");
       MAD(a0) MAD(a1) MAD(a2) MAD(a3) MAD(a4) MAD(a5) MAD(a6) MAD(a7)
     }
+    if (OP == 3) { CHAIN8_64("v_pk_mov_b32 %0, %0, %0 op_sel:[1,0]") }
+    if (OP == 4) { CHAIN8_64("v_mov_b64_e32 %0, %1") }
   }
   uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
   out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
@@ -132,7 +143,12 @@ int main() {
   run("v_pk_add_u16", kop<19>, out, clk);
   run("v_and_or_b32", kop<20>, out, clk);
   run("v_mul_u32_u24", kop<21>, out, clk);
+  run("v_mov_b32_e32", kop<22>, out, clk);
+  run("v_swap_b32 (8/iter)", kop<23>, out, clk);
+  run("add_co+addc_co e32 (4 pairs)", kop<24>, out, clk);
   run("v_lshl_add_u64", kop64<0>, out, clk);
+  run("v_pk_mov_b32 swap", kop64<3>, out, clk);
+  run("v_mov_b64_e32", kop64<4>, out, clk);
   run("v_lshlrev_b64", kop64<1>, out, clk);
   run("v_mad_u64_u32", kop64<2>, out, clk);
   return 0;
