@@ -127,7 +127,7 @@ struct nk_counter {
   bool state_fresh = true;   // spikes/v/r are logically zero (lazy reset)
   bool cur_fresh = true;     // currents are logically zero (lazy reset)
   // top-N selection fused into the LIF kernel (TopFuse)
-  DevBuf<TopCand> bcand;
+  DevBuf<uint64_t> bcand;
   DevBuf<uint32_t> bcnt;
   bool part_used = false;
   // input of the last accumulate (for the uniques pass)
@@ -564,7 +564,8 @@ static int lif_top_uniques(nk_counter *c, int streaming, hipStream_t s) {
   const uint64_t want = std::min<uint64_t>(c->opts.top_n, c->pool);
   const bool uniq = want && c->have_input && c->last_in.n_tiles;
   // top-N selection (and the uniques post step) inside the LIF kernel
-  const bool fused = want && want <= kFuseMaxTopN && lif_blocks(c->pool) <= kFuseMaxBlocks;
+  const bool fused = want && want <= kFuseMaxTopN && lif_blocks(c->pool) <= kFuseMaxBlocks &&
+                     c->pool <= (1ull << 24);
   if ((rc = enqueue_lif(c, streaming, fused ? (uint32_t)want : 0u, uniq && c->part_used, s)))
     return rc;
   HIPCHK(mark(c, 4, s));

@@ -67,7 +67,7 @@ constexpr uint32_t kFuseMaxTopN = 64;
 constexpr uint32_t kFuseMaxBlocks = 1024;
 struct TopFuse {
   uint32_t want;      // 0: not fused
-  TopCand *bcand;     // [blocks * want]
+  uint64_t *bcand;    // [blocks * want] keys (spikes << 24 | 0xFFFFFF - index)
   uint32_t *bcnt;     // [blocks]
   TopState *st;
   TopCand *cand;      // final rows, sorted

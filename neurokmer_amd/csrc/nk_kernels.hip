@@ -696,23 +696,6 @@ __device__ __forceinline__ bool cand_before(const TopCand &a, const TopCand &b) 
   return a.sc != b.sc ? a.sc > b.sc : a.idx < b.idx;
 }
 
-// Bitonic sort of one row per lane across a wave64 (registers + shuffles, no
-// LDS, no barriers): lane 0 ends with the first row by cand_before.  Empty
-// lanes carry {idx ~0, sc 0}, which sorts last.
-__device__ __forceinline__ TopCand wave_sort64(TopCand x) {
-  const int lane = threadIdx.x & 63;
-  for (int size = 2; size <= 64; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      TopCand y;
-      y.idx = __shfl_xor(x.idx, stride, 64);
-      y.sc = __shfl_xor(x.sc, stride, 64);
-      const bool up = (lane & size) == 0, lower = (lane & stride) == 0;
-      if (lower == up ? cand_before(y, x) : cand_before(x, y)) x = y;
-    }
-  }
-  return x;
-}
-
 // Exclusive prefix sum over the threads of a block (blockDim.x <= 1024, a
 // multiple of 64); *total gets the block sum.  Two barriers.
 template <typename T>
@@ -777,14 +760,44 @@ constexpr int kLifPerThread = 8;
 constexpr int kLifBlock = 1024;
 constexpr int kLifWaves = kLifBlock / 64;
 
+// Fused top-N keys: (spikes << 24) | (0xFFFFFF - index), so that descending
+// u64 order is exactly (spikes desc, index asc) (src/spiking_hash.rs:661-673).
+// Needs index < 2^24 (pool <= 2^24: the fused path's pool bound) and
+// spikes < 2^40 (else the selection defers to the host's exact path).
+constexpr int kKeyIdxBits = 24;
+constexpr uint64_t kKeyIdxMask = (1ull << kKeyIdxBits) - 1;
+constexpr uint64_t kKeyMaxSpikes = 1ull << 40;
+constexpr uint32_t kDeferMark = 0xFFFFFFFFu;  // bcnt of a block whose list could not be built
+__device__ __forceinline__ uint64_t top_key(uint64_t sc, uint64_t idx) {
+  return (sc << kKeyIdxBits) | (kKeyIdxMask - idx);
+}
+__device__ __forceinline__ uint64_t key_idx(uint64_t key) { return kKeyIdxMask - (key & kKeyIdxMask); }
+__device__ __forceinline__ uint64_t key_sc(uint64_t key) { return key >> kKeyIdxBits; }
+
+// Bitonic sort of one u64 per lane across a wave64, descending (registers +
+// shuffles).  Empty lanes carry 0.
+__device__ __forceinline__ uint64_t wave_sort64_desc(uint64_t x) {
+  const int lane = threadIdx.x & 63;
+  for (int size = 2; size <= 64; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const uint64_t y = __shfl_xor(x, stride, 64);
+      const bool up = (lane & size) == 0, lower = (lane & stride) == 0;
+      if (lower == up ? y > x : x > y) x = y;
+    }
+  }
+  return x;
+}
+
 // Block-local top `want` rows of this LIF block (want <= kFuseMaxTopN) from its
 // spike histogram `sh` (bin = min(spikes, 4095)): rows above the block
-// threshold in any order, then the threshold ties in index order.  Returns
-// false when the threshold falls in the clamp bin (exact refine on the host).
+// threshold, then the threshold ties in index order.  They go out as keys,
+// sorted descending, to gout, their number to *gcnt.  Returns false when the
+// threshold falls in the clamp bin or a count is too large for a key (the
+// final step then defers to the host's exact path).
 __device__ bool block_top(const uint32_t *sh, const uint64_t *scv, uint64_t base, uint64_t pool,
-                          uint32_t want, TopCand *out, TopCand *gout, uint32_t *gcnt) {
+                          uint32_t want, uint64_t *out, uint64_t *gout, uint32_t *gcnt) {
   __shared__ uint32_t s_w[kLifWaves];
-  __shared__ uint32_t s_T, s_above, s_need, s_n;
+  __shared__ uint32_t s_T, s_above, s_need, s_n, s_big;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   // thread t owns bins 4095-4t .. 4092-4t (counted from the top)
   uint32_t loc = 0;
@@ -796,6 +809,7 @@ __device__ bool block_top(const uint32_t *sh, const uint64_t *scv, uint64_t base
     s_above = total - sh[0];
     s_need = want - s_above;
     s_n = 0;
+    s_big = 0;
   }
   __syncthreads();
   if (total >= want && before < want && before + loc >= want) {
@@ -819,9 +833,8 @@ __device__ bool block_top(const uint32_t *sh, const uint64_t *scv, uint64_t base
   for (int j = 0; j < kLifPerThread; ++j) {
     const uint64_t i = base + (uint64_t)j * kLifBlock + t;
     if (i < pool && scv[j] > T) {
-      const uint32_t at = atomicAdd(&s_n, 1u);
-      out[at].idx = i;
-      out[at].sc = scv[j];
+      if (scv[j] >= kKeyMaxSpikes) s_big = 1;
+      out[atomicAdd(&s_n, 1u)] = top_key(scv[j], i);
     }
   }
   // ties: index order is (row j, thread t)
@@ -838,21 +851,16 @@ __device__ bool block_top(const uint32_t *sh, const uint64_t *scv, uint64_t base
       row += s_w[q];
     }
     const uint32_t r = pre + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-    if (tie && r < need) {
-      out[above + r].idx = i;
-      out[above + r].sc = T;
-    }
+    if (tie && r < need) out[above + r] = top_key(T, i);
     run += row;
     __syncthreads();
   }
   __syncthreads();
-  // this block's rows, sorted, to its candidate slot (wave 0)
-  if (t < 64) {
+  if (s_big) return false;
+  if (t < 64) {  // this block's rows, sorted, to its candidate slot (wave 0)
     const uint32_t n = above + (run < need ? run : need);
-    TopCand x;
-    if ((uint32_t)t < n) x = out[t];
-    else { x.idx = ~0ULL; x.sc = 0; }
-    x = wave_sort64(x);
+    uint64_t x = (uint32_t)t < n ? out[t] : 0ull;
+    x = wave_sort64_desc(x);
     if ((uint32_t)t < n) gout[t] = x;
     if (t == 0) *gcnt = n;
   }
@@ -861,72 +869,39 @@ __device__ bool block_top(const uint32_t *sh, const uint64_t *scv, uint64_t base
 
 // Selection left to the host's exact path: flag it, and leave the uniques pass
 // that is already queued with no work (no top buckets, no hits).
-__device__ void defer_to_host(const TopFuse &tf, uint64_t T, uint64_t n_above, uint64_t need) {
-  tf.st->T = T;
-  tf.st->n_above = n_above;
-  tf.st->need = need;
+__device__ void defer_to_host(const TopFuse &tf) {
+  tf.st->T = kHistBins - 1;
+  tf.st->n_above = 0;
+  tf.st->need = 0;
   tf.st->emit_above = 0;
   tf.st->refine = 1u;
   for (int i = 0; i < 4; ++i) tf.post.flags[i] = 0;
   *tf.post.n_hits = 0;
 }
 
-// The final selection: global threshold from the spike histogram copies, the
-// exact global rows from the block candidates, sort, post-processing.
-__device__ void final_top(const uint32_t *hist, uint64_t pool, const uint64_t *currents,
-                          uint32_t nb, const TopFuse &tf) {
-  __shared__ unsigned long long s_w64[kLifWaves];
+// The final selection over the blocks' candidate lists C (one block of
+// kLifBlock threads).  The global top rows are the top rows of C (every global
+// top row is in its block's list), so the threshold comes from a histogram of
+// C alone; ties at the threshold are taken in index order, which is block
+// order and, inside a block's list, list order.  Then the rows are sorted and
+// the uniques bookkeeping (k_top_post) is done by wave 0.
+__device__ void final_top(uint64_t pool, const uint64_t *currents, uint32_t nb,
+                          const TopFuse &tf) {
+  __shared__ uint32_t s_h[kHistBins];
   __shared__ uint32_t s_w32[kLifWaves];
-  __shared__ unsigned long long s_T, s_above, s_need;
-  __shared__ uint32_t s_na, s_bad;
+  __shared__ uint32_t s_T, s_above, s_need, s_na, s_bad;
   __shared__ uint32_t s_ab[kFuseMaxBlocks], s_tb[kFuseMaxBlocks];
-  __shared__ TopCand s_fin[kFuseMaxTopN];
+  __shared__ uint64_t s_fin[kFuseMaxTopN];
   const int t = threadIdx.x;
-  const uint64_t want = tf.want < pool ? tf.want : pool;
-  // (1) global threshold, as k_topn_threshold: 32 independent loads per thread
-  unsigned long long h4[4] = {0, 0, 0, 0};
-  {
-    uint4 hv[kHistCopies];  // bins 4092-4t .. 4095-4t of every copy: one round trip
-#pragma unroll
-    for (int c = 0; c < kHistCopies; ++c)
-      hv[c] = *reinterpret_cast<const uint4 *>(hist + c * kHistBins + kHistBins - 4 - 4 * t);
-#pragma unroll
-    for (int c = 0; c < kHistCopies; ++c) {
-      h4[0] += hv[c].w;
-      h4[1] += hv[c].z;
-      h4[2] += hv[c].y;
-      h4[3] += hv[c].x;
-    }
-  }
-  const unsigned long long loc = h4[0] + h4[1] + h4[2] + h4[3];
-  unsigned long long total;
-  const unsigned long long before = block_excl_scan(loc, s_w64, &total);
-  if (t == 0) { s_T = 0; s_above = total; s_need = 0; s_na = 0; s_bad = 0; }
-  if ((uint32_t)t < nb) { s_ab[t] = 0; s_tb[t] = 0; }
-  __syncthreads();
-  if (before < want && before + loc >= want) {
-    unsigned long long cum = before;
-    for (int j = 0; j < 4; ++j) {
-      if (cum + h4[j] >= want) {
-        s_T = (unsigned long long)(kHistBins - 1 - (4 * t + j));
-        s_above = cum;
-        s_need = want - cum;
-        break;
-      }
-      cum += h4[j];
-    }
-  }
-  __syncthreads();
-  const uint64_t T = s_T, n_above = s_above, need = s_need;
-  if (T == (uint64_t)(kHistBins - 1)) {  // spike counts >= 4095: host radix refine
-    if (t == 0) defer_to_host(tf, T, n_above, need);
-    return;
-  }
-  // (2) every block's sorted candidate list: rows above T (any order is fine,
-  // the final sort orders them) and the number of ties at T per block
+  const uint32_t want = (uint32_t)(tf.want < pool ? tf.want : pool);
   const uint32_t W = tf.want, M = nb * W;
+  for (int i = t; i < kHistBins; i += kLifBlock) s_h[i] = 0;
+  if ((uint32_t)t < nb) { s_ab[t] = 0; s_tb[t] = 0; }
+  if (t == 0) { s_na = 0; s_bad = 0; }
+  __syncthreads();
+  if ((uint32_t)t < nb && tf.bcnt[t] == kDeferMark) s_bad = 1;
   constexpr int U = 8;
-  TopCand cv[U];
+  uint64_t cv[U];
   uint32_t cn[U];
   // unconditional loads at clamped indices: the U loads of a chunk are in
   // flight together (one round trip); masked afterwards
@@ -939,62 +914,135 @@ __device__ void final_top(const uint32_t *hist, uint64_t pool, const uint64_t *c
       cv[u] = tf.bcand[id];
     }
   };
+  auto live = [&](uint32_t c0, int u) {
+    const uint32_t id = c0 + u * kLifBlock + t;
+    return id < M && id % W < cn[u];
+  };
+  const bool one_chunk = M <= (uint32_t)(U * kLifBlock);
+  __syncthreads();
+  // (1) histogram of the candidates' spike counts -> threshold T
   for (uint32_t c0 = 0; c0 < M; c0 += U * kLifBlock) {
     load_chunk(c0);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
+      if (!live(c0, u)) continue;
+      const uint64_t sc = key_sc(cv[u]);
+      atomicAdd(&s_h[sc < (uint64_t)(kHistBins - 1) ? (uint32_t)sc : (uint32_t)(kHistBins - 1)], 1u);
+    }
+  }
+  __syncthreads();
+  {
+    uint32_t loc = 0;
+    for (int j = 0; j < 4; ++j) loc += s_h[kHistBins - 1 - (4 * t + j)];
+    uint32_t total;
+    const uint32_t before = block_excl_scan(loc, s_w32, &total);
+    if (t == 0) { s_T = 0; s_above = total - s_h[0]; s_need = want - (total - s_h[0]); }
+    __syncthreads();
+    if (total >= want && before < want && before + loc >= want) {
+      uint32_t cum = before;
+      for (int j = 0; j < 4; ++j) {
+        const int bin = kHistBins - 1 - (4 * t + j);
+        if (cum + s_h[bin] >= want) {
+          s_T = (uint32_t)bin;
+          s_above = cum;
+          s_need = want - cum;
+          break;
+        }
+        cum += s_h[bin];
+      }
+    }
+    __syncthreads();
+  }
+  const uint64_t T = s_T;
+  const uint32_t n_above = s_above, need = s_need;
+  if (T == (uint64_t)(kHistBins - 1) || s_bad) {  // spike counts >= 4095: host radix refine
+    if (t == 0) defer_to_host(tf);
+    return;
+  }
+  // (2) rows above T (any order: sorted below) and per-list tie counts
+  for (uint32_t c0 = 0; c0 < M; c0 += U * kLifBlock) {
+    if (!one_chunk) load_chunk(c0);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!live(c0, u)) continue;
       const uint32_t id = c0 + u * kLifBlock + t;
-      if (id >= M || id % W >= cn[u]) continue;
-      if (cv[u].sc > T) {
+      const uint64_t sc = key_sc(cv[u]);
+      if (sc > T) {
         atomicAdd(&s_ab[id / W], 1u);
         const uint32_t at = atomicAdd(&s_na, 1u);
         if (at < kFuseMaxTopN) s_fin[at] = cv[u];
-      } else if (cv[u].sc == T) {
+      } else if (sc == T) {
         atomicAdd(&s_tb[id / W], 1u);
       }
     }
   }
   __syncthreads();
-  // ties: block order is index order, and each list holds its ties in index
-  // order right after its rows above T
   uint32_t ttot;
   const uint32_t tpre = block_excl_scan((uint32_t)t < nb ? s_tb[t] : 0u, s_w32, &ttot);
   if ((uint32_t)t < nb) s_tb[t] = tpre;
   if (t == 0 && (s_na != n_above || ttot < need)) s_bad = 1;  // cannot happen; be safe
   __syncthreads();
   if (s_bad) {
-    if (t == 0) defer_to_host(tf, T, n_above, need);
+    if (t == 0) defer_to_host(tf);
     return;
   }
+  // (3) ties: the first `need` in block order, list order inside a block
   for (uint32_t c0 = 0; c0 < M; c0 += U * kLifBlock) {
-    if (M > U * kLifBlock) load_chunk(c0);  // one chunk: still in registers
+    if (!one_chunk) load_chunk(c0);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
+      if (!live(c0, u) || key_sc(cv[u]) != T) continue;
       const uint32_t id = c0 + u * kLifBlock + t;
-      if (id >= M || id % W >= cn[u] || cv[u].sc != T) continue;
       const uint32_t b = id / W;
-      const uint64_t r = (uint64_t)s_tb[b] + (id % W - s_ab[b]);
+      const uint32_t r = s_tb[b] + (id % W - s_ab[b]);
       if (r < need) s_fin[n_above + r] = cv[u];
     }
   }
   __syncthreads();
-  // (3) exact order (wave 0), rows and their currents out
-  const uint32_t m = (uint32_t)want;
-  if (t < 64) {
-    TopCand x;
-    if ((uint32_t)t < m) x = s_fin[t];
-    else { x.idx = ~0ULL; x.sc = 0; }
-    x = wave_sort64(x);
-    if ((uint32_t)t < m) {
-      tf.cand[t] = x;
-      tf.top_cur[t] = currents[x.idx];
-    }
-    if (t == 0) { tf.st->T = T; tf.st->n_above = n_above; tf.st->need = need;
-                  tf.st->emit_above = n_above; tf.st->refine = 0u; }
+  if (t >= 64) return;
+  // (4) wave 0: exact order, rows and currents out, uniques bookkeeping
+  // (as k_top_post), all without block barriers
+  const int lane = t;
+  const uint32_t m = want;
+  const bool row = (uint32_t)lane < m;
+  const uint64_t key = wave_sort64_desc(row ? s_fin[lane] : 0ull);
+  const uint64_t idx = key_idx(key), sc = key_sc(key);
+  const uint64_t cur = row ? currents[idx] : 0ull;
+  const PostArgs &pa = tf.post;
+  const uint32_t bk = (uint32_t)(idx >> kBinBits);
+  const uint32_t over = (row && pa.part) ? pa.overflow[bk] : 0u;
+  if (row) {
+    tf.cand[lane].idx = idx;
+    tf.cand[lane].sc = sc;
+    tf.top_cur[lane] = cur;
+    pa.uniq[lane] = 0;
+    pa.special[lane] = 0;
   }
-  __syncthreads();
-  // (4) uniques bookkeeping on the final rows
-  top_post_block(tf.cand, tf.top_cur, m, tf.post);
+  unsigned long long sum = cur;
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+  bool first = row && pa.part;  // first row of its bucket in the list
+  for (int j = 0; j < 64; ++j) {
+    const uint32_t bj = __shfl(bk, j, 64);
+    if (j < lane && bj == bk) first = false;
+  }
+  const uint64_t fb = __ballot(first);
+  if (first) pa.tbuckets[__popcll(fb & ((1ull << lane) - 1ull))] = bk;
+  const bool any_over = __ballot(over != 0) != 0;
+  if (lane == 0) {
+    uint64_t cap = 64;
+    while (cap < 2 * (uint64_t)sum + 2) cap <<= 1;
+    pa.flags[0] = cap > pa.set_alloc ? 1u : 0u;  // set too small
+    pa.flags[1] = any_over ? 1u : 0u;            // a top bucket overflowed
+    pa.flags[2] = (uint32_t)__popcll(fb);        // distinct top buckets
+    pa.flags[3] = 0;
+    *pa.set_mask = (cap > pa.set_alloc ? pa.set_alloc : cap) - 1;
+    *pa.n_hits = 0;
+    tf.st->T = T;
+    tf.st->n_above = n_above;
+    tf.st->need = need;
+    tf.st->emit_above = n_above;
+    tf.st->refine = 0u;
+  }
 }
 
 __global__ __launch_bounds__(kLifBlock) void k_lif_apply(uint64_t *__restrict__ currents,
@@ -1011,30 +1059,57 @@ __global__ __launch_bounds__(kLifBlock) void k_lif_apply(uint64_t *__restrict__ 
   __shared__ uint32_t sh[kHistBins];
   __shared__ unsigned long long s_sp[kLifWaves];
   __shared__ unsigned long long s_mx[kLifWaves];
-  __shared__ TopCand s_cand[kFuseMaxTopN];
+  __shared__ uint64_t s_cand[kFuseMaxTopN];
   for (int i = threadIdx.x; i < kHistBins; i += kLifBlock) sh[i] = 0;
   __syncthreads();
   const uint64_t base = (uint64_t)blockIdx.x * kLifBlock * kLifPerThread;
   unsigned long long my_sp = 0, my_mx = 0;
-  uint64_t scv[kLifPerThread];
+  // all loads of this thread's neurons first (a few round trips), then the LIF
+  uint64_t cntv[kLifPerThread], scv[kLifPerThread];
+  float vin[kLifPerThread];
+  uint32_t rin[kLifPerThread];
+  auto idx_of = [&](int j) {  // clamped: unconditional loads
+    const uint64_t i = base + (uint64_t)j * kLifBlock + threadIdx.x;
+    return i < pool ? i : pool - 1;
+  };
+#pragma unroll
   for (int j = 0; j < kLifPerThread; ++j) {
-    scv[j] = 0;
-    uint64_t i = base + (uint64_t)j * kLifBlock + threadIdx.x;
-    if (i >= pool) break;
-    uint64_t cnt = currents[i];
-    if (slices) {  // fused K1c: fold the bucket histograms' partials in first
-      for (uint32_t r = 0; r < slices; ++r) cnt += partials[(uint64_t)r * pool + i];
-      currents[i] = cnt;
+    const uint64_t i = idx_of(j);
+    cntv[j] = currents[i];
+    scv[j] = fresh ? 0 : SC[i];
+    vin[j] = fresh ? 0.0f : V[i];
+    rin[j] = fresh ? 0u : R[i];
+  }
+  for (uint32_t r = 0; r < slices; ++r) {  // fused K1c: fold the partials in
+    const uint32_t *pr = partials + (uint64_t)r * pool;
+    uint32_t pv[kLifPerThread];
+#pragma unroll
+    for (int j = 0; j < kLifPerThread; ++j) pv[j] = pr[idx_of(j)];
+#pragma unroll
+    for (int j = 0; j < kLifPerThread; ++j) cntv[j] += pv[j];
+  }
+  LifEntry ev[kLifPerThread];  // closed-form table rows of fresh neurons
+#pragma unroll
+  for (int j = 0; j < kLifPerThread; ++j)
+    ev[j] = tbl[cntv[j] < (uint64_t)tbl_n ? cntv[j] : (uint64_t)tbl_n - 1];
+#pragma unroll
+  for (int j = 0; j < kLifPerThread; ++j) {
+    const uint64_t i = base + (uint64_t)j * kLifBlock + threadIdx.x;
+    if (i >= pool) {
+      scv[j] = 0;
+      continue;
     }
+    const uint64_t cnt = cntv[j];
+    if (slices) currents[i] = cnt;
     // fresh state (after nk_reset): v = r = spikes = 0 without reading them,
     // and every neuron is written
-    uint64_t sc = fresh ? 0 : SC[i];
+    uint64_t sc = scv[j];
     if (!(lp.skip_zero && cnt == 0) && lp.steps != 0) {
-      float v = fresh ? 0.0f : V[i];
-      uint32_t r = fresh ? 0u : R[i];
+      float v = vin[j];
+      uint32_t r = rin[j];
       uint64_t sp;
       if (v == 0.0f && r == 0 && cnt < (uint64_t)tbl_n) {
-        const LifEntry e = tbl[cnt];
+        const LifEntry e = ev[j];
         sp = e.spikes;
         v = e.v;
         r = e.r;
@@ -1071,24 +1146,25 @@ __global__ __launch_bounds__(kLifBlock) void k_lif_apply(uint64_t *__restrict__ 
   }
   // 8 copies of the global histogram (blocks b, b+8, ... share one), summed by
   // the threshold step: the hot spike-count bins see 8x fewer atomics each
-  uint32_t *hc = hist + (size_t)(blockIdx.x & (kHistCopies - 1)) * kHistBins;
-  for (int i = threadIdx.x; i < kHistBins; i += kLifBlock)
-    if (sh[i]) atomicAdd(&hc[i], sh[i]);
-  if (!tf.want) return;
+  if (!tf.want) {  // the separate top-N kernels read the global histogram
+    uint32_t *hc = hist + (size_t)(blockIdx.x & (kHistCopies - 1)) * kHistBins;
+    for (int i = threadIdx.x; i < kHistBins; i += kLifBlock)
+      if (sh[i]) atomicAdd(&hc[i], sh[i]);
+    return;
+  }
   // fused top-N: this block's candidates (the final step is k_top_final)
   if (!block_top(sh, scv, base, pool, tf.want, s_cand, tf.bcand + (uint64_t)blockIdx.x * tf.want,
                  tf.bcnt + blockIdx.x) &&
       threadIdx.x == 0)
-    tf.bcnt[blockIdx.x] = 0;  // the final step sees the clamp bin and defers to the host
+    tf.bcnt[blockIdx.x] = kDeferMark;  // the final step defers to the host's exact path
 }
 
-// After the LIF kernel (the kernel boundary makes every block's candidates,
-// histogram and currents visible): one block of kLifBlock threads.
-__global__ __launch_bounds__(kLifBlock) void k_top_final(const uint32_t *__restrict__ hist,
-                                                      uint64_t pool,
+// After the LIF kernel (the kernel boundary makes every block's candidates
+// and currents visible): one block of kLifBlock threads.
+__global__ __launch_bounds__(kLifBlock) void k_top_final(uint64_t pool,
                                                       const uint64_t *__restrict__ currents,
                                                       uint32_t nb, TopFuse tf) {
-  final_top(hist, pool, currents, nb, tf);
+  final_top(pool, currents, nb, tf);
 }
 
 // ---------------------------------------------------------------------------
@@ -1374,11 +1450,12 @@ hipError_t launch_lif_apply(uint64_t *currents, const uint32_t *partials, uint32
                             const TopFuse &tf, hipStream_t s) {
   if (!pool) return hipSuccess;
   const unsigned g = lif_blocks(pool);
-  if (tf.want && (tf.want > kFuseMaxTopN || g > kFuseMaxBlocks)) return hipErrorInvalidValue;
+  if (tf.want && (tf.want > kFuseMaxTopN || g > kFuseMaxBlocks || pool > (1ull << 24)))
+    return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_lif_apply, dim3(g), dim3(kLifBlock), 0, s, currents, partials, slices, fresh,
                      v, r, sc, pool, lp, tbl, tbl_n, hist, (unsigned long long *)stats, tf);
   if (tf.want)
-    hipLaunchKernelGGL(k_top_final, dim3(1), dim3(kLifBlock), 0, s, hist, pool, currents, g, tf);
+    hipLaunchKernelGGL(k_top_final, dim3(1), dim3(kLifBlock), 0, s, pool, currents, g, tf);
   return hipGetLastError();
 }
 
