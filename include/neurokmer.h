@@ -40,8 +40,12 @@ typedef struct nk_counter nk_counter;
 /* k-mer key width.  NK_KMER_COMPAT reproduces the reference's release-build
  * u64 semantics for every k (k > 32 keeps the last 32 forward bases and the
  * reference's masked-shift reverse strand, src/models.rs:188,192-194,260-266).
- * It is the only mode in ABI v1. */
+ * NK_KMER_128 is the build's true k <= 64 mode (not in the
+ * reference): u128 keys (canonical = min(fwd, rev) over 2k bits; non-canonical
+ * = pack_kmer in 128 bits), neuron = SipHash-1-3(key 0) over the key's 16 LE
+ * bytes % pool.  Its keys cross this ABI as (lo, hi) pairs of u64. */
 #define NK_KMER_COMPAT 0
+#define NK_KMER_128 1
 
 typedef struct nk_opts {
   int32_t device;        /* HIP device ordinal (default 0) */
@@ -99,7 +103,8 @@ int nk_finalize(nk_counter *c, int streaming_semantics, void *stream);
 /* After nk_finalize on a shard: the distinct k-mer keys of this shard that map
  * to the current top-N neurons (device buffer owned by the handle, valid until
  * the next call).  The caller gathers every shard's list and hands the union
- * to nk_merge_top_kmers(), which recomputes the uniques column exactly. */
+ * to nk_merge_top_kmers(), which recomputes the uniques column exactly.
+ * NK_KMER_128: the buffer holds n_keys (lo, hi) pairs (2 * n_keys u64). */
 int nk_top_kmers(nk_counter *c, const uint64_t **d_keys, size_t *n_keys);
 int nk_merge_top_kmers(nk_counter *c, const uint64_t *d_keys, size_t n_keys, void *stream);
 

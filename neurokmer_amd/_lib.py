@@ -22,6 +22,8 @@ NK_E_IO = -4
 NK_E_PARSE = -5
 NK_E_UNSUPPORTED = -6
 NK_E_DEVICE = -7
+NK_KMER_COMPAT = 0
+NK_KMER_128 = 1
 
 # every symbol include/neurokmer.h declares
 EXPORTS = (

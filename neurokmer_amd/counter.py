@@ -50,13 +50,18 @@ class EnergyTracker:
 class SpikingKmerCounter:
     def __init__(self, k: int, threshold: float, leak: float, refractory: int,
                  spike_cost: float, pool_size: int, use_canonical: bool, *,
-                 device: int = 0, top_n: int = 20, stage_timing: bool = False):
+                 device: int = 0, top_n: int = 20, stage_timing: bool = False,
+                 kmer_width: int = 64):
         self._L = _lib.load()
         o = NkOpts()
         self._L.nk_opts_default(C.byref(o))
         o.device = device
         o.top_n = top_n
         o.stage_timing = 1 if stage_timing else 0
+        if kmer_width not in (64, 128):
+            raise ValueError("kmer_width must be 64 (the reference's u64 keys) or 128")
+        o.kmer_width = _lib.NK_KMER_128 if kmer_width == 128 else _lib.NK_KMER_COMPAT
+        self.kmer_width = kmer_width
         self._h = None
         h = self._L.nk_new(k, threshold, leak, refractory, spike_cost, pool_size,
                            1 if use_canonical else 0, C.byref(o))
@@ -110,7 +115,8 @@ class SpikingKmerCounter:
         check(self._L.nk_finalize(self._h, 1 if streaming else 0, stream or None))
 
     def top_kmers_device(self):
-        """-> (device pointer, count) of this shard's distinct top-N k-mer keys."""
+        """-> (device pointer, count) of this shard's distinct top-N k-mer keys
+        (kmer_width 128: count (lo, hi) u64 pairs)."""
         p = C.c_void_p()
         n = C.c_size_t()
         check(self._L.nk_top_kmers(self._h, C.byref(p), C.byref(n)))

@@ -101,7 +101,8 @@ struct nk_counter {
   DevBuf<unsigned long long> top_keys_n;
   DevBuf<uint32_t> radix_h;
   uint64_t set_cap = 0;     // capacity used by the last uniques pass
-  uint64_t set_alloc = 0;   // allocated capacity of set_keys
+  uint64_t set_alloc = 0;   // allocated capacity of set_keys (keys)
+  bool w128 = false;        // --kmer-width=128: u128 keys, 3 set words per key
   size_t n_top_keys = 0;
   DevBuf<uint64_t> set_mask_d, set_need_d;
   DevBuf<unsigned long long> hits, n_hits;  // uniques hit records (cap = set_alloc / 2)
@@ -236,8 +237,12 @@ nk_counter *nk_new(size_t k, float threshold, float leak, uint32_t refractory, d
   nk_opts o;
   if (opts) o = *opts;
   else nk_opts_default(&o);
-  if (o.kmer_width != NK_KMER_COMPAT) {
-    fail(NK_E_UNSUPPORTED, "kmer_width %d not supported in ABI v1", o.kmer_width);
+  if (o.kmer_width != NK_KMER_COMPAT && o.kmer_width != NK_KMER_128) {
+    fail(NK_E_INVALID, "kmer_width %d unknown", o.kmer_width);
+    return nullptr;
+  }
+  if (o.kmer_width == NK_KMER_128 && k > 64) {
+    fail(NK_E_INVALID, "kmer_width 128 needs k <= 64 (k = %zu)", k);
     return nullptr;
   }
   if (o.top_n > (uint32_t)kMaxTopN) {
@@ -273,6 +278,7 @@ nk_counter *nk_new(size_t k, float threshold, float leak, uint32_t refractory, d
   c->cost = spike_cost;
   c->canonical = use_canonical ? 1 : 0;
   c->opts = o;
+  c->w128 = o.kmer_width == NK_KMER_128;
   c->device = o.device;
   bool ok = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) == hipSuccess;
   for (int i = 0; ok && i <= kStages; ++i) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
@@ -282,7 +288,7 @@ nk_counter *nk_new(size_t k, float threshold, float leak, uint32_t refractory, d
        !c->cand.ensure(kMaxTopN) && !c->top_cur.ensure(kMaxTopN) &&
        !c->uniq.ensure(kMaxTopN) && !c->special.ensure(kMaxTopN) &&
        !c->top_keys_n.ensure(1) && !c->radix_h.ensure(256) && !c->set_mask_d.ensure(1) &&
-       !c->set_need_d.ensure(1) && !c->post_flags.ensure(4) && !c->set_keys.ensure(1 << 20) &&
+       !c->set_need_d.ensure(1) && !c->post_flags.ensure(4) && !c->set_keys.ensure((o.kmer_width == NK_KMER_128 ? 3 : 1) << 20) &&
        !c->hits.ensure(1 << 19) && !c->n_hits.ensure(1) &&
        hipHostMalloc((void **)&c->res_h, nk_counter::kResBytes,
                      hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
@@ -350,7 +356,7 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
   in.n_recs = n_recs;
   in.n_bases = n_bases;
   const uint64_t B = (c->pool + kBinsPerBucket - 1) >> kBinBits;
-  const bool part = c->k <= 32 && c->pool > 0 && B <= (uint64_t)kMaxBuckets;
+  const bool part = !c->w128 && c->k <= 32 && c->pool > 0 && B <= (uint64_t)kMaxBuckets;
   const uint64_t tile = part ? kPartTile : kTile;
   in.n_tiles = n_tiles_for(n_bases, tile);
   int rc = c->tile_rec.ensure(std::max<uint64_t>(in.n_tiles, 1));
@@ -405,7 +411,10 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
       HIPCHK(launch_partials_add(c->partials.p, slices, c->pool, c->cur.p, s));
     c->last_pa = pa;
   } else {
-    HIPCHK(launch_count(in, (int)c->k, c->canonical, c->pool, c->cur.p, s));
+    if (c->w128)
+      HIPCHK(launch_count128(in, (int)c->k, c->canonical, c->pool, c->cur.p, s));
+    else
+      HIPCHK(launch_count(in, (int)c->k, c->canonical, c->pool, c->cur.p, s));
     HIPCHK(mark(c, 2, s));
   }
   HIPCHK(mark(c, 3, s));
@@ -524,7 +533,9 @@ static int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, bool post_don
   if (!post_done) HIPCHK(launch_top_post(c->cand.p, c->top_cur.p, m, c->set_alloc, part ? c->p_over.p : nullptr,
                          part ? 1 : 0, c->set_mask_d.p, c->tbuckets.p, c->post_flags.p, c->uniq.p,
                          c->special.p, c->n_hits.p, s));
-  if (!part) HIPCHK(launch_set_fill(c->set_keys.p, c->set_mask_d.p, c->set_alloc, s));
+  if (!part)
+    HIPCHK(c->w128 ? launch_set_fill128(c->set_keys.p, c->set_mask_d.p, c->set_alloc, s)
+                   : launch_set_fill(c->set_keys.p, c->set_mask_d.p, c->set_alloc, s));
   UniqArgs u{};
   u.top = c->cand.p;
   u.n_top = m;
@@ -544,7 +555,10 @@ static int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, bool post_don
     if ((rc = c->tile_rec.ensure(std::max<uint64_t>(in.n_tiles, 1)))) return rc;
     in.tile_rec = c->tile_rec.p;
     HIPCHK(launch_tile_rec(in, kTile, c->tile_rec.p, s));
-    HIPCHK(launch_uniques(in, (int)c->k, c->canonical, c->pool, u, s));
+    if (c->w128)
+      HIPCHK(launch_uniques128(in, (int)c->k, c->canonical, c->pool, u, s));
+    else
+      HIPCHK(launch_uniques(in, (int)c->k, c->canonical, c->pool, u, s));
   }
   return NK_OK;
 }
@@ -603,7 +617,7 @@ static int lif_top_uniques(nk_counter *c, int streaming, hipStream_t s) {
       HIPCHK(hipStreamSynchronize(s));
       for (uint64_t x : tc) sum += x;
       while (cap < 2 * sum + 2) cap <<= 1;
-      if ((rc = c->set_keys.ensure(cap))) return rc;
+      if ((rc = c->set_keys.ensure(c->w128 ? 3 * cap : cap))) return rc;
       if ((rc = c->hits.ensure(cap / 2))) return rc;
       c->set_alloc = cap;
     }
@@ -747,10 +761,13 @@ int nk_top_kmers(nk_counter *c, const uint64_t **d_keys, size_t *n_keys) {
     return NK_OK;
   }
   int rc;
-  if ((rc = c->top_keys.ensure(c->set_cap + 1))) return rc;
+  if ((rc = c->top_keys.ensure(c->w128 ? 2 * c->set_cap : c->set_cap + 1))) return rc;
   HIPCHK(hipMemsetAsync(c->top_keys_n.p, 0, 8, s));
-  HIPCHK(launch_set_compact(c->set_keys.p, c->set_cap, c->special.p, m, c->cand.p, c->pool,
-                            c->top_keys.p, c->top_keys_n.p, s));
+  if (c->w128)  // (lo, hi) pairs
+    HIPCHK(launch_set_compact128(c->set_keys.p, c->set_cap, c->top_keys.p, c->top_keys_n.p, s));
+  else
+    HIPCHK(launch_set_compact(c->set_keys.p, c->set_cap, c->special.p, m, c->cand.p, c->pool,
+                              c->top_keys.p, c->top_keys_n.p, s));
   unsigned long long n = 0;
   HIPCHK(hipMemcpyAsync(&n, c->top_keys_n.p, 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
@@ -769,12 +786,13 @@ int nk_merge_top_kmers(nk_counter *c, const uint64_t *d_keys, size_t n_keys, voi
   while (cap < 2 * (uint64_t)n_keys + 2) cap <<= 1;
   int rc;
   if (cap > c->set_alloc) {
-    if ((rc = c->set_keys.ensure(cap))) return rc;
+    if ((rc = c->set_keys.ensure(c->w128 ? 3 * cap : cap))) return rc;
     c->set_alloc = cap;
   }
   c->set_cap = cap;
   HIPCHK(launch_set_word(c->set_mask_d.p, cap - 1, s));
-  HIPCHK(launch_set_fill(c->set_keys.p, c->set_mask_d.p, c->set_alloc, s));
+  HIPCHK(c->w128 ? launch_set_fill128(c->set_keys.p, c->set_mask_d.p, c->set_alloc, s)
+                 : launch_set_fill(c->set_keys.p, c->set_mask_d.p, c->set_alloc, s));
   HIPCHK(hipMemsetAsync(c->uniq.p, 0, m * 4, s));
   HIPCHK(hipMemsetAsync(c->special.p, 0, m * 4, s));
   UniqArgs u{};
@@ -785,7 +803,10 @@ int nk_merge_top_kmers(nk_counter *c, const uint64_t *d_keys, size_t n_keys, voi
   u.set_mask = c->set_mask_d.p;
   u.uniq = c->uniq.p;
   u.special = c->special.p;
-  HIPCHK(launch_set_merge(d_keys, n_keys, c->pool, u, s));
+  if (c->w128)
+    HIPCHK(launch_set_merge128(d_keys, n_keys, c->pool, u, s));
+  else
+    HIPCHK(launch_set_merge(d_keys, n_keys, c->pool, u, s));
   uint32_t *hu = reinterpret_cast<uint32_t *>(c->res_h);
   HIPCHK(hipMemcpyAsync(hu, c->uniq.p, m * 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));

@@ -55,6 +55,30 @@ __device__ __forceinline__ uint64_t sip13_u64(uint64_t m) {
   return v0 ^ v1 ^ v2 ^ v3;
 }
 
+// --kmer-width=128: SipHash-1-3 (key 0) over the 16 LE bytes of a u128 key:
+// two message blocks (lo, hi), then the length block (16 << 56), three
+// finalization rounds (oracle/nk_oracle.c nko_sip13_u128).
+__device__ __forceinline__ uint64_t sip13_u128(uint64_t lo, uint64_t hi) {
+  uint64_t v0 = 0x736f6d6570736575ULL;
+  uint64_t v1 = 0x646f72616e646f6dULL;
+  uint64_t v2 = 0x6c7967656e657261ULL;
+  uint64_t v3 = 0x7465646279746573ULL ^ lo;
+  NK_SIPROUND;
+  v0 ^= lo;
+  v3 ^= hi;
+  NK_SIPROUND;
+  v0 ^= hi;
+  const uint64_t b = 16ULL << 56;
+  v3 ^= b;
+  NK_SIPROUND;
+  v0 ^= b;
+  v2 ^= 0xffULL;
+  NK_SIPROUND;
+  NK_SIPROUND;
+  NK_SIPROUND;
+  return v0 ^ v1 ^ v2 ^ v3;
+}
+
 // Exact h % P for any P >= 1 given magic = floor((2^64-1)/P):
 // q = mulhi(h, magic) is floor(h/P) - {0,1,2}, so at most two corrections.
 struct FastMod {

@@ -153,6 +153,19 @@ hipError_t launch_top_post(const TopCand *top, const uint64_t *top_cur, uint32_t
                            uint64_t *set_mask, uint32_t *tbuckets, uint32_t *flags,
                            uint32_t *uniq, uint32_t *special, unsigned long long *n_hits,
                            hipStream_t s);
+// --kmer-width=128 (k <= 64): the count, the top rows' uniques (set of 3
+// words per slot, u.set_keys), and the set helpers; keys outside the set are
+// (lo, hi) pairs of u64.
+hipError_t launch_count128(const KmerInput &in, int k, int canonical, uint64_t pool,
+                           uint64_t *currents, hipStream_t s);
+hipError_t launch_uniques128(const KmerInput &in, int k, int canonical, uint64_t pool,
+                             const UniqArgs &u, hipStream_t s);
+hipError_t launch_set_fill128(unsigned long long *set3, const uint64_t *mask, uint64_t max_cap,
+                              hipStream_t s);
+hipError_t launch_set_compact128(const unsigned long long *set3, uint64_t cap, uint64_t *out,
+                                 unsigned long long *count, hipStream_t s);
+hipError_t launch_set_merge128(const uint64_t *keys, uint64_t n, uint64_t pool, const UniqArgs &u,
+                               hipStream_t s);
 hipError_t launch_set_word(uint64_t *w, uint64_t v, hipStream_t s);
 // tile -> first record index for the count kernels, fused with a zero list
 hipError_t launch_prep(const KmerInput &in, uint64_t tile_size, uint32_t *tile_rec,

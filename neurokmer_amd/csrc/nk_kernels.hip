@@ -228,6 +228,128 @@ __global__ __launch_bounds__(kBlock) void k_kmers_compat(KmerInput in, int k, Fa
 }
 
 // ---------------------------------------------------------------------------
+// --kmer-width=128 (k <= 64): count (MODE 0: global atomics) and uniques of the
+// top rows (MODE 1) over u128 keys.
+//
+// The uniques set holds a key as three 43-bit chunks in u64 words whose bit
+// 63 marks the word written.  Word 0 is claimed by CAS; a lane that matches
+// word 0 of a slot another lane is still publishing polls again on its next
+// loop iteration (never spins inside one), so no store ordering, fence or
+// intra-wave wait is needed, and distinct keys are counted exactly.
+// ---------------------------------------------------------------------------
+constexpr uint64_t kW128Valid = 1ull << 63;
+constexpr uint64_t kW128Mask = (1ull << 43) - 1;
+__device__ __forceinline__ void key128_words(const Key128 &k, uint64_t w[3]) {
+  w[0] = (k.lo & kW128Mask) | kW128Valid;
+  w[1] = (((k.lo >> 43) | (k.hi << 21)) & kW128Mask) | kW128Valid;
+  w[2] = (k.hi >> 22) | kW128Valid;
+}
+__device__ __forceinline__ Key128 words_key128(uint64_t w0, uint64_t w1, uint64_t w2) {
+  Key128 k;
+  w0 &= kW128Mask;
+  w1 &= kW128Mask;
+  w2 &= ~kW128Valid;
+  k.lo = w0 | (w1 << 43);
+  k.hi = (w1 >> 21) | (w2 << 22);
+  return k;
+}
+__device__ __forceinline__ void set_insert128(const UniqArgs &u, uint32_t slot, const Key128 &key) {
+  uint64_t w[3];
+  key128_words(key, w);
+  const uint64_t mask = *u.set_mask;
+  unsigned long long *S = u.set_keys;  // 3 words per slot
+  uint64_t h = mix64(key.lo ^ mix64(key.hi)) & mask;
+  for (;;) {
+    unsigned long long cur = __hip_atomic_load(&S[3 * h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == 0) {
+      const unsigned long long prev = atomicCAS(&S[3 * h], 0ull, (unsigned long long)w[0]);
+      if (prev == 0) {
+        __hip_atomic_store(&S[3 * h + 1], (unsigned long long)w[1], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&S[3 * h + 2], (unsigned long long)w[2], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        atomicAdd(&u.uniq[slot], 1u);
+        return;
+      }
+      cur = prev;
+    }
+    if (cur == w[0]) {
+      const unsigned long long a =
+          __hip_atomic_load(&S[3 * h + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long b =
+          __hip_atomic_load(&S[3 * h + 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!(a & kW128Valid) || !(b & kW128Valid)) continue;  // being published: poll again
+      if (a == w[1] && b == w[2]) return;
+    }
+    h = (h + 1) & mask;
+  }
+}
+
+template <bool CANON, int MODE>
+__global__ __launch_bounds__(kBlock) void k_kmers128(KmerInput in, int k, FastMod fm,
+                                                     unsigned long long *__restrict__ currents,
+                                                     UniqArgs u) {
+  __shared__ TileLds<kTile, !CANON> L;
+  extern __shared__ uint64_t dyn[];  // MODE 1: probe table
+  uint64_t *tbl_idx = dyn;
+  uint32_t *tbl_slot = reinterpret_cast<uint32_t *>(dyn + (MODE == 1 ? u.tbl_size : 0));
+  if (MODE == 1) build_top_tbl(u, tbl_idx, tbl_slot);  // contains __syncthreads
+  const uint64_t T0 = (uint64_t)blockIdx.x * kTile;
+  stage_tile<kTile, kBlock, !CANON>(L, in, blockIdx.x, k);
+#pragma unroll 2
+  for (int j = 0; j < kPerThread; ++j) {
+    const int q = j * kBlock + threadIdx.x;
+    if (T0 + (uint64_t)q + (uint64_t)k > in.n_bases) break;
+    if (!window_valid(L, T0, q, k, in.n_bases)) continue;
+    const Key128 key = window_key128<kTile, !CANON, CANON>(L, q, k);
+    const uint64_t idx = fastmod(sip13_u128(key.lo, key.hi), fm);
+    if (MODE == 0) {
+      atomicAdd(&currents[idx], 1ULL);
+    } else {
+      const int slot = probe_top(tbl_idx, tbl_slot, u.tbl_size - 1, idx);
+      if (slot >= 0) set_insert128(u, (uint32_t)slot, key);
+    }
+  }
+}
+
+__global__ void k_set_fill128(unsigned long long *__restrict__ S, const uint64_t *__restrict__ mask) {
+  const uint64_t n = 3 * (*mask + 1);
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    S[i] = 0;
+}
+
+// the set's keys as (lo, hi) pairs
+__global__ void k_set_compact128(const unsigned long long *__restrict__ S, uint64_t cap,
+                                 uint64_t *__restrict__ out, unsigned long long *__restrict__ count) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long w0 = S[3 * i];
+    if (!w0) continue;
+    const Key128 k = words_key128(w0, S[3 * i + 1], S[3 * i + 2]);
+    const unsigned long long at = atomicAdd(count, 1ull);
+    out[2 * at] = k.lo;
+    out[2 * at + 1] = k.hi;
+  }
+}
+
+// the union of several ranks' top k-mers ((lo, hi) pairs) into the set
+__global__ void k_set_merge128(const uint64_t *__restrict__ keys, uint64_t n, FastMod fm,
+                               UniqArgs u) {
+  extern __shared__ uint64_t dyn[];
+  uint64_t *tbl_idx = dyn;
+  uint32_t *tbl_slot = reinterpret_cast<uint32_t *>(dyn + u.tbl_size);
+  build_top_tbl(u, tbl_idx, tbl_slot);
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const Key128 key{keys[2 * i], keys[2 * i + 1]};
+    const uint64_t idx = fastmod(sip13_u128(key.lo, key.hi), fm);
+    const int slot = probe_top(tbl_idx, tbl_slot, u.tbl_size - 1, idx);
+    if (slot >= 0) set_insert128(u, (uint32_t)slot, key);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // K1 partitioned (k <= 32, pool <= 256 * 32768): the MI355X-native count.
 //
 // Random per-k-mer global atomics run at the memory side (~20 G/s chip-wide),
@@ -1507,6 +1629,54 @@ hipError_t launch_set_fill(unsigned long long *keys, const uint64_t *mask, uint6
   if (g > 2048) g = 2048;
   if (!g) return hipSuccess;
   hipLaunchKernelGGL(k_set_fill, dim3(g), dim3(256), 0, s, keys, mask);
+  return hipGetLastError();
+}
+
+// --kmer-width=128
+template <int MODE>
+static hipError_t launch_kmers128(const KmerInput &in, int k, int canonical, uint64_t pool,
+                                  unsigned long long *cur, const UniqArgs &u, hipStream_t s) {
+  if (!in.n_tiles) return hipSuccess;
+  if (k < 1 || k > 64) return hipErrorInvalidValue;
+  FastMod fm = make_fastmod(pool);
+  dim3 g((unsigned)in.n_tiles), b(kBlock);
+  size_t dyn = MODE == 1 ? tbl_bytes(u) : 0;
+  if (canonical) hipLaunchKernelGGL((k_kmers128<true, MODE>), g, b, dyn, s, in, k, fm, cur, u);
+  else hipLaunchKernelGGL((k_kmers128<false, MODE>), g, b, dyn, s, in, k, fm, cur, u);
+  return hipGetLastError();
+}
+hipError_t launch_count128(const KmerInput &in, int k, int canonical, uint64_t pool,
+                           uint64_t *currents, hipStream_t s) {
+  UniqArgs u{};
+  return launch_kmers128<0>(in, k, canonical, pool, (unsigned long long *)currents, u, s);
+}
+hipError_t launch_uniques128(const KmerInput &in, int k, int canonical, uint64_t pool,
+                             const UniqArgs &u, hipStream_t s) {
+  return launch_kmers128<1>(in, k, canonical, pool, nullptr, u, s);
+}
+hipError_t launch_set_fill128(unsigned long long *set3, const uint64_t *mask, uint64_t max_cap,
+                              hipStream_t s) {
+  unsigned g = (unsigned)((3 * max_cap + 255) / 256);
+  if (g > 2048) g = 2048;
+  if (!g) return hipSuccess;
+  hipLaunchKernelGGL(k_set_fill128, dim3(g), dim3(256), 0, s, set3, mask);
+  return hipGetLastError();
+}
+hipError_t launch_set_compact128(const unsigned long long *set3, uint64_t cap, uint64_t *out,
+                                 unsigned long long *count, hipStream_t s) {
+  unsigned g = (unsigned)((cap + 255) / 256);
+  if (g > 4096) g = 4096;
+  if (!g) g = 1;
+  hipLaunchKernelGGL(k_set_compact128, dim3(g), dim3(256), 0, s, set3, cap, out, count);
+  return hipGetLastError();
+}
+hipError_t launch_set_merge128(const uint64_t *keys, uint64_t n, uint64_t pool, const UniqArgs &u,
+                               hipStream_t s) {
+  if (!n) return hipSuccess;
+  unsigned g = (unsigned)((n + 255) / 256);
+  if (g > 2048) g = 2048;
+  hipLaunchKernelGGL(k_set_merge128, dim3(g), dim3(256), tbl_bytes(u), s, keys, n,
+                     make_fastmod(pool), u);
   return hipGetLastError();
 }
 

@@ -172,6 +172,72 @@ __device__ __forceinline__ uint64_t window_key(const TileLds<TILE, RAW> &L, int 
   }
 }
 
+// --kmer-width=128 key of the window at local position q (k <= 64): the 128
+// bases from q out of five code words, fwd = the top 2k bits (MSB-first
+// stream), rev = the low 2k bits of the LSB-first complement stream;
+// canonical = min as u128.  Non-canonical: pack_kmer in 128 bits.
+struct Key128 {
+  uint64_t lo, hi;
+};
+__device__ __forceinline__ bool key128_less(const Key128 &a, const Key128 &b) {
+  return a.hi != b.hi ? a.hi < b.hi : a.lo < b.lo;
+}
+template <int TILE, bool RAW, bool CANON>
+__device__ __forceinline__ Key128 window_key128(const TileLds<TILE, RAW> &L, int q, int k) {
+  const int w = q >> 4, s = 2 * (q & 15);
+  uint32_t W[4];  // bases q .. q+63, MSB-first, W[0] most significant
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    W[c] = (uint32_t)(((((uint64_t)L.F[w + c] << 32) | L.F[w + c + 1]) << s) >> 32);
+  uint64_t vhi = ((uint64_t)W[0] << 32) | W[1], vlo = ((uint64_t)W[2] << 32) | W[3];
+  // fwd = V >> (128 - 2k)
+  const int sh = 128 - 2 * k;  // 0 .. 126
+  Key128 fwd;
+  if (sh >= 64) {
+    fwd.lo = vhi >> (sh - 64);
+    fwd.hi = 0;
+  } else if (sh == 0) {
+    fwd.lo = vlo;
+    fwd.hi = vhi;
+  } else {
+    fwd.lo = (vlo >> sh) | (vhi << (64 - sh));
+    fwd.hi = vhi >> sh;
+  }
+  if (CANON) {
+    uint32_t Y[4];  // LSB-first complement stream from bit s: Y[0] least significant
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      Y[c] = (uint32_t)(((((uint64_t)L.R[w + c + 1] << 32) | L.R[w + c]) >> s));
+    Key128 rev;
+    rev.lo = ((uint64_t)Y[1] << 32) | Y[0];
+    rev.hi = ((uint64_t)Y[3] << 32) | Y[2];
+    if (k < 32) {
+      rev.lo &= (1ULL << (2 * k)) - 1ULL;
+      rev.hi = 0;
+    } else if (k < 64) {
+      rev.hi &= (1ULL << (2 * k - 64)) - 1ULL;
+    }
+    return key128_less(rev, fwd) ? rev : fwd;
+  } else {
+    const int iw = q >> 4, is = q & 15;
+    const uint64_t z0 = ((uint64_t)L.INV[iw] | ((uint64_t)L.INV[iw + 1] << 16) |
+                         ((uint64_t)L.INV[iw + 2] << 32) | ((uint64_t)L.INV[iw + 3] << 48));
+    const uint64_t z = (z0 >> is) | (is ? ((uint64_t)L.INV[iw + 4] << (64 - is)) : 0ULL);
+    const uint64_t kmask = k >= 64 ? ~0ULL : ((1ULL << k) - 1ULL);
+    if (!(z & kmask)) return fwd;
+    const uint8_t *raw = reinterpret_cast<const uint8_t *>(L.RAWB);
+    Key128 pk{0, 0};
+    for (int i = 0; i < k; ++i) {
+      uint8_t bb = raw[q + i];
+      if (valid_byte(bb)) {
+        pk.hi = (pk.hi << 2) | (pk.lo >> 62);
+        pk.lo = (pk.lo << 2) | code_of(bb);
+      }
+    }
+    return pk;
+  }
+}
+
 // Same key straight from global memory (rare: uniques hits only).
 template <bool CANON>
 __device__ __forceinline__ uint64_t global_window_key(const uint8_t *b, uint64_t p, int k) {

@@ -68,6 +68,16 @@ def lib():
         L.nko_top_abundant.argtypes = [C.c_void_p, C.c_size_t, u64p, u64p, u32p]
         L.nko_get_count.restype = C.c_int
         L.nko_get_count.argtypes = [C.c_void_p, C.c_uint64, u32p]
+        # --kmer-width=128
+        L.nko_sip13_u128.restype = C.c_uint64
+        L.nko_sip13_u128.argtypes = [C.c_uint64, C.c_uint64]
+        L.nko_kmer_keys128.restype = C.c_size_t
+        L.nko_kmer_keys128.argtypes = [u8p, C.c_size_t, C.c_size_t, C.c_int, u64p]
+        L.nko_new_w.restype = C.c_void_p
+        L.nko_new_w.argtypes = [C.c_size_t, C.c_float, C.c_float, C.c_uint32, C.c_double,
+                                C.c_size_t, C.c_int, C.c_int]
+        L.nko_get_count128.restype = C.c_int
+        L.nko_get_count128.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, u32p]
         _lib = L
     return _lib
 
@@ -94,6 +104,20 @@ def kmer_keys(seq: bytes, k: int, canonical: bool) -> np.ndarray:
     return out[:m]
 
 
+def sip13_u128(key: int) -> int:
+    return int(lib().nko_sip13_u128(key & (2**64 - 1), key >> 64))
+
+
+def kmer_keys128(seq: bytes, k: int, canonical: bool) -> list:
+    """--kmer-width=128 keys of one record as Python ints."""
+    n = max(0, len(seq) - k + 1)
+    out = np.zeros(2 * max(n, 1), np.uint64)
+    buf = np.frombuffer(seq, dtype=np.uint8) if seq else np.zeros(1, np.uint8)
+    m = lib().nko_kmer_keys128(_ptr(buf, C.c_uint8), len(seq), k, int(canonical),
+                               _ptr(out, C.c_uint64))
+    return [int(out[2 * i]) | (int(out[2 * i + 1]) << 64) for i in range(m)]
+
+
 def lif(count, steps, thr, leak, refr, skip_zero, v=0.0, r=0, spikes=0):
     cv, cr, cs = C.c_float(v), C.c_uint32(r), C.c_uint64(spikes)
     lib().nko_lif(count, steps, thr, leak, refr, int(skip_zero), C.byref(cv), C.byref(cr),
@@ -112,11 +136,15 @@ def records_to_arrays(seqs):
 class OracleCounter:
     """SpikingKmerCounter restated in C (see oracle/nk_oracle.h)."""
 
-    def __init__(self, k, threshold, leak, refractory, spike_cost, pool_size, use_canonical):
+    def __init__(self, k, threshold, leak, refractory, spike_cost, pool_size, use_canonical,
+                 width=64):
         self._L = lib()
         self.pool = pool_size
-        self._h = self._L.nko_new(k, threshold, leak, refractory, spike_cost, pool_size,
-                                  int(use_canonical))
+        self.width = width
+        self._h = self._L.nko_new_w(k, threshold, leak, refractory, spike_cost, pool_size,
+                                    int(use_canonical), width)
+        if not self._h:
+            raise ValueError("bad width/k")
 
     def __del__(self):
         if getattr(self, "_h", None):
@@ -199,4 +227,8 @@ class OracleCounter:
 
     def get_count(self, kmer):
         out = C.c_uint32(0)
-        return int(out.value) if self._L.nko_get_count(self._h, kmer, C.byref(out)) else None
+        if self.width == 128:
+            ok = self._L.nko_get_count128(self._h, kmer & (2**64 - 1), kmer >> 64, C.byref(out))
+        else:
+            ok = self._L.nko_get_count(self._h, kmer, C.byref(out))
+        return int(out.value) if ok else None

@@ -165,6 +165,71 @@ size_t nko_kmer_keys(const uint8_t *seq, size_t len, size_t k, int canonical, ui
 }
 
 /* ------------------------------------------------------------------------ */
+/* --kmer-width=128: the build's true k<=64 mode.  Not in  */
+/* the reference; defined here and restated on the device:                   */
+/*   canonical: fwd = sum code(b_i) << 2(k-1-i), rev = sum comp(b_i) << 2i    */
+/*     over the window (A1 codes: other bytes -> 0 on both strands),         */
+/*     key = min(fwd, rev) as u128;                                          */
+/*   non-canonical: pack_kmer in u128 (skips non-ACGT, keeps the last 64);   */
+/*   neuron = SipHash-1-3(key 0) over the key's 16 LE bytes (what u128::hash */
+/*     feeds SipHasher13: Hasher::write_u128 -> to_ne_bytes) % pool.         */
+/* ------------------------------------------------------------------------ */
+uint64_t nko_sip13_u128(uint64_t lo, uint64_t hi) {
+  uint8_t le[16];
+  for (int i = 0; i < 8; ++i) le[i] = (uint8_t)(lo >> (8 * i));
+  for (int i = 0; i < 8; ++i) le[8 + i] = (uint8_t)(hi >> (8 * i));
+  return nko_siphash(1, 3, 0, 0, le, 16);
+}
+
+typedef unsigned __int128 u128;
+typedef void (*emit128_fn)(u128 key, void *ctx);
+static void record_kmers128(const uint8_t *seq, size_t len, size_t k, int canonical,
+                            emit128_fn emit, void *ctx) {
+  if (len < k) return;
+  const u128 mask = k >= 64 ? ~(u128)0 : (((u128)1 << (2 * k)) - 1);
+  if (canonical) {
+    u128 fwd = 0, rev = 0;
+    for (size_t i = 0; i < k; ++i) fwd = ((fwd << 2) | base_to_bits(seq[i])) & mask;
+    for (size_t i = k; i-- > 0;) rev = ((rev << 2) | base_to_comp_bits(seq[i])) & mask;
+    emit(fwd < rev ? fwd : rev, ctx);
+    for (size_t i = 1; i + k <= len; ++i) {
+      const uint8_t nx = seq[i + k - 1];
+      fwd = ((fwd << 2) | base_to_bits(nx)) & mask;
+      rev = (rev >> 2) | ((u128)base_to_comp_bits(nx) << (2 * (k - 1)));
+      emit(fwd < rev ? fwd : rev, ctx);
+    }
+  } else {
+    for (size_t i = 0; i + k <= len; ++i) {
+      u128 packed = 0;
+      for (size_t j = 0; j < k; ++j) {
+        const uint8_t b = seq[i + j];
+        if (b == 'A' || b == 'a' || b == 'C' || b == 'c' || b == 'G' || b == 'g' || b == 'T' ||
+            b == 't')
+          packed = (packed << 2) | base_to_bits(b);
+      }
+      emit(packed, ctx);
+    }
+  }
+}
+
+typedef struct { uint64_t *out; size_t n; } collect128_ctx;
+static void collect128_emit(u128 key, void *ctx) {
+  collect128_ctx *c = (collect128_ctx *)ctx;
+  c->out[2 * c->n] = (uint64_t)key;
+  c->out[2 * c->n + 1] = (uint64_t)(key >> 64);
+  c->n++;
+}
+size_t nko_kmer_keys128(const uint8_t *seq, size_t len, size_t k, int canonical, uint64_t *out) {
+  collect128_ctx c = {out, 0};
+  if (k == 0 || k > 64) return 0;
+  record_kmers128(seq, len, k, canonical, collect128_emit, &c);
+  return c.n;
+}
+static uint64_t map128(u128 key, uint64_t pool) {
+  return nko_sip13_u128((uint64_t)key, (uint64_t)(key >> 64)) % pool;
+}
+
+/* ------------------------------------------------------------------------ */
 /* Exact k-mer map (the reference's HashMap<u64,u32> / DashMap<u64,AtomicU32>)*/
 /* Open addressing, linear probing; counts wrap at 2^32 like the AtomicU32.   */
 /* ------------------------------------------------------------------------ */
@@ -224,6 +289,58 @@ static int kmap_get(const kmap_t *m, uint64_t key, uint32_t *out) {
   return 0;
 }
 
+/* the same map over u128 keys (--kmer-width=128) */
+typedef struct {
+  u128 *keys;
+  uint32_t *vals;
+  uint8_t *used;
+  size_t cap, n;
+} kmap128_t;
+static inline uint64_t mix128(u128 k) { return mix64((uint64_t)k ^ mix64((uint64_t)(k >> 64))); }
+static void kmap128_init(kmap128_t *m, size_t cap_hint) {
+  size_t cap = 64;
+  while (cap < cap_hint * 2) cap <<= 1;
+  m->cap = cap;
+  m->n = 0;
+  m->keys = (u128 *)malloc(cap * sizeof(u128));
+  m->vals = (uint32_t *)malloc(cap * sizeof(uint32_t));
+  m->used = (uint8_t *)calloc(cap, 1);
+}
+static void kmap128_free(kmap128_t *m) {
+  free(m->keys); free(m->vals); free(m->used);
+  memset(m, 0, sizeof(*m));
+}
+static void kmap128_add(kmap128_t *m, u128 key, uint32_t v);
+static void kmap128_grow(kmap128_t *m) {
+  kmap128_t nm;
+  kmap128_init(&nm, m->cap);
+  for (size_t i = 0; i < m->cap; ++i)
+    if (m->used[i]) kmap128_add(&nm, m->keys[i], m->vals[i]);
+  kmap128_free(m);
+  *m = nm;
+}
+static void kmap128_add(kmap128_t *m, u128 key, uint32_t v) {
+  if ((m->n + 1) * 2 > m->cap) kmap128_grow(m);
+  size_t msk = m->cap - 1, i = mix128(key) & msk;
+  while (m->used[i]) {
+    if (m->keys[i] == key) { m->vals[i] += v; return; }
+    i = (i + 1) & msk;
+  }
+  m->used[i] = 1;
+  m->keys[i] = key;
+  m->vals[i] = v;
+  m->n++;
+}
+static int kmap128_get(const kmap128_t *m, u128 key, uint32_t *out) {
+  if (!m->cap) return 0;
+  size_t msk = m->cap - 1, i = mix128(key) & msk;
+  while (m->used[i]) {
+    if (m->keys[i] == key) { *out = m->vals[i]; return 1; }
+    i = (i + 1) & msk;
+  }
+  return 0;
+}
+
 /* ------------------------------------------------------------------------ */
 /* LifNeuron (src/models.rs:9-51) and EnergyTracker (:145-173)               */
 /* ------------------------------------------------------------------------ */
@@ -269,13 +386,19 @@ struct nko_counter {
   uint64_t *currents;
   uint32_t *kpn;
   kmap_t counts;
+  int width;           /* 64: the reference's u64 keys; 128: --kmer-width=128 */
+  kmap128_t counts128; /* counts when width == 128 */
   /* energy */
   uint64_t total_spikes, total_energy;
 };
 
-nko_counter *nko_new(size_t k, float threshold, float leak, uint32_t refractory,
-                     double spike_cost, size_t pool_size, int use_canonical) {
+nko_counter *nko_new_w(size_t k, float threshold, float leak, uint32_t refractory,
+                       double spike_cost, size_t pool_size, int use_canonical, int width) {
+  if (width != 64 && width != 128) return NULL;
+  if (width == 128 && (k == 0 || k > 64)) return NULL;
   nko_counter *c = (nko_counter *)calloc(1, sizeof(*c));
+  c->width = width;
+  kmap128_init(&c->counts128, 16);
   c->k = k; c->pool = pool_size; c->thr = threshold; c->leak = leak;
   c->refr = refractory; c->cost = spike_cost; c->canonical = use_canonical;
   c->steps = 1000; /* src/spiking_hash.rs:70 */
@@ -289,10 +412,16 @@ nko_counter *nko_new(size_t k, float threshold, float leak, uint32_t refractory,
   return c;
 }
 
+nko_counter *nko_new(size_t k, float threshold, float leak, uint32_t refractory,
+                     double spike_cost, size_t pool_size, int use_canonical) {
+  return nko_new_w(k, threshold, leak, refractory, spike_cost, pool_size, use_canonical, 64);
+}
+
 void nko_free(nko_counter *c) {
   if (!c) return;
   free(c->v); free(c->r); free(c->sc); free(c->currents); free(c->kpn);
   kmap_free(&c->counts);
+  kmap128_free(&c->counts128);
   free(c);
 }
 
@@ -310,12 +439,20 @@ typedef struct {
   size_t next; /* record work queue: rayon's work unit is one record (:94-95) */
   pthread_mutex_t mu;
   kmap_t *maps; /* one map per record, like `maps.push(local_counts)` (:141) */
+  kmap128_t *maps128; /* width 128 */
 } fold_shared;
 
 typedef struct {
   fold_shared *s;
   uint64_t *currents; /* per-split `vec![0u64; pool_size]` (:97) */
 } fold_arg;
+
+typedef struct { uint64_t *currents; kmap128_t *map; uint64_t pool; } rec128_ctx;
+static void rec128_emit(u128 key, void *vctx) {
+  rec128_ctx *x = (rec128_ctx *)vctx;
+  kmap128_add(x->map, key, 1);
+  x->currents[map128(key, x->pool)] += 1;
+}
 
 typedef struct { uint64_t *currents; kmap_t *map; uint8_t *unique; uint64_t pool; } rec_ctx;
 static void rec_emit(uint64_t key, void *vctx) {
@@ -337,6 +474,12 @@ static void *fold_worker(void *p) {
     if (i >= s->n_recs) break;
     const uint8_t *seq = s->bases + s->offsets[i];
     size_t len = (size_t)(s->offsets[i + 1] - s->offsets[i]);
+    if (c->width == 128) {
+      kmap128_init(&s->maps128[i], 16);
+      rec128_ctx x = {a->currents, &s->maps128[i], c->pool};
+      record_kmers128(seq, len, c->k, c->canonical, rec128_emit, &x);
+      continue;
+    }
     uint8_t *unique = (uint8_t *)calloc(c->pool ? c->pool : 1, 1); /* :100 */
     kmap_init(&s->maps[i], 16);
     rec_ctx x = {a->currents, &s->maps[i], unique, c->pool};
@@ -363,6 +506,7 @@ static int accumulate(nko_counter *c, const uint8_t *bases, const uint64_t *offs
   s.c = c; s.bases = bases; s.offsets = offsets; s.n_recs = n_recs; s.next = 0;
   pthread_mutex_init(&s.mu, NULL);
   s.maps = (kmap_t *)calloc(n_recs ? n_recs : 1, sizeof(kmap_t));
+  s.maps128 = (kmap128_t *)calloc(n_recs ? n_recs : 1, sizeof(kmap128_t));
   fold_arg *args = (fold_arg *)calloc((size_t)n_threads, sizeof(fold_arg));
   pthread_t *th = (pthread_t *)calloc((size_t)n_threads, sizeof(pthread_t));
   for (int t = 0; t < n_threads; ++t) {
@@ -381,20 +525,33 @@ static int accumulate(nko_counter *c, const uint8_t *bases, const uint64_t *offs
     free(args[t].currents);
   }
   /* counts.clear(); merge the local maps serially (:157-165) */
-  kmap_free(&c->counts);
-  kmap_init(&c->counts, 16);
-  for (size_t i = 0; i < n_recs; ++i) {
-    kmap_t *m = &s.maps[i];
-    for (size_t j = 0; j < m->cap; ++j)
-      if (m->used[j]) kmap_add(&c->counts, m->keys[j], m->vals[j]);
-    kmap_free(m);
-  }
-  /* kmer_per_neuron rebuild (:167-172) */
   memset(c->kpn, 0, P * sizeof(uint32_t));
-  for (size_t j = 0; j < c->counts.cap; ++j)
-    if (c->counts.used[j]) c->kpn[nko_map_kmer(c->counts.keys[j], c->pool)] += 1;
+  if (c->width == 128) {
+    kmap128_free(&c->counts128);
+    kmap128_init(&c->counts128, 16);
+    for (size_t i = 0; i < n_recs; ++i) {
+      kmap128_t *m = &s.maps128[i];
+      for (size_t j = 0; j < m->cap; ++j)
+        if (m->used[j]) kmap128_add(&c->counts128, m->keys[j], m->vals[j]);
+      kmap128_free(m);
+    }
+    for (size_t j = 0; j < c->counts128.cap; ++j)
+      if (c->counts128.used[j]) c->kpn[map128(c->counts128.keys[j], c->pool)] += 1;
+  } else {
+    kmap_free(&c->counts);
+    kmap_init(&c->counts, 16);
+    for (size_t i = 0; i < n_recs; ++i) {
+      kmap_t *m = &s.maps[i];
+      for (size_t j = 0; j < m->cap; ++j)
+        if (m->used[j]) kmap_add(&c->counts, m->keys[j], m->vals[j]);
+      kmap_free(m);
+    }
+    /* kmer_per_neuron rebuild (:167-172) */
+    for (size_t j = 0; j < c->counts.cap; ++j)
+      if (c->counts.used[j]) c->kpn[nko_map_kmer(c->counts.keys[j], c->pool)] += 1;
+  }
   pthread_mutex_destroy(&s.mu);
-  free(s.maps); free(args); free(th);
+  free(s.maps); free(s.maps128); free(args); free(th);
   return 0;
 }
 
@@ -435,13 +592,23 @@ static void seq_emit(uint64_t key, void *vctx) {
   x->c->currents[idx] += 1;
   x->unique[idx] = 1;
 }
+static void seq128_emit(u128 key, void *vctx) {
+  seq_ctx *x = (seq_ctx *)vctx;
+  uint64_t idx = map128(key, x->c->pool);
+  kmap128_add(&x->c->counts128, key, 1);
+  x->c->currents[idx] += 1;
+  x->unique[idx] = 1;
+}
 int nko_process_sequence(nko_counter *c, const uint8_t *seq, size_t len) {
   if (c->k == 0) return -1;
   if (len < c->k) return 0;
   if (c->pool == 0) return -1;
   uint8_t *unique = (uint8_t *)calloc(c->pool, 1);
   seq_ctx x = {c, unique};
-  record_kmers(seq, len, c->k, c->canonical, seq_emit, &x);
+  if (c->width == 128)
+    record_kmers128(seq, len, c->k, c->canonical, seq128_emit, &x);
+  else
+    record_kmers(seq, len, c->k, c->canonical, seq_emit, &x);
   for (size_t i = 0; i < c->pool; ++i)
     if (unique[i]) c->kpn[i] += 1;
   for (size_t i = 0; i < c->pool; ++i) {
@@ -462,7 +629,9 @@ const uint32_t *nko_kmer_per_neuron(const nko_counter *c) { return c->kpn; }
 uint64_t nko_total_spikes(const nko_counter *c) { return c->total_spikes; }
 uint64_t nko_total_energy_fixed(const nko_counter *c) { return c->total_energy; }
 double nko_energy_used(const nko_counter *c) { return (double)c->total_energy / 1000.0; }
-size_t nko_distinct_kmers(const nko_counter *c) { return c->counts.n; }
+size_t nko_distinct_kmers(const nko_counter *c) {
+  return c->width == 128 ? c->counts128.n : c->counts.n;
+}
 void nko_set_steps(nko_counter *c, uint64_t steps) { c->steps = steps; }
 uint64_t nko_get_steps(const nko_counter *c) { return c->steps; }
 
@@ -488,6 +657,10 @@ size_t nko_top_abundant(const nko_counter *c, size_t n, uint64_t *idx, uint64_t 
   }
   free(t);
   return m;
+}
+
+int nko_get_count128(const nko_counter *c, uint64_t lo, uint64_t hi, uint32_t *out) {
+  return kmap128_get(&c->counts128, ((u128)hi << 64) | lo, out);
 }
 
 int nko_get_count(const nko_counter *c, uint64_t kmer, uint32_t *out) {

@@ -40,6 +40,12 @@ uint64_t nko_siphash(int c_rounds, int d_rounds, uint64_t k0, uint64_t k1,
                      const uint8_t *msg, size_t len);
 /* SipHasher13::new_with_keys(0,0); u64::hash -> write_u64 (8 LE bytes); finish(). */
 uint64_t nko_sip13_u64(uint64_t m);
+/* --kmer-width=128 (the build's own mode, see nk_oracle.c):
+ * SipHash-1-3 (key 0) over the 16 LE bytes of a u128 (lo word first). */
+uint64_t nko_sip13_u128(uint64_t lo, uint64_t hi);
+/* 128-bit keys of one record, as (lo, hi) pairs; returns the key count. */
+size_t nko_kmer_keys128(const uint8_t *seq, size_t len, size_t k, int canonical,
+                        uint64_t *out);
 /* map_kmer_to_neuron: src/spiking_hash.rs:78-82 */
 uint64_t nko_map_kmer(uint64_t kmer, uint64_t pool);
 /* pack_kmer: src/utils.rs:26-39 */
@@ -58,6 +64,9 @@ typedef struct nko_counter nko_counter;
 
 nko_counter *nko_new(size_t k, float threshold, float leak, uint32_t refractory,
                      double spike_cost, size_t pool_size, int use_canonical);
+/* width 64 (= nko_new) or 128 (k <= 64); NULL on a bad width/k */
+nko_counter *nko_new_w(size_t k, float threshold, float leak, uint32_t refractory,
+                       double spike_cost, size_t pool_size, int use_canonical, int width);
 void nko_free(nko_counter *c);
 /* records = bases[offsets[i] .. offsets[i+1]), i < n_recs.  n_threads >= 1:
  * records are distributed over threads like rayon's par_iter (work unit = one
@@ -84,6 +93,7 @@ size_t nko_top_abundant(const nko_counter *c, size_t n, uint64_t *idx,
                         uint64_t *spikes, uint32_t *uniques);
 /* 1 and *out set if present, 0 if absent */
 int nko_get_count(const nko_counter *c, uint64_t kmer, uint32_t *out);
+int nko_get_count128(const nko_counter *c, uint64_t lo, uint64_t hi, uint32_t *out);
 
 #ifdef __cplusplus
 }

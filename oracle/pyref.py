@@ -116,6 +116,42 @@ def pack_kmer(window: bytes) -> int:
     return packed
 
 
+M128 = (1 << 128) - 1
+
+
+def sip13_u128(key: int) -> int:
+    """--kmer-width=128: SipHash-1-3 (key 0) over the u128's 16 LE bytes
+    (Hasher::write_u128 -> to_ne_bytes on a little-endian host)."""
+    return siphash(1, 3, 0, 0, (key & M128).to_bytes(16, "little"))
+
+
+def kmer_keys128(seq: bytes, k: int, canonical: bool) -> list[int]:
+    """--kmer-width=128 keys (the build's own mode), written per
+    window rather than rolled, as an independent check of oracle/nk_oracle.c:
+    fwd = sum code(b_i) << 2(k-1-i), rev = sum comp(b_i) << 2i, key = min;
+    non-canonical: pack_kmer in 128 bits."""
+    if not 1 <= k <= 64:
+        raise ValueError("k must be in 1..64")
+    out = []
+    for i in range(0, len(seq) - k + 1):
+        w = seq[i:i + k]
+        if canonical:
+            fwd = 0
+            for b in w:
+                fwd = (fwd << 2) | _FWD.get(b, 0)
+            rev = 0
+            for j, b in enumerate(w):
+                rev |= _CMP.get(b, 0) << (2 * j)
+            out.append(min(fwd, rev))
+        else:
+            packed = 0
+            for b in w:
+                if b in _FWD:
+                    packed = ((packed << 2) & M128) | _FWD[b]
+            out.append(packed)
+    return out
+
+
 def kmer_keys(seq: bytes, k: int, canonical: bool) -> list[int]:
     """The keys the reference derives from one record (src/spiking_hash.rs:102-138)."""
     if k <= 0:

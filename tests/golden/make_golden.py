@@ -49,6 +49,47 @@ def lif_table():
     return rows
 
 
+def width128():
+    """--kmer-width=128 (the build's own mode): SipHash-1-3 over
+    16-byte keys, key derivation cases and one small end-to-end case, all from
+    oracle/pyref.py's per-window restatement."""
+    ks = [0, 1, 2**64 - 1, 2**64, 2**64 + 1, 2**127, 2**128 - 1,
+          0x0123456789ABCDEF_FEDCBA9876543210]
+    ks += [int(a) | (int(b) << 64) for a, b in zip(synth.random_words(12, seed=78),
+                                                 synth.random_words(12, seed=79))]
+    kats = [{"key": str(k), "sip13": pyref.sip13_u128(k)} for k in ks]
+    bases, offs = synth.make_records(2000, 1, seed=6, n_rate=0.01, mixed_case=True)
+    seq = bases.tobytes()[:400]
+    cases = []
+    for k in (1, 21, 32, 33, 47, 63, 64):
+        for canon in (False, True):
+            cases.append({"k": k, "canonical": canon,
+                          "keys": [str(x) for x in pyref.kmer_keys128(seq, k, canon)]})
+    # end to end: currents, LIF (steps 1000), top-20 with distinct keys per neuron
+    k, pool = 63, 701
+    eb, eo = synth.make_records(9000, 3, seed=8, repeats_per_mb=40000, motif_len=90,
+                                n_rate=0.002)
+    recs = synth.records_list(eb, eo)
+    cur = [0] * pool
+    distinct = [set() for _ in range(pool)]
+    for r in recs:
+        for key in pyref.kmer_keys128(r, k, True):
+            i = pyref.sip13_u128(key) % pool
+            cur[i] += 1
+            distinct[i].add(key)
+    sc, vb, rr = [], [], []
+    for c in cur:
+        v, r_, sp = pyref.lif_run(c, 1000, 1.0, 0.95, 2, True)
+        sc.append(sp); vb.append(pyref.f32_bits(v)); rr.append(r_)
+    order = sorted(range(pool), key=lambda i: (-sc[i], i))[:20]
+    e2e128 = {"k": k, "pool": pool, "canonical": True,
+              "records": [x.decode("latin-1") for x in recs], "currents": cur,
+              "spike_counts": sc, "voltage_bits": vb, "refractory": rr,
+              "total_spikes": sum(sc),
+              "top20": [[i, sc[i], len(distinct[i])] for i in order]}
+    return {"sip13_u128": kats, "seq": seq.decode("latin-1"), "cases": cases, "e2e": e2e128}
+
+
 CASES = [
     # name, total bases, records, k, pool, canonical, streaming, extra synth kwargs, steps
     ("noncanon_k21_p1000", 4000, 5, 21, 1000, False, False, dict(n_rate=0.01, mixed_case=True), None),
@@ -86,6 +127,7 @@ def main():
     json.dump(sip_kats(), open(os.path.join(HERE, "sip13_kat.json"), "w"))
     json.dump(key_cases(), open(os.path.join(HERE, "kmer_keys.json"), "w"))
     json.dump(lif_table(), open(os.path.join(HERE, "lif_table_default.json"), "w"))
+    json.dump(width128(), open(os.path.join(HERE, "width128.json"), "w"))
     for case in CASES:
         json.dump(e2e(*case), open(os.path.join(HERE, f"e2e_{case[0]}.json"), "w"))
     print("golden fixtures written to", HERE)

@@ -5,6 +5,7 @@ Every comparison is bit-exact: u64 currents, u64 spike counts, f32 voltages
 "unique k-mers colliding".  Inputs are seeded synthetic records with N runs,
 lowercase bases, other IUPAC bytes, empty records and records shorter than k.
 """
+import json
 import os
 import subprocess
 
@@ -20,6 +21,8 @@ if not torch.cuda.is_available():
 from neurokmer_amd import SpikingKmerCounter, synth  # noqa: E402
 from neurokmer_amd import _lib  # noqa: E402
 from oracle import cbind, pyref  # noqa: E402
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 def ragged_records(total=60_000, seed=7, max_len=4000, **kw):
@@ -50,9 +53,9 @@ def assert_same(gpu, ref, n=20):
 
 
 def run_both(bases, offs, k, pool, canon, thr=1.0, leak=0.95, refr=2, cost=1.0, steps=None,
-             top_n=20, streaming=False):
-    g = SpikingKmerCounter(k, thr, leak, refr, cost, pool, canon, top_n=top_n)
-    r = cbind.OracleCounter(k, thr, leak, refr, cost, pool, canon)
+             top_n=20, streaming=False, width=64):
+    g = SpikingKmerCounter(k, thr, leak, refr, cost, pool, canon, top_n=top_n, kmer_width=width)
+    r = cbind.OracleCounter(k, thr, leak, refr, cost, pool, canon, width=width)
     if steps is not None:
         g.set_steps(steps)
         r.set_steps(steps)
@@ -235,6 +238,63 @@ def test_split_phase_two_shards_equals_whole():
     r = cbind.OracleCounter(21, 1.0, 0.95, 2, 1.0, 9001, True)
     r.process_parallel_arrays(bases, offs)
     assert_same(a, r)
+
+
+# ---- --kmer-width=128 (the build's true k <= 64 mode) -------
+@pytest.mark.parametrize("canon", [True, False])
+@pytest.mark.parametrize("k", [1, 17, 32, 33, 47, 63, 64])
+def test_width128_parity(k, canon):
+    bases, offs = ragged_records(n_rate=0.01, mixed_case=True, seed=211 + k)
+    g, r = run_both(bases, offs, k, 5003, canon, width=128)
+    assert_same(g, r)
+
+
+def test_width128_repeats_large_pool():
+    # config 5's shape in small: k=63, a pool past the fused top-N bound, repeats
+    bases, offs = synth.make_records(400_000, 5, repeats_per_mb=20_000, motif_len=120, seed=41)
+    g, r = run_both(bases, offs, 63, (1 << 24) + 3, True, width=128)
+    assert_same(g, r)
+
+
+def test_width128_golden_e2e():
+    d = json.load(open(os.path.join(GOLD, "width128.json")))["e2e"]
+    g = SpikingKmerCounter(d["k"], 1.0, 0.95, 2, 1.0, d["pool"], True, kmer_width=128)
+    g.process_parallel([x.encode("latin-1") for x in d["records"]])
+    assert list(g.currents()) == d["currents"]
+    assert list(g.spike_counts()) == d["spike_counts"]
+    assert list(g.voltages().view(np.uint32)) == d["voltage_bits"]
+    assert [list(t) for t in g.top_abundant_neurons(20)] == d["top20"]
+
+
+def test_width128_split_phase_two_shards():
+    bases, offs = synth.make_records(200_000, 6, repeats_per_mb=9000, motif_len=70, seed=29)
+    sh = []
+    for lo, hi in ((0, 3), (3, 6)):
+        b = bases[int(offs[lo]):int(offs[hi])]
+        o = (offs[lo:hi + 1] - offs[lo]).astype(np.uint64)
+        sh.append((torch.from_numpy(np.concatenate([b, np.zeros(16, np.uint8)])).cuda(),
+                   torch.from_numpy(o.view(np.int64)).cuda(), hi - lo, b.size))
+    torch.cuda.synchronize()
+    cs = [SpikingKmerCounter(45, 1.0, 0.95, 2, 1.0, 7001, True, kmer_width=128) for _ in sh]
+    for c, x in zip(cs, sh):
+        c.accumulate_device(x[0].data_ptr(), x[1].data_ptr(), x[2], x[3])
+    tot = cs[0].currents() + cs[1].currents()
+    t = torch.from_numpy(tot.view(np.int64)).cuda()
+    for c in cs:
+        cur = torch.as_tensor(_CAI(c.device_currents_ptr(), tot.size), device="cuda")
+        cur.copy_(t)
+        torch.cuda.synchronize()
+        c.finalize(False)
+    keys = []
+    for c in cs:
+        p, n = c.top_kmers_device()  # n (lo, hi) pairs
+        keys.append(torch.as_tensor(_CAI(p, 2 * n), device="cuda").clone() if n
+                    else torch.zeros(0, dtype=torch.int64, device="cuda"))
+    allk = torch.cat(keys)
+    cs[0].merge_top_kmers(allk.data_ptr(), allk.numel() // 2)
+    r = cbind.OracleCounter(45, 1.0, 0.95, 2, 1.0, 7001, True, width=128)
+    r.process_parallel_arrays(bases, offs)
+    assert_same(cs[0], r)
 
 
 class _CAI:

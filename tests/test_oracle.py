@@ -288,3 +288,25 @@ def test_device_window_model_matches_reference():
                         else:
                             key = fwd
                         assert key == want[q], (seed, k, canon, q)
+
+
+def test_width128_oracle_matches_golden():
+    """--kmer-width=128 (the build's own mode): the C
+    restatement against fixtures from the independent per-window Python
+    restatement (tests/golden/make_golden.py width128)."""
+    d = json.load(open(os.path.join(GOLD, "width128.json")))
+    for e in d["sip13_u128"]:
+        assert cbind.sip13_u128(int(e["key"])) == e["sip13"]
+    seq = d["seq"].encode("latin-1")
+    for c in d["cases"]:
+        got = cbind.kmer_keys128(seq, c["k"], c["canonical"])
+        assert [str(x) for x in got] == c["keys"], (c["k"], c["canonical"])
+    e = d["e2e"]
+    o = cbind.OracleCounter(e["k"], 1.0, 0.95, 2, 1.0, e["pool"], True, width=128)
+    o.process_parallel([r.encode("latin-1") for r in e["records"]])
+    assert list(o.currents()) == e["currents"]
+    assert list(o.spike_counts()) == e["spike_counts"]
+    assert list(o.voltages().view(np.uint32)) == e["voltage_bits"]
+    assert list(o.refractory()) == e["refractory"]
+    assert o.total_spikes == e["total_spikes"]
+    assert [list(t) for t in o.top_abundant_neurons(20)] == e["top20"]
