@@ -49,14 +49,21 @@ typedef struct nk_counter nk_counter;
 
 typedef struct nk_opts {
   int32_t device;        /* HIP device ordinal (default 0) */
-  int32_t kmer_width;    /* NK_KMER_COMPAT */
+  int32_t kmer_width;    /* NK_KMER_COMPAT (default) or NK_KMER_128 */
   uint32_t top_n;        /* neurons whose "unique k-mers colliding" are tracked
                             by every process call (default 20 = src/main.rs:50) */
   uint32_t stage_timing; /* 0 (default): HIP events around the count kernel only
                             (nk_last_timings: index, count, post, total);
                             1: an event between every stage (each costs ~6 us
                             of GPU idle time on MI355X) */
-  uint32_t reserved[12];
+  uint32_t exact_counts; /* 1: also build the exact k-mer count table on the
+                            device (the reference's `counts` DashMap and the full
+                            `kmer_per_neuron`, src/spiking_hash.rs:27,157-172):
+                            enables nk_get_count(s), nk_copy_kmer_per_neuron,
+                            nk_distinct_kmers and nk_process_sequence.
+                            NK_KMER_COMPAT only.  Default 0: the metric's path,
+                            uniques for the top rows only. */
+  uint32_t reserved[11];
 } nk_opts;
 
 /* Fills *o with the defaults above. */
@@ -123,9 +130,25 @@ typedef struct nk_top_row {
 } nk_top_row;
 long nk_top_abundant_neurons(nk_counter *c, size_t n, nk_top_row *out);
 
-/* SpikingKmerCounter::get_count(&self, kmer) — src/spiking_hash.rs:675-682.
- * ABI v1: NK_E_UNSUPPORTED (the exact k-mer table is not built on device yet). */
+/* SpikingKmerCounter::get_count(&self, kmer) — src/spiking_hash.rs:675-682:
+ * *present = 1 and *out = the k-mer's count (u32, wrapping like AtomicU32), or
+ * *present = 0.  Needs nk_opts.exact_counts (else NK_E_UNSUPPORTED). */
 int nk_get_count(nk_counter *c, uint64_t kmer, uint32_t *out, int *present);
+/* SpikingKmerCounter::process_sequence(&mut self, seq) — src/spiking_hash.rs:
+ * 203-273: one record; counts[key] += 1 per k-mer, currents[H(key) % P] += 1
+ * on top of the currents already held, kmer_per_neuron[idx] += 1 per neuron
+ * the record touches, then ONE LifNeuron::update(current as f32) for every
+ * neuron with current > 0 and currents = 0.  len < k: no-op.  Needs
+ * nk_opts.exact_counts (the uniques column is kmer_per_neuron). */
+int nk_process_sequence(nk_counter *c, const uint8_t *seq, size_t len);
+/* Batched get_count over host arrays (out[i], present[i] per key). */
+int nk_get_counts(nk_counter *c, const uint64_t *kmers, size_t n, uint32_t *out,
+                  uint8_t *present);
+/* Number of distinct k-mers in the table (the reference's counts.len()). */
+long nk_distinct_kmers(nk_counter *c);
+/* The full `kmer_per_neuron` (src/spiking_hash.rs:28,167-172,262-267): out[i]
+ * for every neuron i < pool (n must equal pool_size).  Needs exact_counts. */
+int nk_copy_kmer_per_neuron(nk_counter *c, uint32_t *out, size_t n);
 
 /* EnergyTracker / accessors — src/models.rs:145-173, src/spiking_hash.rs:684-695 */
 uint64_t nk_total_spikes(const nk_counter *c);        /* energy.total_spikes() */

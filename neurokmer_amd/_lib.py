@@ -29,7 +29,8 @@ NK_KMER_128 = 1
 EXPORTS = (
     "nk_opts_default", "nk_new", "nk_free", "nk_process_parallel", "nk_process_parallel_device",
     "nk_process_file_streaming", "nk_accumulate_device", "nk_finalize", "nk_top_kmers",
-    "nk_merge_top_kmers", "nk_top_abundant_neurons", "nk_get_count", "nk_total_spikes",
+    "nk_merge_top_kmers", "nk_top_abundant_neurons", "nk_get_count", "nk_get_counts",
+    "nk_distinct_kmers", "nk_copy_kmer_per_neuron", "nk_process_sequence", "nk_total_spikes",
     "nk_energy_used", "nk_set_steps", "nk_get_steps", "nk_pool_size", "nk_k",
     "nk_use_canonical", "nk_copy_currents", "nk_copy_spike_counts", "nk_copy_voltages",
     "nk_copy_refractory", "nk_device_currents", "nk_reset", "nk_reset_async", "nk_last_timings",
@@ -40,7 +41,8 @@ EXPORTS = (
 
 class NkOpts(C.Structure):
     _fields_ = [("device", C.c_int32), ("kmer_width", C.c_int32), ("top_n", C.c_uint32),
-                ("stage_timing", C.c_uint32), ("reserved", C.c_uint32 * 12)]
+                ("stage_timing", C.c_uint32), ("exact_counts", C.c_uint32),
+                ("reserved", C.c_uint32 * 11)]
 
 
 class NkTopRow(C.Structure):
@@ -93,6 +95,10 @@ def load(share_torch: bool = True):
         "nk_merge_top_kmers": (C.c_int, [vp, vp, sz, vp]),
         "nk_top_abundant_neurons": (C.c_long, [vp, sz, P(NkTopRow)]),
         "nk_get_count": (C.c_int, [vp, u64, P(u32), P(C.c_int)]),
+        "nk_get_counts": (C.c_int, [vp, vp, sz, vp, vp]),
+        "nk_distinct_kmers": (C.c_long, [vp]),
+        "nk_copy_kmer_per_neuron": (C.c_int, [vp, vp, sz]),
+        "nk_process_sequence": (C.c_int, [vp, vp, sz]),
         "nk_total_spikes": (u64, [vp]),
         "nk_energy_used": (C.c_double, [vp]),
         "nk_set_steps": (None, [vp, u64]),

@@ -51,7 +51,7 @@ class SpikingKmerCounter:
     def __init__(self, k: int, threshold: float, leak: float, refractory: int,
                  spike_cost: float, pool_size: int, use_canonical: bool, *,
                  device: int = 0, top_n: int = 20, stage_timing: bool = False,
-                 kmer_width: int = 64):
+                 kmer_width: int = 64, exact_counts: bool = False):
         self._L = _lib.load()
         o = NkOpts()
         self._L.nk_opts_default(C.byref(o))
@@ -61,6 +61,7 @@ class SpikingKmerCounter:
         if kmer_width not in (64, 128):
             raise ValueError("kmer_width must be 64 (the reference's u64 keys) or 128")
         o.kmer_width = _lib.NK_KMER_128 if kmer_width == 128 else _lib.NK_KMER_COMPAT
+        o.exact_counts = 1 if exact_counts else 0
         self.kmer_width = kmer_width
         self._h = None
         h = self._L.nk_new(k, threshold, leak, refractory, spike_cost, pool_size,
@@ -144,11 +145,37 @@ class SpikingKmerCounter:
         return [(int(rows[i].idx), int(rows[i].spikes), int(rows[i].uniques)) for i in range(m)]
 
     def get_count(self, kmer: int) -> Optional[int]:
-        """src/spiking_hash.rs:675-682 (NK_E_UNSUPPORTED in ABI v1)."""
+        """src/spiking_hash.rs:675-682 (needs exact_counts=True)."""
         out = C.c_uint32()
         present = C.c_int()
         check(self._L.nk_get_count(self._h, kmer, C.byref(out), C.byref(present)))
         return int(out.value) if present.value else None
+
+    def process_sequence(self, seq: bytes) -> None:
+        """src/spiking_hash.rs:203-273 (needs exact_counts=True)."""
+        buf = np.frombuffer(bytes(seq), dtype=np.uint8)
+        check(self._L.nk_process_sequence(self._h, buf.ctypes.data if buf.size else None,
+                                          buf.size))
+
+    def get_counts(self, kmers) -> tuple:
+        """Batched get_count: -> (counts u32[n], present bool[n])."""
+        q = np.ascontiguousarray(kmers, dtype=np.uint64)
+        out = np.zeros(max(q.size, 1), np.uint32)
+        pres = np.zeros(max(q.size, 1), np.uint8)
+        check(self._L.nk_get_counts(self._h, q.ctypes.data if q.size else None, q.size,
+                                    out.ctypes.data, pres.ctypes.data))
+        return out[:q.size], pres[:q.size].astype(bool)
+
+    def distinct_kmers(self) -> int:
+        """counts.len() (needs exact_counts=True)."""
+        n = int(self._L.nk_distinct_kmers(self._h))
+        if n < 0:
+            check(n)
+        return n
+
+    def kmer_per_neuron(self) -> np.ndarray:
+        """The full kmer_per_neuron map as a dense u32 array (needs exact_counts=True)."""
+        return self._copy("nk_copy_kmer_per_neuron", np.uint32)
 
     def energy_used(self) -> float:
         return float(self._L.nk_energy_used(self._h))

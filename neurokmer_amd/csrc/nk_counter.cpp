@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "neurokmer.h"
+#include "nk_exact.h"
 #include "nk_fastx.h"
 #include "nk_kernels.h"
 
@@ -127,6 +128,19 @@ struct nk_counter {
   bool lif_zeroed = false;   // hist/stats already zeroed by this call's prep kernel
   bool state_fresh = true;   // spikes/v/r are logically zero (lazy reset)
   bool cur_fresh = true;     // currents are logically zero (lazy reset)
+  // exact k-mer table (opts.exact_counts, nk_exact.h)
+  DevBuf<uint64_t> x_keys, x_sorted, x_uniq, x_q;
+  DevBuf<uint32_t> x_cnt, x_tile_rec, kpn, x_out, x_pres;
+  DevBuf<uint8_t> x_tmp;
+  DevBuf<unsigned long long> x_n;  // [0] keys of the last input, [1] distinct keys
+  bool exact_built = false;        // the sorted table holds the last process/accumulate input
+  // process_sequence: delta counts on top of the sorted table, kmer_per_neuron
+  DevBuf<unsigned long long> d_keys, d_meta;
+  DevBuf<uint32_t> d_vals;
+  DevBuf<uint8_t> touched;
+  uint64_t d_cap = 0, d_bound = 0;  // delta capacity, upper bound of its distinct keys
+  bool d_dirty = true;              // delta must be cleared before use
+  bool kpn_valid = false;           // kpn holds kmer_per_neuron (else it is all zero)
   // top-N selection fused into the LIF kernel (TopFuse)
   DevBuf<uint64_t> bcand;
   DevBuf<uint32_t> bcnt;
@@ -173,6 +187,10 @@ static int zero_state_on(nk_counter *c, hipStream_t) {
   c->have_input = false;
   c->state_fresh = true;
   c->cur_fresh = true;
+  c->exact_built = false;  // a fresh counter's `counts` is empty
+  c->d_dirty = true;
+  c->d_bound = 0;
+  c->kpn_valid = false;
   return NK_OK;
 }
 
@@ -239,6 +257,10 @@ nk_counter *nk_new(size_t k, float threshold, float leak, uint32_t refractory, d
   else nk_opts_default(&o);
   if (o.kmer_width != NK_KMER_COMPAT && o.kmer_width != NK_KMER_128) {
     fail(NK_E_INVALID, "kmer_width %d unknown", o.kmer_width);
+    return nullptr;
+  }
+  if (o.kmer_width == NK_KMER_128 && o.exact_counts) {
+    fail(NK_E_UNSUPPORTED, "exact_counts is implemented for NK_KMER_COMPAT keys only");
     return nullptr;
   }
   if (o.kmer_width == NK_KMER_128 && k > 64) {
@@ -311,6 +333,10 @@ void nk_free(nk_counter *c) {
   c->p_off.release(); c->p_pos.release(); c->p_fill.release(); c->p_desc.release();
   c->p_over.release(); c->partials.release(); c->tbuckets.release();
   c->bcand.release(); c->bcnt.release();
+  c->x_keys.release(); c->x_sorted.release(); c->x_uniq.release(); c->x_q.release();
+  c->x_cnt.release(); c->x_tile_rec.release(); c->kpn.release(); c->x_out.release();
+  c->x_pres.release(); c->x_tmp.release(); c->x_n.release();
+  c->d_keys.release(); c->d_meta.release(); c->d_vals.release(); c->touched.release();
   c->tile_rec.release(); c->hist.release(); c->tie_cnt.release(); c->uniq.release();
   c->special.release(); c->stats.release(); c->lif_tbl.release(); c->topst.release();
   c->cand.release(); c->top_cur.release(); c->set_keys.release(); c->top_keys.release();
@@ -338,6 +364,38 @@ int nk_reset_async(nk_counter *c, void *stream) {
 // ---------------------------------------------------------------------------
 // accumulate: currents = histogram of H(kmer) % pool over this input
 // ---------------------------------------------------------------------------
+// The exact k-mer table of this input (opts.exact_counts; nk_exact.h).  One
+// host synchronisation (the key count sizes the sort).
+static int build_exact(nk_counter *c, const KmerInput &in0, hipStream_t s) {
+  int rc;
+  const int end_bit = c->k <= 32 ? (int)(2 * c->k) : 64;
+  KmerInput in = in0;
+  in.n_tiles = n_tiles_for(in.n_bases, kTile);
+  if ((rc = c->x_n.ensure(2)) || (rc = c->x_tile_rec.ensure(std::max<uint64_t>(in.n_tiles, 1))) ||
+      (rc = c->x_keys.ensure(std::max<uint64_t>(in.n_bases, 1))) || (rc = c->kpn.ensure(c->pool)))
+    return rc;
+  in.tile_rec = c->x_tile_rec.p;
+  HIPCHK(hipMemsetAsync(c->x_n.p, 0, 16, s));
+  HIPCHK(launch_tile_rec(in, kTile, c->x_tile_rec.p, s));
+  HIPCHK(exact_keys(in, (int)c->k, c->canonical, c->x_keys.p, c->x_n.p, s));
+  unsigned long long n = 0;
+  HIPCHK(hipMemcpyAsync(&n, c->x_n.p, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  const uint64_t nn = std::max<uint64_t>(n, 1);
+  if ((rc = c->x_sorted.ensure(nn)) || (rc = c->x_uniq.ensure(nn)) || (rc = c->x_cnt.ensure(nn)) ||
+      (rc = c->x_tmp.ensure(exact_temp_bytes(nn, end_bit))))
+    return rc;
+  HIPCHK(exact_sort_rle(c->x_keys.p, c->x_sorted.p, n, end_bit, c->x_uniq.p, c->x_cnt.p,
+                        c->x_n.p + 1, c->x_tmp.p, c->x_tmp.n, s));
+  HIPCHK(hipMemsetAsync(c->kpn.p, 0, c->pool * 4, s));
+  HIPCHK(exact_kpn(c->x_uniq.p, c->x_n.p + 1, n, c->pool, c->kpn.p, s));
+  c->exact_built = true;
+  c->kpn_valid = true;
+  c->d_dirty = true;  // counts.clear() (src/spiking_hash.rs:157,426)
+  c->d_bound = 0;
+  return NK_OK;
+}
+
 // defer_partials: leave K1c (currents += partials) to the LIF kernel of the
 // same process call instead of a separate pass
 static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_offs,
@@ -418,6 +476,7 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
     HIPCHK(mark(c, 2, s));
   }
   HIPCHK(mark(c, 3, s));
+  if (c->opts.exact_counts && (rc = build_exact(c, in, s))) return rc;
   c->last_in = in;
   c->have_input = true;
   c->top_valid = false;
@@ -573,7 +632,12 @@ static int enqueue_readback(nk_counter *c, uint32_t m, bool uniq, hipStream_t s)
 // LIF + exact top-N + uniques with ONE host synchronisation in the common
 // case; the rare corrections (spike counts past the histogram, a hash set too
 // small for the top rows, an overflowed top bucket) are redone after it.
-static int lif_top_uniques(nk_counter *c, int streaming, hipStream_t s) {
+// use_kpn: the uniques column comes from the exact table's kmer_per_neuron
+// (a process call with opts.exact_counts) instead of the uniques pass
+static int finish_top(nk_counter *c, uint64_t want, bool fused, bool uniq, bool use_kpn,
+                      hipStream_t s);
+
+static int lif_top_uniques(nk_counter *c, int streaming, bool use_kpn, hipStream_t s) {
   int rc;
   const uint64_t want = std::min<uint64_t>(c->opts.top_n, c->pool);
   const bool uniq = want && c->have_input && c->last_in.n_tiles;
@@ -583,12 +647,28 @@ static int lif_top_uniques(nk_counter *c, int streaming, hipStream_t s) {
   if ((rc = enqueue_lif(c, streaming, fused ? (uint32_t)want : 0u, uniq && c->part_used, s)))
     return rc;
   HIPCHK(mark(c, 4, s));
+  return finish_top(c, want, fused, uniq, use_kpn, s);
+}
+
+// After a LIF pass (hist, stats and, when fused, the selected rows on the
+// device): exact top-N, uniques, one readback, energy and c->top.
+static int finish_top(nk_counter *c, uint64_t want, bool fused, bool uniq, bool use_kpn,
+                      hipStream_t s) {
+  int rc;
   if (want && !fused) {
     HIPCHK(launch_topn_threshold(c->hist.p, want, c->pool, c->topst.p, s));
     if ((rc = enqueue_select(c, want, s))) return rc;
   }
   HIPCHK(mark(c, 5, s));
-  if (uniq && (rc = enqueue_uniques(c, (uint32_t)want, false, fused, s))) return rc;
+  auto uniques = [&](bool post_done) -> int {
+    if (!uniq) return NK_OK;
+    if (use_kpn) {
+      HIPCHK(exact_top_uniques(c->cand.p, (uint32_t)want, c->kpn.p, c->uniq.p, s));
+      return NK_OK;
+    }
+    return enqueue_uniques(c, (uint32_t)want, false, post_done, s);
+  };
+  if ((rc = uniques(fused))) return rc;
   if ((rc = enqueue_readback(c, (uint32_t)want, uniq, s))) return rc;
   HIPCHK(mark(c, 6, s));
   HIPCHK(hipStreamSynchronize(s));
@@ -603,11 +683,11 @@ static int lif_top_uniques(nk_counter *c, int streaming, hipStream_t s) {
     if ((rc = refine_threshold(c, want, h->stats[1], st, s))) return rc;
     HIPCHK(hipMemcpyAsync(c->topst.p, &st, sizeof st, hipMemcpyHostToDevice, s));
     if ((rc = enqueue_select(c, want, s))) return rc;
-    if (uniq && (rc = enqueue_uniques(c, (uint32_t)want, false, false, s))) return rc;
+    if ((rc = uniques(false))) return rc;
     if ((rc = enqueue_readback(c, (uint32_t)want, uniq, s))) return rc;
     HIPCHK(hipStreamSynchronize(s));
   }
-  if (uniq) {
+  if (uniq && !use_kpn) {
     // set too small: grow to the capacity the top rows need, redo the pass
     if (h->flags[0]) {
       uint64_t cap = c->set_alloc;
@@ -671,7 +751,7 @@ int nk_finalize(nk_counter *c, int streaming, void *stream) {
   (void)hipSetDevice(c->device);
   hipStream_t s = pick_stream(c, stream);
   HIPCHK(mark(c, 7, s));
-  int rc = lif_top_uniques(c, streaming, s);
+  int rc = lif_top_uniques(c, streaming, false, s);
   if (rc) return rc;
   c->top_valid = true;
   // an accumulate on this handle precedes: report its stages too
@@ -688,7 +768,7 @@ static int process_device(nk_counter *c, const uint8_t *d_bases, const uint64_t 
     return rc;
   }
   hipStream_t s = pick_stream(c, stream);
-  if ((rc = lif_top_uniques(c, streaming, s))) return rc;
+  if ((rc = lif_top_uniques(c, streaming, c->opts.exact_counts && c->exact_built, s))) return rc;
   c->top_valid = true;
   collect_timings(c, true);
   return NK_OK;
@@ -833,9 +913,181 @@ long nk_top_abundant_neurons(nk_counter *c, size_t n, nk_top_row *out) {
   return (long)m;
 }
 
-int nk_get_count(nk_counter *c, uint64_t, uint32_t *, int *) {
-  (void)c;
-  return fail(NK_E_UNSUPPORTED, "get_count: exact k-mer table not built on device in ABI v1");
+static DeltaArgs delta_args(nk_counter *c) {
+  DeltaArgs d{};
+  if (c->d_dirty || !c->d_cap) return d;  // keys == null: no delta
+  d.keys = c->d_keys.p;
+  d.vals = c->d_vals.p;
+  d.mask = c->d_cap - 1;
+  d.meta = c->d_meta.p;
+  return d;
+}
+
+// room in the delta for `add` more distinct keys (load <= 1/2)
+static int delta_reserve(nk_counter *c, uint64_t add, hipStream_t s) {
+  int rc;
+  if ((rc = c->d_meta.ensure(2))) return rc;
+  uint64_t cap = c->d_cap ? c->d_cap : 1024;
+  while (2 * (c->d_bound + add) > cap) cap <<= 1;
+  if (c->d_dirty) {
+    if (cap > c->d_cap) {
+      if ((rc = c->d_keys.ensure(cap)) || (rc = c->d_vals.ensure(cap))) return rc;
+      c->d_cap = cap;
+    }
+    DeltaArgs d{c->d_keys.p, c->d_vals.p, c->d_cap - 1, c->d_meta.p};
+    HIPCHK(delta_clear(d, s));
+    c->d_dirty = false;
+    c->d_bound = 0;
+  } else if (cap > c->d_cap) {  // grow: rehash into a new table
+    DevBuf<unsigned long long> nk;
+    DevBuf<uint32_t> nv;
+    if ((rc = nk.ensure(cap)) || (rc = nv.ensure(cap))) return rc;
+    DeltaArgs from = delta_args(c);
+    DevBuf<unsigned long long> nm;
+    if ((rc = nm.ensure(2))) return rc;
+    DeltaArgs to{nk.p, nv.p, cap - 1, nm.p};
+    HIPCHK(delta_clear(to, s));
+    HIPCHK(delta_rehash(from, to, s));
+    HIPCHK(hipMemcpyAsync(c->d_meta.p, nm.p, 16, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::swap(c->d_keys.p, nk.p);
+    std::swap(c->d_keys.n, nk.n);
+    std::swap(c->d_vals.p, nv.p);
+    std::swap(c->d_vals.n, nv.n);
+    c->d_cap = cap;
+    nm.release();
+    nk.release();
+    nv.release();
+  }
+  return NK_OK;
+}
+
+static int need_exact(nk_counter *c) {
+  if (!c) return fail(NK_E_INVALID, "null counter");
+  if (!c->opts.exact_counts)
+    return fail(NK_E_UNSUPPORTED, "the exact k-mer table needs nk_opts.exact_counts = 1");
+  return NK_OK;
+}
+
+// SpikingKmerCounter::process_sequence (src/spiking_hash.rs:203-273)
+int nk_process_sequence(nk_counter *c, const uint8_t *seq, size_t len) {
+  int rc = need_exact(c);
+  if (rc) return rc;
+  if (len && !seq) return fail(NK_E_INVALID, "null sequence");
+  if (len < c->k) return NK_OK;  // :205-207: no k-mers, no LIF step
+  if (c->pool == 0)
+    return fail(NK_E_INVALID, "pool_size 0 with k-mers present (the reference panics on % 0)");
+  (void)hipSetDevice(c->device);
+  hipStream_t s = c->own_stream;
+  if ((rc = c->in_bases.ensure(len + 16)) || (rc = c->in_offs.ensure(2)) ||
+      (rc = c->x_n.ensure(2)) || (rc = c->kpn.ensure(c->pool)))
+    return rc;
+  const uint64_t offs[2] = {0, (uint64_t)len};
+  HIPCHK(hipMemcpyAsync(c->in_bases.p, seq, len, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(c->in_offs.p, offs, 16, hipMemcpyHostToDevice, s));
+  KmerInput in{};
+  in.bases = c->in_bases.p;
+  in.offsets = c->in_offs.p;
+  in.n_recs = 1;
+  in.n_bases = len;
+  in.n_tiles = n_tiles_for(len, kTile);
+  if ((rc = c->x_tile_rec.ensure(in.n_tiles)) || (rc = c->x_keys.ensure(len))) return rc;
+  in.tile_rec = c->x_tile_rec.p;
+  // this step reads the state: materialise lazily-zero buffers
+  if ((rc = materialize(c, true, s)) || (rc = materialize(c, false, s))) return rc;
+  if (!c->kpn_valid) {
+    HIPCHK(hipMemsetAsync(c->kpn.p, 0, c->pool * 4, s));
+    c->kpn_valid = true;
+  }
+  if (!c->touched.n) {
+    if ((rc = c->touched.ensure(c->pool))) return rc;
+    HIPCHK(hipMemsetAsync(c->touched.p, 0, c->pool, s));  // seq_lif keeps it zero
+  }
+  const uint64_t add = len - c->k + 1;
+  if ((rc = delta_reserve(c, add, s))) return rc;
+  c->d_bound += add;
+  HIPCHK(hipMemsetAsync(c->x_n.p, 0, 8, s));  // [0] only: [1] is the sorted table's size
+  HIPCHK(launch_tile_rec(in, kTile, c->x_tile_rec.p, s));
+  HIPCHK(exact_keys(in, (int)c->k, c->canonical, c->x_keys.p, c->x_n.p, s));
+  HIPCHK(seq_accumulate(c->x_keys.p, c->x_n.p, add, c->pool, (unsigned long long *)c->cur.p,
+                        c->touched.p, delta_args(c), c->exact_built ? c->x_uniq.p : nullptr,
+                        c->exact_built ? c->x_n.p + 1 : nullptr, s));
+  ZeroList z{};
+  z.ptr[0] = c->hist.p;  z.bytes[0] = kHistBins * kHistCopies * 4;
+  z.ptr[1] = c->stats.p; z.bytes[1] = 16;
+  z.n = 2;
+  HIPCHK(launch_zero(z, s));
+  HIPCHK(seq_lif(c->pool, (unsigned long long *)c->cur.p, c->touched.p, c->kpn.p, c->v.p, c->r.p,
+                 c->sc.p, c->thr, c->leak, c->refr, c->hist.p, c->stats.p, s));
+  c->have_input = false;  // no uniques pass: the column comes from kmer_per_neuron
+  const uint64_t want = std::min<uint64_t>(c->opts.top_n, c->pool);
+  if ((rc = finish_top(c, want, false, want != 0, true, s))) return rc;
+  c->top_valid = true;
+  return NK_OK;
+}
+
+int nk_get_counts(nk_counter *c, const uint64_t *kmers, size_t n, uint32_t *out,
+                  uint8_t *present) {
+  int rc = need_exact(c);
+  if (rc) return rc;
+  if (n && (!kmers || !out || !present)) return fail(NK_E_INVALID, "null argument");
+  if (!n) return NK_OK;
+  if (!c->exact_built && c->d_dirty) {  // empty table (fresh or reset counter)
+    memset(out, 0, n * 4);
+    memset(present, 0, n);
+    return NK_OK;
+  }
+  (void)hipSetDevice(c->device);
+  hipStream_t s = c->own_stream;
+  if ((rc = c->x_q.ensure(n)) || (rc = c->x_out.ensure(n)) || (rc = c->x_pres.ensure(n)))
+    return rc;
+  HIPCHK(hipMemcpyAsync(c->x_q.p, kmers, n * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(exact_lookup2(c->exact_built ? c->x_uniq.p : nullptr, c->x_cnt.p,
+                       c->exact_built ? c->x_n.p + 1 : nullptr, delta_args(c), c->x_q.p, n,
+                       c->x_out.p, c->x_pres.p, s));
+  std::vector<uint32_t> pres(n);
+  HIPCHK(hipMemcpyAsync(out, c->x_out.p, n * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(pres.data(), c->x_pres.p, n * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  for (size_t i = 0; i < n; ++i) present[i] = pres[i] ? 1 : 0;
+  return NK_OK;
+}
+
+int nk_get_count(nk_counter *c, uint64_t kmer, uint32_t *out, int *present) {
+  if (!out || !present) return fail(NK_E_INVALID, "null argument");
+  uint8_t p = 0;
+  int rc = nk_get_counts(c, &kmer, 1, out, &p);
+  *present = p;
+  return rc;
+}
+
+long nk_distinct_kmers(nk_counter *c) {
+  int rc = need_exact(c);
+  if (rc) return rc;
+  (void)hipSetDevice(c->device);
+  HIPCHK(hipStreamSynchronize(c->own_stream));
+  unsigned long long n = 0, m[2] = {0, 0};
+  if (c->exact_built) HIPCHK(hipMemcpy(&n, c->x_n.p + 1, 8, hipMemcpyDeviceToHost));
+  if (!c->d_dirty) HIPCHK(hipMemcpy(m, c->d_meta.p, 16, hipMemcpyDeviceToHost));
+  // meta[1]: keys process_sequence added that the sorted table did not hold
+  // (k_seq_accumulate; the ~0 key included)
+  return (long)(n + m[1]);
+}
+
+int nk_copy_kmer_per_neuron(nk_counter *c, uint32_t *out, size_t n) {
+  int rc = need_exact(c);
+  if (rc) return rc;
+  if (n != c->pool) return fail(NK_E_INVALID, "n (%zu) must equal pool_size (%zu)", n, c->pool);
+  if (!n) return NK_OK;
+  if (!out) return fail(NK_E_INVALID, "null argument");
+  if (!c->kpn_valid) {
+    memset(out, 0, n * 4);
+    return NK_OK;
+  }
+  (void)hipSetDevice(c->device);
+  HIPCHK(hipStreamSynchronize(c->own_stream));
+  HIPCHK(hipMemcpy(out, c->kpn.p, n * 4, hipMemcpyDeviceToHost));
+  return NK_OK;
 }
 
 uint64_t nk_total_spikes(const nk_counter *c) { return c ? c->total_spikes : 0; }

@@ -1,0 +1,71 @@
+// Exact k-mer count table on the device: the reference's
+// `counts: DashMap<u64, AtomicU32>` (src/spiking_hash.rs:27,157-165,441-447),
+// `get_count` (:675-682) and the full `kmer_per_neuron` (:167-172,467-473).
+//
+// Built only when nk_opts.exact_counts is set (the reference always builds it;
+// it is off the metric's hot path):
+//   1. every k-mer key of the input, compacted (one atomic per workgroup);
+//   2. radix sort (rocPRIM) over the key's 2k significant bits;
+//   3. run-length encode -> sorted unique keys + u32 counts (a count wraps at
+//      2^32 like the reference's AtomicU32 / u32 `+=`);
+//   4. kmer_per_neuron[H(key) % P] += 1 per unique key.
+// get_count = binary search in the sorted keys (+ the process_sequence delta
+// table, nk_counter.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "nk_kernels.h"
+
+namespace nk {
+
+// keys of every valid window of `in` (in.tile_rec for kTile tiles), in any
+// order; *n_keys (device) must be 0 on entry
+hipError_t exact_keys(const KmerInput &in, int k, int canonical, uint64_t *keys,
+                      unsigned long long *n_keys, hipStream_t s);
+// scratch bytes for exact_sort_rle over n keys
+size_t exact_temp_bytes(size_t n, int end_bit);
+// sort keys[0..n) (keys is clobbered) and run-length encode into uniq/cnt;
+// *n_uniq (device) receives the number of distinct keys
+hipError_t exact_sort_rle(uint64_t *keys, uint64_t *keys_sorted, size_t n, int end_bit,
+                          uint64_t *uniq, uint32_t *cnt, unsigned long long *n_uniq, void *tmp,
+                          size_t tmp_bytes, hipStream_t s);
+// kpn[H(key) % pool] += 1 for every distinct key (kpn zeroed by the caller)
+hipError_t exact_kpn(const uint64_t *uniq, const unsigned long long *n_uniq, size_t max_n,
+                     uint64_t pool, uint32_t *kpn, hipStream_t s);
+// out[i] = count of q[i] in the sorted table (present[i] = 0/1)
+hipError_t exact_lookup(const uint64_t *uniq, const uint32_t *cnt,
+                        const unsigned long long *n_uniq, const uint64_t *q, size_t nq,
+                        uint32_t *out, uint32_t *present, hipStream_t s);
+// ---- process_sequence (src/spiking_hash.rs:203-273) ------------------------
+// The k-mers a process_sequence call adds to `counts` go to a device hash
+// table ("delta") on top of the sorted table of the last process call.
+struct DeltaArgs {
+  unsigned long long *keys;   // [cap], kEmpty = free
+  uint32_t *vals;             // [cap]
+  uint64_t mask;              // cap - 1
+  unsigned long long *meta;   // [0] count of key ~0, [1] keys new to counts (distinct)
+};
+hipError_t delta_clear(const DeltaArgs &d, hipStream_t s);
+hipError_t delta_rehash(const DeltaArgs &from, const DeltaArgs &to, hipStream_t s);
+// one sequence's keys: currents[H(key) % pool] += 1, touched[idx] = 1, counts[key] += 1
+hipError_t seq_accumulate(const uint64_t *keys, const unsigned long long *n_keys, size_t max_n,
+                          uint64_t pool, unsigned long long *currents, uint8_t *touched,
+                          const DeltaArgs &d, const uint64_t *uniq,
+                          const unsigned long long *n_uniq, hipStream_t s);
+// kmer_per_neuron += touched; one LifNeuron::update(current as f32) for every
+// neuron with current > 0; currents = 0; spike-count histogram + stats
+hipError_t seq_lif(uint64_t pool, unsigned long long *currents, uint8_t *touched, uint32_t *kpn,
+                   float *v, uint32_t *r, uint64_t *sc, float thr, float leak, uint32_t refr,
+                   uint32_t *hist, uint64_t *stats, hipStream_t s);
+// get_count over the sorted table (may be empty: n_uniq null) plus the delta
+hipError_t exact_lookup2(const uint64_t *uniq, const uint32_t *cnt,
+                         const unsigned long long *n_uniq, const DeltaArgs &d, const uint64_t *q,
+                         size_t nq, uint32_t *out, uint32_t *present, hipStream_t s);
+
+// uniques column of the top rows from kmer_per_neuron
+hipError_t exact_top_uniques(const TopCand *cand, uint32_t m, const uint32_t *kpn, uint32_t *uniq,
+                             hipStream_t s);
+
+}  // namespace nk

@@ -1,0 +1,417 @@
+// Exact k-mer count table (nk_exact.h).  The key extraction, the per-neuron
+// distinct count and the lookups are kernels of this file; the sort and the
+// run-length encoding are rocPRIM's device radix sort / RLE.
+#include <cstring>  // before rocprim: its texture_cache_iterator uses memset
+
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_run_length_encode.hpp>
+
+#include "nk_device.h"
+#include "nk_exact.h"
+#include "nk_tile.h"
+
+namespace nk {
+
+namespace {
+
+constexpr int kXTile = kTile;     // 4096 positions per workgroup
+constexpr int kXBlock = kBlock;   // 256 threads
+constexpr int kXPer = kXTile / kXBlock;
+
+// exclusive scan over a 256-thread block, *total = sum
+__device__ __forceinline__ uint32_t scan256(uint32_t x, uint32_t *s_w, uint32_t *total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t incl = x;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) s_w[w] = incl;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+  for (int i = 0; i < kXBlock / 64; ++i) {
+    pre += i < w ? s_w[i] : 0u;
+    tot += s_w[i];
+  }
+  *total = tot;
+  return pre + incl - x;
+}
+
+// k <= 32: keys from the staged tile, exactly as the count kernels derive them
+template <bool CANON>
+__global__ __launch_bounds__(kXBlock) void k_keys_tile(KmerInput in, int k,
+                                                       uint64_t *__restrict__ keys,
+                                                       unsigned long long *__restrict__ n_keys) {
+  __shared__ TileLds<kXTile, !CANON> L;
+  __shared__ uint32_t s_w[kXBlock / 64];
+  __shared__ unsigned long long s_base;
+  const uint64_t T0 = (uint64_t)blockIdx.x * kXTile;
+  stage_tile<kXTile, kXBlock, !CANON>(L, in, blockIdx.x, k);
+  uint64_t kv[kXPer];  // fixed slots (no dynamic register indexing) + a valid mask
+  uint32_t ok = 0;
+#pragma unroll
+  for (int j = 0; j < kXPer; ++j) {
+    const int q = j * kXBlock + threadIdx.x;
+    kv[j] = 0;
+    if (T0 + (uint64_t)q + (uint64_t)k > in.n_bases) continue;
+    if (!window_valid(L, T0, q, k, in.n_bases)) continue;
+    kv[j] = window_key<kXTile, !CANON, CANON>(L, q, k);
+    ok |= 1u << j;
+  }
+  uint32_t total;
+  const uint32_t pre = scan256((uint32_t)__popc(ok), s_w, &total);
+  if (threadIdx.x == 0) s_base = total ? atomicAdd(n_keys, (unsigned long long)total) : 0ull;
+  __syncthreads();
+  uint64_t at = s_base + pre;
+#pragma unroll
+  for (int j = 0; j < kXPer; ++j)
+    if ((ok >> j) & 1u) keys[at++] = kv[j];
+}
+
+// k > 32 (NK_KMER_COMPAT): the reference's release-build keys, one window per
+// position, walking the records like the count kernel
+template <bool CANON>
+__global__ __launch_bounds__(kXBlock) void k_keys_compat(KmerInput in, int k,
+                                                         uint64_t *__restrict__ keys,
+                                                         unsigned long long *__restrict__ n_keys) {
+  __shared__ uint32_t s_w[kXBlock / 64];
+  __shared__ unsigned long long s_base;
+  const uint64_t T0 = (uint64_t)blockIdx.x * kXTile;
+  uint64_t r = in.tile_rec[blockIdx.x];
+  uint64_t kv[kXPer];
+  uint32_t ok = 0;
+#pragma unroll
+  for (int j = 0; j < kXPer; ++j) {
+    kv[j] = 0;
+    const uint64_t p = T0 + (uint64_t)j * kXBlock + threadIdx.x;
+    if (p >= in.n_bases) continue;
+    while (r + 1 < in.n_recs && in.offsets[r + 1] <= p) ++r;
+    const uint64_t s0 = in.offsets[r], e0 = in.offsets[r + 1];
+    if (p < s0 || p + (uint64_t)k > e0) continue;
+    kv[j] = compat_key<CANON>(in.bases, s0, p, k);
+    ok |= 1u << j;
+  }
+  uint32_t total;
+  const uint32_t pre = scan256((uint32_t)__popc(ok), s_w, &total);
+  if (threadIdx.x == 0) s_base = total ? atomicAdd(n_keys, (unsigned long long)total) : 0ull;
+  __syncthreads();
+  uint64_t at = s_base + pre;
+#pragma unroll
+  for (int j = 0; j < kXPer; ++j)
+    if ((ok >> j) & 1u) keys[at++] = kv[j];
+}
+
+__global__ void k_kpn(const uint64_t *__restrict__ uniq, const unsigned long long *__restrict__ n_uniq,
+                      FastMod fm, uint32_t *__restrict__ kpn) {
+  const uint64_t n = *n_uniq;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    atomicAdd(&kpn[fastmod(sip13_u64(uniq[i]), fm)], 1u);
+}
+
+__global__ void k_lookup(const uint64_t *__restrict__ uniq, const uint32_t *__restrict__ cnt,
+                         const unsigned long long *__restrict__ n_uniq,
+                         const uint64_t *__restrict__ q, uint64_t nq, uint32_t *__restrict__ out,
+                         uint32_t *__restrict__ present) {
+  const uint64_t n = *n_uniq;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nq;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t key = q[i];
+    uint64_t lo = 0, hi = n;  // first index with uniq >= key
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (uniq[mid] < key) lo = mid + 1;
+      else hi = mid;
+    }
+    const bool hit = lo < n && uniq[lo] == key;
+    out[i] = hit ? cnt[lo] : 0u;
+    present[i] = hit ? 1u : 0u;
+  }
+}
+
+__global__ void k_top_uniques(const TopCand *__restrict__ cand, uint32_t m,
+                              const uint32_t *__restrict__ kpn, uint32_t *__restrict__ uniq) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) uniq[i] = kpn[cand[i].idx];
+}
+
+constexpr unsigned long long kDEmpty = ~0ULL;
+
+__device__ __forceinline__ uint64_t dmix(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ bool in_sorted(const uint64_t *uniq, uint64_t n, uint64_t key,
+                                          uint64_t *at) {
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (uniq[mid] < key) lo = mid + 1;
+    else hi = mid;
+  }
+  *at = lo;
+  return lo < n && uniq[lo] == key;
+}
+
+// counts[key] += v in the delta; returns true if the key was new to the delta
+__device__ bool delta_add(const DeltaArgs &d, uint64_t key, uint32_t v) {
+  if (key == kDEmpty) return atomicAdd(&d.meta[0], (unsigned long long)v) == 0;
+  uint64_t h = dmix(key) & d.mask;
+  for (;;) {
+    unsigned long long cur = d.keys[h];
+    if (cur == kDEmpty) {
+      cur = atomicCAS(&d.keys[h], kDEmpty, (unsigned long long)key);
+      if (cur == kDEmpty) {
+        atomicAdd(&d.vals[h], v);
+        return true;
+      }
+    }
+    if (cur == key) {
+      atomicAdd(&d.vals[h], v);
+      return false;
+    }
+    h = (h + 1) & d.mask;
+  }
+}
+
+__device__ bool delta_get(const DeltaArgs &d, uint64_t key, uint32_t *v) {
+  if (key == kDEmpty) {
+    *v = (uint32_t)d.meta[0];
+    return d.meta[0] != 0;
+  }
+  uint64_t h = dmix(key) & d.mask;
+  for (;;) {
+    const unsigned long long cur = d.keys[h];
+    if (cur == kDEmpty) return false;
+    if (cur == key) {
+      *v = d.vals[h];
+      return true;
+    }
+    h = (h + 1) & d.mask;
+  }
+}
+
+__global__ void k_delta_clear(DeltaArgs d) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= d.mask;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    d.keys[i] = kDEmpty;
+    d.vals[i] = 0;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 2) d.meta[threadIdx.x] = 0;
+}
+
+__global__ void k_delta_rehash(DeltaArgs from, DeltaArgs to) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= from.mask;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    if (from.keys[i] != kDEmpty) delta_add(to, from.keys[i], from.vals[i]);
+  if (blockIdx.x == 0 && threadIdx.x < 2) to.meta[threadIdx.x] = from.meta[threadIdx.x];
+}
+
+__global__ void k_seq_accumulate(const uint64_t *__restrict__ keys,
+                                 const unsigned long long *__restrict__ n_keys, FastMod fm,
+                                 unsigned long long *__restrict__ currents,
+                                 uint8_t *__restrict__ touched, DeltaArgs d,
+                                 const uint64_t *__restrict__ uniq,
+                                 const unsigned long long *__restrict__ n_uniq) {
+  const uint64_t n = *n_keys, nu = n_uniq ? *n_uniq : 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t key = keys[i];
+    const uint64_t idx = fastmod(sip13_u64(key), fm);
+    atomicAdd(&currents[idx], 1ULL);  // :217-223,236-241,251-254
+    touched[idx] = 1;                 // local_unique[idx] = true
+    uint64_t at;
+    if (delta_add(d, key, 1) && !in_sorted(uniq, nu, key, &at))
+      atomicAdd(&d.meta[1], 1ull);    // a key new to `counts`
+  }
+}
+
+__global__ __launch_bounds__(256) void k_seq_lif(uint64_t pool, unsigned long long *__restrict__ currents,
+                                                 uint8_t *__restrict__ touched,
+                                                 uint32_t *__restrict__ kpn, float *__restrict__ V,
+                                                 uint32_t *__restrict__ R,
+                                                 uint64_t *__restrict__ SC, float thr, float leak,
+                                                 uint32_t refr, uint32_t *__restrict__ hist,
+                                                 unsigned long long *__restrict__ stats) {
+  __shared__ uint32_t sh[kHistBins];
+  for (int i = threadIdx.x; i < kHistBins; i += 256) sh[i] = 0;
+  __syncthreads();
+  unsigned long long sp = 0, mx = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < pool;
+       i += (uint64_t)gridDim.x * 256) {
+    if (touched[i]) {  // :258-263 kmer_per_neuron[idx] += 1 per sequence
+      kpn[i] += 1;
+      touched[i] = 0;
+    }
+    const unsigned long long cur = currents[i];
+    uint64_t sc = SC[i];
+    if (cur != 0) {  // :266-271: `current > 0.0 && neuron.update(current as f32)`
+      const float c = (float)(double)cur;
+      uint32_t r = R[i];
+      if (r > 0) {
+        R[i] = r - 1;
+      } else {
+        const float v = lif_step(V[i], leak, c);
+        if (v >= thr) {
+          V[i] = 0.0f;
+          R[i] = refr;
+          sc += 1;
+          SC[i] = sc;
+          sp += 1;
+        } else {
+          V[i] = v;
+        }
+      }
+      currents[i] = 0;  // :270
+    }
+    mx = sc > mx ? sc : mx;
+    atomicAdd(&sh[sc < (uint64_t)(kHistBins - 1) ? (uint32_t)sc : (uint32_t)(kHistBins - 1)], 1u);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    sp += __shfl_down(sp, o, 64);
+    const unsigned long long om = __shfl_down(mx, o, 64);
+    mx = om > mx ? om : mx;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (sp) atomicAdd(&stats[0], sp);
+    atomicMax(&stats[1], mx);
+  }
+  __syncthreads();
+  uint32_t *hc = hist + (size_t)(blockIdx.x & (kHistCopies - 1)) * kHistBins;
+  for (int i = threadIdx.x; i < kHistBins; i += 256)
+    if (sh[i]) atomicAdd(&hc[i], sh[i]);
+}
+
+__global__ void k_lookup2(const uint64_t *__restrict__ uniq, const uint32_t *__restrict__ cnt,
+                          const unsigned long long *__restrict__ n_uniq, DeltaArgs d,
+                          const uint64_t *__restrict__ q, uint64_t nq, uint32_t *__restrict__ out,
+                          uint32_t *__restrict__ present) {
+  const uint64_t n = n_uniq ? *n_uniq : 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nq;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t key = q[i];
+    uint64_t at;
+    const bool hm = in_sorted(uniq, n, key, &at);
+    uint32_t dv = 0;
+    const bool hd = d.keys && delta_get(d, key, &dv);
+    out[i] = (hm ? cnt[at] : 0u) + (hd ? dv : 0u);  // u32 wrap like AtomicU32
+    present[i] = (hm || hd) ? 1u : 0u;
+  }
+}
+
+unsigned grid_for(uint64_t n, unsigned cap) {
+  uint64_t g = (n + 255) / 256;
+  if (g > cap) g = cap;
+  return g ? (unsigned)g : 1u;
+}
+
+}  // namespace
+
+hipError_t exact_keys(const KmerInput &in, int k, int canonical, uint64_t *keys,
+                      unsigned long long *n_keys, hipStream_t s) {
+  if (!in.n_tiles) return hipSuccess;
+  const dim3 g((unsigned)in.n_tiles), b(kXBlock);
+  if (k <= 32) {
+    if (canonical) hipLaunchKernelGGL(k_keys_tile<true>, g, b, 0, s, in, k, keys, n_keys);
+    else hipLaunchKernelGGL(k_keys_tile<false>, g, b, 0, s, in, k, keys, n_keys);
+  } else {
+    if (canonical) hipLaunchKernelGGL(k_keys_compat<true>, g, b, 0, s, in, k, keys, n_keys);
+    else hipLaunchKernelGGL(k_keys_compat<false>, g, b, 0, s, in, k, keys, n_keys);
+  }
+  return hipGetLastError();
+}
+
+size_t exact_temp_bytes(size_t n, int end_bit) {
+  size_t a = 0, b = 0;
+  (void)rocprim::radix_sort_keys(nullptr, a, (const uint64_t *)nullptr, (uint64_t *)nullptr, n, 0,
+                                 end_bit);
+  (void)rocprim::run_length_encode(nullptr, b, (const uint64_t *)nullptr, n, (uint64_t *)nullptr,
+                                   (uint32_t *)nullptr, (unsigned long long *)nullptr);
+  return (a > b ? a : b) + 256;
+}
+
+hipError_t exact_sort_rle(uint64_t *keys, uint64_t *keys_sorted, size_t n, int end_bit,
+                          uint64_t *uniq, uint32_t *cnt, unsigned long long *n_uniq, void *tmp,
+                          size_t tmp_bytes, hipStream_t s) {
+  if (!n) return hipMemsetAsync(n_uniq, 0, sizeof(unsigned long long), s);
+  size_t tb = tmp_bytes;
+  hipError_t e = rocprim::radix_sort_keys(tmp, tb, (const uint64_t *)keys, keys_sorted, n, 0,
+                                          end_bit, s);
+  if (e != hipSuccess) return e;
+  tb = tmp_bytes;
+  return rocprim::run_length_encode(tmp, tb, (const uint64_t *)keys_sorted, n, uniq, cnt, n_uniq,
+                                    s);
+}
+
+hipError_t exact_kpn(const uint64_t *uniq, const unsigned long long *n_uniq, size_t max_n,
+                     uint64_t pool, uint32_t *kpn, hipStream_t s) {
+  if (!pool || !max_n) return hipSuccess;
+  FastMod fm;
+  fm.p = pool;
+  fm.magic = (~0ULL) / pool;
+  hipLaunchKernelGGL(k_kpn, dim3(grid_for(max_n, 8192)), dim3(256), 0, s, uniq, n_uniq, fm, kpn);
+  return hipGetLastError();
+}
+
+hipError_t exact_lookup(const uint64_t *uniq, const uint32_t *cnt,
+                        const unsigned long long *n_uniq, const uint64_t *q, size_t nq,
+                        uint32_t *out, uint32_t *present, hipStream_t s) {
+  if (!nq) return hipSuccess;
+  hipLaunchKernelGGL(k_lookup, dim3(grid_for(nq, 4096)), dim3(256), 0, s, uniq, cnt, n_uniq, q,
+                     (uint64_t)nq, out, present);
+  return hipGetLastError();
+}
+
+hipError_t delta_clear(const DeltaArgs &d, hipStream_t s) {
+  hipLaunchKernelGGL(k_delta_clear, dim3(grid_for(d.mask + 1, 4096)), dim3(256), 0, s, d);
+  return hipGetLastError();
+}
+
+hipError_t delta_rehash(const DeltaArgs &from, const DeltaArgs &to, hipStream_t s) {
+  hipLaunchKernelGGL(k_delta_rehash, dim3(grid_for(from.mask + 1, 4096)), dim3(256), 0, s, from,
+                     to);
+  return hipGetLastError();
+}
+
+hipError_t seq_accumulate(const uint64_t *keys, const unsigned long long *n_keys, size_t max_n,
+                          uint64_t pool, unsigned long long *currents, uint8_t *touched,
+                          const DeltaArgs &d, const uint64_t *uniq,
+                          const unsigned long long *n_uniq, hipStream_t s) {
+  if (!max_n || !pool) return hipSuccess;
+  FastMod fm;
+  fm.p = pool;
+  fm.magic = (~0ULL) / pool;
+  hipLaunchKernelGGL(k_seq_accumulate, dim3(grid_for(max_n, 4096)), dim3(256), 0, s, keys, n_keys,
+                     fm, currents, touched, d, uniq, n_uniq);
+  return hipGetLastError();
+}
+
+hipError_t seq_lif(uint64_t pool, unsigned long long *currents, uint8_t *touched, uint32_t *kpn,
+                   float *v, uint32_t *r, uint64_t *sc, float thr, float leak, uint32_t refr,
+                   uint32_t *hist, uint64_t *stats, hipStream_t s) {
+  if (!pool) return hipSuccess;
+  hipLaunchKernelGGL(k_seq_lif, dim3(grid_for(pool, 2048)), dim3(256), 0, s, pool, currents,
+                     touched, kpn, v, r, sc, thr, leak, refr, hist,
+                     (unsigned long long *)stats);
+  return hipGetLastError();
+}
+
+hipError_t exact_lookup2(const uint64_t *uniq, const uint32_t *cnt,
+                         const unsigned long long *n_uniq, const DeltaArgs &d, const uint64_t *q,
+                         size_t nq, uint32_t *out, uint32_t *present, hipStream_t s) {
+  if (!nq) return hipSuccess;
+  hipLaunchKernelGGL(k_lookup2, dim3(grid_for(nq, 4096)), dim3(256), 0, s, uniq, cnt, n_uniq, d, q,
+                     (uint64_t)nq, out, present);
+  return hipGetLastError();
+}
+
+hipError_t exact_top_uniques(const TopCand *cand, uint32_t m, const uint32_t *kpn, uint32_t *uniq,
+                             hipStream_t s) {
+  if (!m) return hipSuccess;
+  hipLaunchKernelGGL(k_top_uniques, dim3((m + 255) / 256), dim3(256), 0, s, cand, m, kpn, uniq);
+  return hipGetLastError();
+}
+
+}  // namespace nk

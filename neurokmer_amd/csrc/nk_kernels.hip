@@ -183,7 +183,6 @@ __global__ __launch_bounds__(kBlock) void k_kmers_compat(KmerInput in, int k, Fa
   }
 
   const uint64_t T0 = (uint64_t)blockIdx.x * kTile;
-  const uint32_t sh = (uint32_t)((2 * (k - 1)) & 63);
   uint64_t r = in.tile_rec[blockIdx.x];
   for (int j = 0; j < kPerThread; ++j) {
     const uint64_t p = T0 + (uint64_t)j * kBlock + threadIdx.x;
@@ -191,32 +190,7 @@ __global__ __launch_bounds__(kBlock) void k_kmers_compat(KmerInput in, int k, Fa
     while (r + 1 < in.n_recs && in.offsets[r + 1] <= p) ++r;
     const uint64_t s0 = in.offsets[r], e0 = in.offsets[r + 1];
     if (p < s0 || p + (uint64_t)k > e0) continue;
-    const uint8_t *b = in.bases;
-    uint64_t key;
-    if (CANON) {
-      uint64_t fwd = 0;
-      for (int i = 0; i < 32; ++i) fwd = (fwd << 2) | code_of(b[p + k - 32 + i]);
-      const uint64_t jj = p - s0;
-      uint64_t rev = 0;
-      if (jj < 32) {
-        uint64_t ri = 0;
-        for (int i = 31; i >= 0; --i) ri = (ri << 2) | comp_of(b[s0 + i]);
-        rev = ri >> (2 * jj);
-      }
-      uint64_t umax = sh / 2;
-      if (jj >= 1 && jj - 1 < umax) umax = jj - 1;
-      if (jj >= 1)
-        for (uint64_t uu = 0; uu <= umax; ++uu)
-          rev |= (uint64_t)comp_of(b[p + k - 1 - uu]) << (sh - 2 * uu);
-      key = fwd < rev ? fwd : rev;
-    } else {
-      uint64_t pk = 0;
-      for (int i = 0; i < k; ++i) {
-        uint8_t bb = b[p + i];
-        if (valid_byte(bb)) pk = (pk << 2) | code_of(bb);
-      }
-      key = pk;
-    }
+    const uint64_t key = compat_key<CANON>(in.bases, s0, p, k);
     const uint64_t idx = fastmod(sip13_u64(key), fm);
     if (MODE == 0) {
       atomicAdd(&currents[idx], 1ULL);

@@ -238,6 +238,39 @@ __device__ __forceinline__ Key128 window_key128(const TileLds<TILE, RAW> &L, int
   }
 }
 
+// k > 32, NK_KMER_COMPAT: the reference's release-build key of the window at
+// absolute position p of the record starting at s0 (src/models.rs:188,
+// 192-194,260-266; src/utils.rs:36): forward = the last 32 bases; reverse =
+// the masked-shift residue of init for the first 32 slides plus the last
+// <= 31 inserted complements at bit (2(k-1) & 63) - 2t.
+template <bool CANON>
+__device__ __forceinline__ uint64_t compat_key(const uint8_t *b, uint64_t s0, uint64_t p, int k) {
+  if (CANON) {
+    const uint32_t sh = (uint32_t)((2 * (k - 1)) & 63);
+    uint64_t fwd = 0;
+    for (int i = 0; i < 32; ++i) fwd = (fwd << 2) | code_of(b[p + k - 32 + i]);
+    const uint64_t jj = p - s0;
+    uint64_t rev = 0;
+    if (jj < 32) {
+      uint64_t ri = 0;
+      for (int i = 31; i >= 0; --i) ri = (ri << 2) | comp_of(b[s0 + i]);
+      rev = ri >> (2 * jj);
+    }
+    uint64_t umax = sh / 2;
+    if (jj >= 1 && jj - 1 < umax) umax = jj - 1;
+    if (jj >= 1)
+      for (uint64_t uu = 0; uu <= umax; ++uu)
+        rev |= (uint64_t)comp_of(b[p + k - 1 - uu]) << (sh - 2 * uu);
+    return fwd < rev ? fwd : rev;
+  }
+  uint64_t pk = 0;
+  for (int i = 0; i < k; ++i) {
+    const uint8_t bb = b[p + i];
+    if (valid_byte(bb)) pk = (pk << 2) | code_of(bb);
+  }
+  return pk;
+}
+
 // Same key straight from global memory (rare: uniques hits only).
 template <bool CANON>
 __device__ __forceinline__ uint64_t global_window_key(const uint8_t *b, uint64_t p, int k) {

@@ -400,3 +400,96 @@ def test_full_size_properties(shape):
     pb = np.concatenate(segs)
     gg, rr = run_both(pb, po, 31, 2_000_000, True)
     assert_same(gg, rr)
+
+
+# ---- exact k-mer table and process_sequence (§8f-3) --------
+def _keys_of(bases, offs, k, canon, width=64):
+    out = set()
+    for i in range(offs.size - 1):
+        rec = bases[int(offs[i]):int(offs[i + 1])].tobytes()
+        out.update(int(x) for x in cbind.kmer_keys(rec, k, canon))
+    return out
+
+
+def assert_exact_same(g, r, keys, pool):
+    np.testing.assert_array_equal(g.kmer_per_neuron(), r.kmer_per_neuron())
+    assert g.distinct_kmers() == r.distinct_kmers()
+    rng = np.random.default_rng(len(keys))
+    probe = sorted(keys)
+    probe += [int(x) for x in rng.integers(0, 2**63, 500, dtype=np.uint64)]  # mostly absent
+    cnt, pres = g.get_counts(np.array(probe, dtype=np.uint64))
+    for kk, c, p in zip(probe, cnt, pres):
+        want = r.get_count(kk)
+        assert (int(c) if p else None) == want, kk
+    if probe:
+        assert g.get_count(probe[0]) == r.get_count(probe[0])
+
+
+@pytest.mark.parametrize("k,canon", [(21, True), (21, False), (31, True), (32, False),
+                                     (33, True), (40, False), (5, True)])
+def test_exact_counts_table(k, canon):
+    bases, offs = ragged_records(total=90_000, n_rate=0.01, mixed_case=True, seed=300 + k,
+                                 repeats_per_mb=20_000, motif_len=70)
+    g = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, 4099, canon, exact_counts=True)
+    r = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, 4099, canon)
+    g.process_parallel_arrays(bases, offs)
+    r.process_parallel_arrays(bases, offs)
+    assert_same(g, r)
+    assert_exact_same(g, r, _keys_of(bases, offs, k, canon), 4099)
+
+
+def test_exact_counts_partitioned_config2_shape():
+    # the metric's path (k=31, pool 2M, partitioned count) with the table on
+    bases, offs = synth.make_records(2_000_000, 7, repeats_per_mb=64, motif_len=200, seed=3)
+    g = SpikingKmerCounter(31, 1.0, 0.95, 2, 1.0, 2_000_000, True, exact_counts=True)
+    r = cbind.OracleCounter(31, 1.0, 0.95, 2, 1.0, 2_000_000, True)
+    g.process_parallel_arrays(bases, offs)
+    r.process_parallel_arrays(bases, offs)
+    assert_same(g, r)
+    np.testing.assert_array_equal(g.kmer_per_neuron(), r.kmer_per_neuron())
+    assert g.distinct_kmers() == r.distinct_kmers()
+
+
+def test_get_count_needs_exact_counts():
+    g = SpikingKmerCounter(21, 1.0, 0.95, 2, 1.0, 1000, True)
+    with pytest.raises(_lib.NeuroKmerError) as e:
+        g.get_count(5)
+    assert e.value.code == _lib.NK_E_UNSUPPORTED
+    with pytest.raises(_lib.NeuroKmerError):
+        g.process_sequence(b"ACGT" * 20)
+    with pytest.raises(_lib.NeuroKmerError):
+        SpikingKmerCounter(31, 1.0, 0.95, 2, 1.0, 1000, True, exact_counts=True, kmer_width=128)
+
+
+@pytest.mark.parametrize("canon", [True, False])
+def test_process_sequence_matches_reference(canon):
+    """process_parallel, then reads through process_sequence (single LIF step,
+    accumulating counts and kmer_per_neuron), a reset, more reads."""
+    k, pool = 17, 997
+    bases, offs = synth.make_records(60_000, 4, repeats_per_mb=30_000, motif_len=50, seed=8,
+                                     n_rate=0.003)
+    reads, roffs = synth.make_reads(120, 90, seed=9)
+    rl = synth.records_list(reads, roffs)
+    rl[3] = rl[3][:10]           # shorter than k: no-op
+    rl[5] = b"N" * 40 + rl[5]    # invalid bytes
+    g = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, canon, exact_counts=True)
+    r = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, canon)
+    g.process_parallel_arrays(bases, offs)
+    r.process_parallel_arrays(bases, offs)
+    keys = _keys_of(bases, offs, k, canon)
+    for i, rd in enumerate(rl):
+        g.process_sequence(rd)
+        r.process_sequence(rd)
+        keys.update(int(x) for x in cbind.kmer_keys(rd, k, canon))
+        if i % 30 == 29:
+            assert_same(g, r)
+            assert_exact_same(g, r, keys, pool)
+    g.reset()
+    r2 = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, canon)
+    keys2 = set()
+    for rd in rl[:40]:
+        g.process_sequence(rd)
+        r2.process_sequence(rd)
+        keys2.update(int(x) for x in cbind.kmer_keys(rd, k, canon))
+    assert_same(g, r2)
+    assert_exact_same(g, r2, keys2, pool)
