@@ -92,8 +92,15 @@ int nk_process_parallel_device(nk_counter *c, const uint8_t *d_bases,
                                size_t n_bases, void *stream);
 
 /* SpikingKmerCounter::process_file_streaming(&mut self, path)
- * — src/spiking_hash.rs:277-486 (FASTA/FASTQ, format from the first byte). */
+ * — src/spiking_hash.rs:277-486 (FASTA/FASTQ, format from the first byte;
+ * gzip read transparently).  The file is parsed on the device in chunks that
+ * are counted as they arrive (GPU FASTX ingest, needletail's rules as the host
+ * reader restates them); a FASTQ file with blank lines between records goes
+ * through the host reader instead. */
 int nk_process_file_streaming(nk_counter *c, const char *path);
+/* The CLI's in-memory mode from a file: stream_sequences(path).collect() then
+ * process_parallel (src/main.rs:40-46), through the same GPU ingest. */
+int nk_process_file_parallel(nk_counter *c, const char *path);
 
 /* Split-phase form of the two calls above, for multi-GPU use (one process per
  * GPU; the caller all-reduces the u64 currents between the phases):

@@ -28,7 +28,7 @@ NK_KMER_128 = 1
 # every symbol include/neurokmer.h declares
 EXPORTS = (
     "nk_opts_default", "nk_new", "nk_free", "nk_process_parallel", "nk_process_parallel_device",
-    "nk_process_file_streaming", "nk_accumulate_device", "nk_finalize", "nk_top_kmers",
+    "nk_process_file_streaming", "nk_process_file_parallel", "nk_accumulate_device", "nk_finalize", "nk_top_kmers",
     "nk_merge_top_kmers", "nk_top_abundant_neurons", "nk_get_count", "nk_get_counts",
     "nk_distinct_kmers", "nk_copy_kmer_per_neuron", "nk_process_sequence", "nk_total_spikes",
     "nk_energy_used", "nk_set_steps", "nk_get_steps", "nk_pool_size", "nk_k",
@@ -89,6 +89,7 @@ def load(share_torch: bool = True):
         "nk_process_parallel": (C.c_int, [vp, vp, vp, sz]),
         "nk_process_parallel_device": (C.c_int, [vp, vp, vp, sz, sz, vp]),
         "nk_process_file_streaming": (C.c_int, [vp, C.c_char_p]),
+        "nk_process_file_parallel": (C.c_int, [vp, C.c_char_p]),
         "nk_accumulate_device": (C.c_int, [vp, vp, vp, sz, sz, vp]),
         "nk_finalize": (C.c_int, [vp, C.c_int, vp]),
         "nk_top_kmers": (C.c_int, [vp, P(vp), P(sz)]),

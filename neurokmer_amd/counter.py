@@ -103,8 +103,12 @@ class SpikingKmerCounter:
                                                  stream or None))
 
     def process_file_streaming(self, path: str) -> None:
-        """src/spiking_hash.rs:277-486."""
+        """src/spiking_hash.rs:277-486 (GPU FASTX ingest)."""
         check(self._L.nk_process_file_streaming(self._h, str(path).encode()))
+
+    def process_file_parallel(self, path: str) -> None:
+        """stream_sequences(path).collect() + process_parallel (src/main.rs:40-46)."""
+        check(self._L.nk_process_file_parallel(self._h, str(path).encode()))
 
     # split phase (multi-GPU: allreduce currents between the two)
     def accumulate_device(self, d_bases: int, d_offsets: int, n_recs: int, n_bases: int,

@@ -107,16 +107,9 @@ int main(int argc, char **argv) {
     printf("Starting streaming for: %s\n", input.c_str());
     rc = nk_process_file_streaming(c, input.c_str());
   } else {
-    std::vector<uint8_t> bases;
-    std::vector<uint64_t> offs;
-    std::string err;
-    rc = nk::read_fastx_all(input.c_str(), bases, offs, err);
-    if (rc) {
-      fprintf(stderr, "Error: %s\n", err.c_str());
-      nk_free(c);
-      return 1;
-    }
-    rc = nk_process_parallel(c, bases.data(), offs.data(), offs.size() - 1);
+    // stream_sequences(input).collect() + process_parallel (src/main.rs:40-46),
+    // parsed on the device (nk_process_file_parallel)
+    rc = nk_process_file_parallel(c, input.c_str());
     if (!rc) {
       std::vector<uint64_t> cur(nk_pool_size(c));
       unsigned long long tot = 0;

@@ -8,6 +8,7 @@
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
+#include <zlib.h>
 
 #include <algorithm>
 #include <string>
@@ -16,6 +17,7 @@
 #include "neurokmer.h"
 #include "nk_exact.h"
 #include "nk_fastx.h"
+#include "nk_ingest.h"
 #include "nk_kernels.h"
 
 using namespace nk;
@@ -820,14 +822,44 @@ int nk_process_parallel(nk_counter *c, const uint8_t *bases, const uint64_t *off
   return process_host(c, bases, offs, n_recs, 0);
 }
 
-int nk_process_file_streaming(nk_counter *c, const char *path) {
+static int ingest_file(nk_counter *c, const char *path, bool *fallback);
+
+// A FASTA/FASTQ file through the GPU ingest (nk_ingest.h), then the LIF rule of
+// process_file_streaming (streaming = 1, src/spiking_hash.rs:277-486) or of
+// process_parallel over the file's records (streaming = 0, src/main.rs:45-46).
+static int process_file(nk_counter *c, const char *path, int streaming) {
   if (!c) return fail(NK_E_INVALID, "null counter");
-  std::vector<uint8_t> bases;
-  std::vector<uint64_t> offs;
-  std::string err;
-  int rc = read_fastx_all(path, bases, offs, err);
-  if (rc) return fail(rc, "%s", err.c_str());
-  return process_host(c, bases.data(), offs.data(), offs.size() - 1, 1);
+  if (!path) return fail(NK_E_INVALID, "null path");
+  bool fallback = c->pool == 0;  // pool 0: the host path checks for k-mers (% 0)
+  int rc;
+  if (!fallback) {
+    rc = ingest_file(c, path, &fallback);
+    if (rc) return rc;
+  }
+  if (fallback) {  // the host reader (nk_fastx.cpp): blank lines between FASTQ records
+    std::vector<uint8_t> bases;
+    std::vector<uint64_t> offs;
+    std::string err;
+    rc = read_fastx_all(path, bases, offs, err);
+    if (rc) return fail(rc, "%s", err.c_str());
+    return process_host(c, bases.data(), offs.data(), offs.size() - 1, streaming);
+  }
+  hipStream_t s = c->own_stream;
+  HIPCHK(mark(c, 0, s));
+  HIPCHK(mark(c, 1, s));
+  HIPCHK(mark(c, 2, s));
+  if ((rc = lif_top_uniques(c, streaming, c->opts.exact_counts && c->exact_built, s))) return rc;
+  c->top_valid = true;
+  collect_timings(c, true);
+  return NK_OK;
+}
+
+int nk_process_file_streaming(nk_counter *c, const char *path) {
+  return process_file(c, path, 1);
+}
+
+int nk_process_file_parallel(nk_counter *c, const char *path) {
+  return process_file(c, path, 0);
 }
 
 int nk_top_kmers(nk_counter *c, const uint64_t **d_keys, size_t *n_keys) {
@@ -966,6 +998,234 @@ static int need_exact(nk_counter *c) {
   if (!c) return fail(NK_E_INVALID, "null counter");
   if (!c->opts.exact_counts)
     return fail(NK_E_UNSUPPORTED, "the exact k-mer table needs nk_opts.exact_counts = 1");
+  return NK_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Chunked accumulate over a growing resident input (GPU FASTX ingest)
+// ---------------------------------------------------------------------------
+struct StreamAcc {
+  bool part = false;
+  uint64_t tile = kTile;
+  uint32_t slices = 0;
+  PartArgs pa{};
+};
+
+// zero the accumulators and size the partition arena for ~est_bases bases
+static int acc_begin(nk_counter *c, uint64_t est_bases, StreamAcc &sa, hipStream_t s) {
+  int rc;
+  const uint64_t B = (c->pool + kBinsPerBucket - 1) >> kBinBits;
+  sa.part = !c->w128 && c->k <= 32 && c->pool > 0 && B <= (uint64_t)kMaxBuckets;
+  sa.tile = sa.part ? kPartTile : kTile;
+  ZeroList z{};
+  z.ptr[z.n] = c->cur.p; z.bytes[z.n++] = c->pool * 8;
+  if (sa.part) {
+    uint64_t cap = std::max<uint64_t>(est_bases, 1) / B * 5 / 4 + 4 * kPartTile;
+    cap = (cap + 63) & ~63ull;
+    sa.slices = (uint32_t)std::max<uint64_t>(1, 256 / B);
+    // segments per bucket: one per tile per launch; chunk-straddling tiles add a few
+    const uint64_t max_segs = n_tiles_for(std::max<uint64_t>(est_bases, 1), kPartTile) + 4096;
+    if ((rc = c->p_off.ensure(B * cap)) || (rc = c->p_pos.ensure(B * cap)) ||
+        (rc = c->p_fill.ensure(B)) || (rc = c->p_desc.ensure(B * max_segs)) ||
+        (rc = c->p_over.ensure(B)) || (rc = c->partials.ensure(sa.slices * c->pool)))
+      return rc;
+    sa.pa.n_buckets = (uint32_t)B;
+    sa.pa.cap = cap;
+    sa.pa.off = c->p_off.p;
+    sa.pa.pos = c->p_pos.p;
+    sa.pa.fill = c->p_fill.p;
+    sa.pa.desc = c->p_desc.p;
+    sa.pa.max_segs = max_segs;
+    sa.pa.overflow = c->p_over.p;
+    sa.pa.currents = (unsigned long long *)c->cur.p;
+    z.ptr[z.n] = c->p_fill.p; z.bytes[z.n++] = B * 8;
+    z.ptr[z.n] = c->p_over.p; z.bytes[z.n++] = B * 4;
+  }
+  z.ptr[z.n] = c->hist.p;  z.bytes[z.n++] = kHistBins * kHistCopies * 4;
+  z.ptr[z.n] = c->stats.p; z.bytes[z.n++] = 16;
+  c->lif_zeroed = true;
+  if (c->pool) HIPCHK(launch_zero(z, s));
+  c->cur_fresh = false;
+  c->part_used = sa.part;
+  return NK_OK;
+}
+
+// count the windows that start in [pos_lo, pos_hi) of the resident input
+static int acc_batch(nk_counter *c, StreamAcc &sa, const KmerInput &whole, uint64_t pos_lo,
+                     uint64_t pos_hi, hipStream_t s) {
+  if (pos_hi <= pos_lo || !c->pool) return NK_OK;
+  KmerInput in = whole;
+  in.tile_base = pos_lo / sa.tile;
+  in.n_tiles = (pos_hi + sa.tile - 1) / sa.tile - in.tile_base;
+  in.pos_lo = pos_lo;
+  in.pos_hi = pos_hi;
+  int rc = c->tile_rec.ensure(in.n_tiles);
+  if (rc) return rc;
+  in.tile_rec = c->tile_rec.p;
+  HIPCHK(launch_tile_rec(in, sa.tile, c->tile_rec.p, s));
+  if (sa.part)
+    HIPCHK(launch_part(in, (int)c->k, c->canonical, c->pool, sa.pa, s));
+  else if (c->w128)
+    HIPCHK(launch_count128(in, (int)c->k, c->canonical, c->pool, c->cur.p, s));
+  else
+    HIPCHK(launch_count(in, (int)c->k, c->canonical, c->pool, c->cur.p, s));
+  return NK_OK;
+}
+
+// bucket histograms (folded into the LIF kernel of the process call) and the
+// bookkeeping of a finished input
+static int acc_end(nk_counter *c, StreamAcc &sa, const KmerInput &whole, hipStream_t s) {
+  int rc;
+  if (sa.part) {
+    HIPCHK(launch_bucket_hist(sa.pa, c->pool, sa.slices, c->partials.p, s));
+    c->pend_slices = sa.slices;
+    c->last_pa = sa.pa;
+  }
+  c->last_in = whole;
+  c->last_in.n_tiles = n_tiles_for(whole.n_bases, sa.tile);
+  c->have_input = true;
+  c->top_valid = false;
+  if (c->opts.exact_counts && (rc = build_exact(c, whole, s))) return rc;
+  return NK_OK;
+}
+
+static size_t ingest_chunk_bytes() {
+  const char *e = getenv("NK_INGEST_CHUNK");  // tests: small chunks exercise the carries
+  size_t v = e ? (size_t)strtoull(e, nullptr, 10) : 0;
+  if (v < 64) v = (size_t)64 << 20;
+  return v;
+}
+
+// Parse a FASTA/FASTQ file on the device in chunks and count it as it arrives
+// (src/spiking_hash.rs:277-486 semantics for the records; the caller runs the
+// LIF rule).  *fallback: the file needs the host reader (a blank line between
+// FASTQ records).
+static int ingest_file(nk_counter *c, const char *path, bool *fallback) {
+  *fallback = false;
+  gzFile f = gzopen(path, "rb");
+  if (!f) return fail(NK_E_IO, "cannot open %s", path);
+  gzbuffer(f, 1 << 20);
+  struct FileCloser {
+    gzFile f;
+    ~FileCloser() { gzclose(f); }
+  } closer{f};
+  uint64_t fsize = 0;
+  bool gz = false;
+  {
+    FILE *raw = fopen(path, "rb");
+    if (raw) {
+      unsigned char m[2] = {0, 0};
+      gz = fread(m, 1, 2, raw) == 2 && m[0] == 0x1f && m[1] == 0x8b;
+      fseeko(raw, 0, SEEK_END);
+      fsize = (uint64_t)ftello(raw);
+      fclose(raw);
+    }
+  }
+  (void)hipSetDevice(c->device);
+  hipStream_t s = c->own_stream;
+  int rc;
+  size_t chunk = ingest_chunk_bytes();
+  std::vector<uint8_t> hb;  // carry + chunk (host)
+  hb.resize(chunk);
+  size_t have = 0;
+  auto read_more = [&](size_t want) -> size_t {
+    if (hb.size() < have + want) hb.resize(have + want);
+    size_t got = 0;
+    while (got < want) {
+      const int n = gzread(f, hb.data() + have + got, (unsigned)std::min<size_t>(want - got, 1u << 30));
+      if (n <= 0) break;
+      got += (size_t)n;
+    }
+    have += got;
+    return got;
+  };
+  bool eof = read_more(chunk) < chunk;
+  if (!have) return fail(NK_E_PARSE, "empty file");
+  const bool fastq = hb[0] == '@';
+  if (hb[0] != '>' && !fastq)
+    return fail(NK_E_PARSE, "unknown format: first byte is neither '>' nor '@'");
+  // resident input: the file size bounds the bases of a plain file
+  uint64_t cap_bases = (gz ? 4 * fsize : fsize) + 64;
+  uint64_t cap_recs = 1024;
+  if ((rc = c->in_bases.ensure(cap_bases + 16)) || (rc = c->in_offs.ensure(cap_recs + 1)))
+    return rc;
+  DevBuf<uint8_t> draw, scratch;
+  DevBuf<IngestState> dst;
+  if ((rc = draw.ensure(chunk)) || (rc = scratch.ensure(ingest_scratch_bytes(chunk))) ||
+      (rc = dst.ensure(1)))
+    return rc;
+  IngestState st{};
+  st.at_line_start = 1;
+  HIPCHK(hipMemcpyAsync(dst.p, &st, sizeof st, hipMemcpyHostToDevice, s));
+  StreamAcc sa;
+  if ((rc = acc_begin(c, fastq ? cap_bases / 2 : cap_bases, sa, s))) return rc;
+  uint64_t counted = 0;  // windows below this start were counted
+  for (;;) {
+    const size_t len = have;
+    // capacity of the resident buffers for this chunk (grow: wait, copy, free)
+    const uint64_t need_b = st.data_end + len + 64, need_r = st.n_rec + len / 2 + 4;
+    if (need_b > c->in_bases.n || need_r + 1 > c->in_offs.n) {
+      HIPCHK(hipStreamSynchronize(s));
+      if (need_b > c->in_bases.n) {
+        DevBuf<uint8_t> nb;
+        if ((rc = nb.ensure(std::max<uint64_t>(need_b, 2 * c->in_bases.n)))) return rc;
+        HIPCHK(hipMemcpy(nb.p, c->in_bases.p, st.data_end, hipMemcpyDeviceToDevice));
+        std::swap(nb.p, c->in_bases.p);
+        std::swap(nb.n, c->in_bases.n);
+        nb.release();
+      }
+      if (need_r + 1 > c->in_offs.n) {
+        DevBuf<uint64_t> no;
+        if ((rc = no.ensure(std::max<uint64_t>(need_r + 1, 2 * c->in_offs.n)))) return rc;
+        HIPCHK(hipMemcpy(no.p, c->in_offs.p, (st.n_rec + 1) * 8, hipMemcpyDeviceToDevice));
+        std::swap(no.p, c->in_offs.p);
+        std::swap(no.n, c->in_offs.n);
+        no.release();
+      }
+    }
+    if (len > draw.n) {
+      HIPCHK(hipStreamSynchronize(s));
+      if ((rc = draw.ensure(len)) || (rc = scratch.ensure(ingest_scratch_bytes(len)))) return rc;
+    }
+    HIPCHK(hipMemcpyAsync(draw.p, hb.data(), len, hipMemcpyHostToDevice, s));
+    IngestBufs ib{c->in_bases.p, c->in_offs.p, c->in_bases.n, c->in_offs.n - 1, scratch.p};
+    HIPCHK(fastq ? ingest_fastq(draw.p, len, eof, ib, dst.p, s)
+                 : ingest_fasta(draw.p, len, eof, ib, dst.p, s));
+    HIPCHK(hipMemcpyAsync(&st, dst.p, sizeof st, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (fastq && st.blank) {
+      *fallback = true;
+      return NK_OK;
+    }
+    // count what is complete: every window of a FASTQ chunk's records (they
+    // are whole); FASTA: windows that end inside the bases parsed so far
+    KmerInput whole{};
+    whole.bases = c->in_bases.p;
+    whole.offsets = c->in_offs.p;
+    whole.n_recs = st.n_rec;
+    whole.n_bases = st.data_end;
+    const bool last = eof || st.stop;
+    uint64_t hi = st.data_end;
+    if (!fastq && !last) hi = st.data_end >= c->k - 1 ? st.data_end - (c->k - 1) : 0;
+    if (st.n_rec && hi > counted) {
+      if ((rc = acc_batch(c, sa, whole, counted, hi, s))) return rc;
+      counted = hi;
+    }
+    if (last) {
+      if ((rc = acc_end(c, sa, whole, s))) return rc;
+      break;
+    }
+    // next chunk: FASTQ carries its unfinished record's bytes
+    size_t keep = 0;
+    if (fastq) {
+      keep = len - (size_t)st.consumed;
+      if (st.consumed == 0 && keep >= hb.size() / 2) chunk *= 2;  // a record longer than the chunk
+      memmove(hb.data(), hb.data() + st.consumed, keep);
+    }
+    have = keep;
+    const size_t want = chunk > keep ? chunk - keep : chunk;
+    eof = read_more(want) < want;
+  }
   return NK_OK;
 }
 

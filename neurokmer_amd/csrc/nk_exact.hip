@@ -45,8 +45,9 @@ __global__ __launch_bounds__(kXBlock) void k_keys_tile(KmerInput in, int k,
   __shared__ TileLds<kXTile, !CANON> L;
   __shared__ uint32_t s_w[kXBlock / 64];
   __shared__ unsigned long long s_base;
-  const uint64_t T0 = (uint64_t)blockIdx.x * kXTile;
-  stage_tile<kXTile, kXBlock, !CANON>(L, in, blockIdx.x, k);
+  const uint64_t tile = in.tile_base + blockIdx.x;
+  const uint64_t T0 = tile * kXTile;
+  stage_tile<kXTile, kXBlock, !CANON>(L, in, tile, k);
   uint64_t kv[kXPer];  // fixed slots (no dynamic register indexing) + a valid mask
   uint32_t ok = 0;
 #pragma unroll
@@ -54,7 +55,7 @@ __global__ __launch_bounds__(kXBlock) void k_keys_tile(KmerInput in, int k,
     const int q = j * kXBlock + threadIdx.x;
     kv[j] = 0;
     if (T0 + (uint64_t)q + (uint64_t)k > in.n_bases) continue;
-    if (!window_valid(L, T0, q, k, in.n_bases)) continue;
+    if (!window_valid(L, T0, q, k, in.n_bases, in.pos_lo, in.pos_hi)) continue;
     kv[j] = window_key<kXTile, !CANON, CANON>(L, q, k);
     ok |= 1u << j;
   }
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(kXBlock) void k_keys_compat(KmerInput in, int k,
                                                          unsigned long long *__restrict__ n_keys) {
   __shared__ uint32_t s_w[kXBlock / 64];
   __shared__ unsigned long long s_base;
-  const uint64_t T0 = (uint64_t)blockIdx.x * kXTile;
+  const uint64_t T0 = (in.tile_base + blockIdx.x) * kXTile;
   uint64_t r = in.tile_rec[blockIdx.x];
   uint64_t kv[kXPer];
   uint32_t ok = 0;
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(kXBlock) void k_keys_compat(KmerInput in, int k,
   for (int j = 0; j < kXPer; ++j) {
     kv[j] = 0;
     const uint64_t p = T0 + (uint64_t)j * kXBlock + threadIdx.x;
-    if (p >= in.n_bases) continue;
+    if (p >= in.n_bases || p < in.pos_lo || p >= in.pos_hi) continue;
     while (r + 1 < in.n_recs && in.offsets[r + 1] <= p) ++r;
     const uint64_t s0 = in.offsets[r], e0 = in.offsets[r + 1];
     if (p < s0 || p + (uint64_t)k > e0) continue;

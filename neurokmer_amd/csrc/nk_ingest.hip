@@ -1,0 +1,471 @@
+// nk_ingest.hip — GPU FASTA/FASTQ parse of one raw chunk (nk_ingest.h).
+//
+// FASTA (5 launches, 3 passes over the chunk): A per 4-KiB block: the last
+// line start and the header lines that start in it; B one block: exclusive
+// max-scan of the line starts and sum-scan of the headers; C per block: the
+// base bytes (now that every byte's line kind is known); D one block: scan of
+// the base counts, the new totals and the carried line state; E per block:
+// scatter of the bases and of the record offsets.
+//
+// FASTQ (the chunk starts at a record boundary): A newline counts; B scan; C
+// newline positions; D per record: the four lines' validity and the sequence
+// length; E one block: first bad record, sequence offsets, new totals; F one
+// wave per record: copy of the sequence bytes.
+#include "nk_ingest.h"
+
+namespace nk {
+
+namespace {
+
+constexpr int kIB = 256;              // threads per block
+constexpr int kIPer = 16;             // bytes per thread
+constexpr int kIS = kIB * kIPer;      // bytes per block
+constexpr int kScanT = 1024;          // threads of the single-block scans
+
+struct FaScratch {
+  long long *ls;              // [NB] last line start in the block (-1: none)
+  unsigned long long *hdr;    // [NB] header lines starting in the block
+  unsigned long long *keep;   // [NB] base bytes in the block
+  unsigned long long base_out, rec_base;  // resident positions of this chunk
+};
+
+__device__ __forceinline__ bool is_ls(const uint8_t *R, uint64_t i, uint32_t at_line_start) {
+  return i == 0 ? at_line_start != 0 : R[i - 1] == '\n';
+}
+
+// exclusive block scans over up to 1024 threads
+template <typename T, typename Op>
+__device__ T block_scan_excl(T x, T ident, Op op, T *s_w, T *total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  T incl = x;
+  for (int o = 1; o < 64; o <<= 1) {
+    const T y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl = op(incl, y);
+  }
+  if (lane == 63) s_w[w] = incl;
+  __syncthreads();
+  T pre = ident, tot = ident;
+  for (int i = 0; i < nw; ++i) {
+    if (i < w) pre = op(pre, s_w[i]);
+    tot = op(tot, s_w[i]);
+  }
+  __syncthreads();
+  *total = tot;
+  // exclusive within the wave: shift the inclusive value by one lane
+  T ex = __shfl_up(incl, 1, 64);
+  if (lane == 0) ex = ident;
+  return op(pre, ex);
+}
+struct OpAdd {
+  __device__ unsigned long long operator()(unsigned long long a, unsigned long long b) const {
+    return a + b;
+  }
+};
+struct OpMax {
+  __device__ long long operator()(long long a, long long b) const { return a > b ? a : b; }
+};
+
+// ---- FASTA ------------------------------------------------------------------
+__global__ __launch_bounds__(kIB) void k_fa_a(const uint8_t *__restrict__ R, uint64_t L,
+                                              const IngestState *__restrict__ st, FaScratch f) {
+  __shared__ long long s_l[kIB / 64];
+  __shared__ unsigned long long s_h[kIB / 64];
+  const uint64_t b0 = (uint64_t)blockIdx.x * kIS + (uint64_t)threadIdx.x * kIPer;
+  const uint32_t als = st->at_line_start;
+  long long last = -1;
+  unsigned long long h = 0;
+  for (int j = 0; j < kIPer; ++j) {
+    const uint64_t i = b0 + j;
+    if (i >= L) break;
+    if (is_ls(R, i, als)) {
+      last = (long long)i;
+      h += R[i] == '>';
+    }
+  }
+  long long tl;
+  unsigned long long th;
+  block_scan_excl<long long>(last, -1LL, OpMax(), s_l, &tl);
+  block_scan_excl<unsigned long long>(h, 0ull, OpAdd(), s_h, &th);
+  if (threadIdx.x == 0) {
+    f.ls[blockIdx.x] = tl;
+    f.hdr[blockIdx.x] = th;
+  }
+}
+
+// in-place exclusive scans of the per-block arrays (one block of kScanT)
+template <typename T, typename Op>
+__device__ void scan_array_excl(T *a, uint64_t n, T ident, Op op, T *s_w, T *total_out) {
+  const uint64_t per = (n + kScanT - 1) / kScanT;
+  const uint64_t lo = threadIdx.x * per, hi = lo + per < n ? lo + per : n;
+  T loc = ident;
+  for (uint64_t i = lo; i < hi; ++i) loc = op(loc, a[i]);
+  T tot;
+  T run = block_scan_excl<T>(loc, ident, op, s_w, &tot);
+  for (uint64_t i = lo; i < hi; ++i) {
+    const T v = a[i];
+    a[i] = run;
+    run = op(run, v);
+  }
+  if (total_out) *total_out = tot;
+}
+
+__global__ __launch_bounds__(kScanT) void k_fa_b(uint64_t NB, FaScratch f) {
+  __shared__ long long s_l[kScanT / 64];
+  __shared__ unsigned long long s_h[kScanT / 64];
+  scan_array_excl<long long>(f.ls, NB, -1LL, OpMax(), s_l, nullptr);
+  scan_array_excl<unsigned long long>(f.hdr, NB, 0ull, OpAdd(), s_h, nullptr);
+}
+
+// header kind of the line holding byte i, given the line start at or before
+// it (ls >= 0) or the carried state
+__device__ __forceinline__ bool line_hdr(const uint8_t *R, long long ls, const IngestState &st) {
+  return ls >= 0 ? R[ls] == '>' : st.line_is_hdr != 0;
+}
+
+// per thread: my 16 bytes' line starts folded with the block carry; returns
+// the line start in effect before my first byte
+__device__ __forceinline__ long long thread_carry_ls(const uint8_t *R, uint64_t L, uint64_t b0,
+                                                     uint32_t als, long long blk_carry,
+                                                     long long *s_l) {
+  long long last = -1;
+  for (int j = 0; j < kIPer; ++j) {
+    const uint64_t i = b0 + j;
+    if (i >= L) break;
+    if (is_ls(R, i, als)) last = (long long)i;
+  }
+  long long tot;
+  const long long ex = block_scan_excl<long long>(last, -1LL, OpMax(), s_l, &tot);
+  return ex > blk_carry ? ex : blk_carry;
+}
+
+__global__ __launch_bounds__(kIB) void k_fa_c(const uint8_t *__restrict__ R, uint64_t L,
+                                              const IngestState *__restrict__ st, FaScratch f) {
+  __shared__ long long s_l[kIB / 64];
+  __shared__ unsigned long long s_k[kIB / 64];
+  const IngestState S = *st;
+  const uint64_t b0 = (uint64_t)blockIdx.x * kIS + (uint64_t)threadIdx.x * kIPer;
+  long long ls = thread_carry_ls(R, L, b0, S.at_line_start, f.ls[blockIdx.x], s_l);
+  unsigned long long keep = 0;
+  bool hdr = line_hdr(R, ls, S);
+  for (int j = 0; j < kIPer; ++j) {
+    const uint64_t i = b0 + j;
+    if (i >= L) break;
+    if (is_ls(R, i, S.at_line_start)) hdr = R[i] == '>';
+    const uint8_t c = R[i];
+    keep += !hdr && c != '\n' && c != '\r';
+  }
+  unsigned long long tk;
+  block_scan_excl<unsigned long long>(keep, 0ull, OpAdd(), s_k, &tk);
+  if (threadIdx.x == 0) f.keep[blockIdx.x] = tk;
+}
+
+__global__ __launch_bounds__(kScanT) void k_fa_d(const uint8_t *__restrict__ R, uint64_t L,
+                                                 uint64_t NB, IngestState *__restrict__ st,
+                                                 FaScratch *__restrict__ fs, uint64_t *offsets) {
+  __shared__ unsigned long long s_k[kScanT / 64];
+  __shared__ unsigned long long s_tot;
+  unsigned long long tk;
+  scan_array_excl<unsigned long long>(fs->keep, NB, 0ull, OpAdd(), s_k, &tk);
+  if (threadIdx.x == 0) s_tot = tk;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  IngestState S = *st;
+  // headers in this chunk: exclusive prefix of the last block + its own count
+  unsigned long long nh = 0;
+  {
+    const uint64_t b = NB - 1;
+    nh = fs->hdr[b];
+    for (uint64_t i = b * kIS; i < L; ++i) nh += is_ls(R, i, S.at_line_start) && R[i] == '>';
+  }
+  // the line state after the chunk: the last line start = the blocks before
+  // the last one (exclusive max-scan) or one in the last block
+  long long last_ls = fs->ls[NB - 1];
+  for (uint64_t i = (NB - 1) * kIS; i < L; ++i)
+    if (is_ls(R, i, S.at_line_start)) last_ls = (long long)i;
+  const bool ends_nl = L > 0 && R[L - 1] == '\n';
+  uint32_t hdr_after = S.line_is_hdr;
+  if (!ends_nl && L > 0) hdr_after = line_hdr(R, last_ls, S) ? 1u : 0u;
+  fs->base_out = S.data_end;
+  fs->rec_base = S.n_rec;
+  S.data_end += s_tot;
+  S.n_rec += nh;
+  S.at_line_start = L == 0 ? S.at_line_start : (ends_nl ? 1u : 0u);
+  S.line_is_hdr = ends_nl ? 0u : hdr_after;
+  *st = S;
+  offsets[S.n_rec] = S.data_end;  // provisional end of the last record
+}
+
+__global__ __launch_bounds__(kIB) void k_fa_e(const uint8_t *__restrict__ R, uint64_t L,
+                                              const IngestState *__restrict__ st_before,
+                                              const FaScratch *__restrict__ fs, FaScratch f,
+                                              uint8_t *__restrict__ bases,
+                                              uint64_t *__restrict__ offsets) {
+  __shared__ long long s_l[kIB / 64];
+  __shared__ unsigned long long s_k[kIB / 64], s_h[kIB / 64];
+  const IngestState S = *st_before;  // the state the chunk started from
+  const uint64_t b0 = (uint64_t)blockIdx.x * kIS + (uint64_t)threadIdx.x * kIPer;
+  long long ls = thread_carry_ls(R, L, b0, S.at_line_start, f.ls[blockIdx.x], s_l);
+  unsigned long long keep = 0, h = 0;
+  bool hdr = line_hdr(R, ls, S);
+  for (int j = 0; j < kIPer; ++j) {
+    const uint64_t i = b0 + j;
+    if (i >= L) break;
+    if (is_ls(R, i, S.at_line_start)) {
+      hdr = R[i] == '>';
+      h += hdr;
+    }
+    const uint8_t c = R[i];
+    keep += !hdr && c != '\n' && c != '\r';
+  }
+  unsigned long long tk, th;
+  unsigned long long kp = block_scan_excl<unsigned long long>(keep, 0ull, OpAdd(), s_k, &tk);
+  unsigned long long hp = block_scan_excl<unsigned long long>(h, 0ull, OpAdd(), s_h, &th);
+  kp += fs->base_out + f.keep[blockIdx.x];
+  hp += fs->rec_base + f.hdr[blockIdx.x];
+  hdr = line_hdr(R, ls, S);
+  for (int j = 0; j < kIPer; ++j) {
+    const uint64_t i = b0 + j;
+    if (i >= L) break;
+    if (is_ls(R, i, S.at_line_start)) {
+      hdr = R[i] == '>';
+      if (hdr) offsets[hp++] = kp;  // a record starts: bases before it
+    }
+    const uint8_t c = R[i];
+    if (!hdr && c != '\n' && c != '\r') bases[kp++] = c;
+  }
+}
+
+// ---- FASTQ ------------------------------------------------------------------
+struct FqScratch {
+  unsigned long long *nl;    // [NB] newlines per block -> exclusive prefix
+  uint32_t *nlpos;           // [newlines] positions
+  uint32_t *seqlen;          // [records]
+  uint8_t *flag;             // [records] 0 ok, 1 bad, 2 blank header
+  unsigned long long *pos;   // [records] output offset of the sequence
+  unsigned long long out_base, rec_base, n_good;
+};
+
+__global__ __launch_bounds__(kIB) void k_fq_a(const uint8_t *__restrict__ R, uint64_t L,
+                                              FqScratch f) {
+  __shared__ unsigned long long s_n[kIB / 64];
+  const uint64_t b0 = (uint64_t)blockIdx.x * kIS + (uint64_t)threadIdx.x * kIPer;
+  unsigned long long n = 0;
+  for (int j = 0; j < kIPer; ++j)
+    if (b0 + j < L) n += R[b0 + j] == '\n';
+  unsigned long long tn;
+  block_scan_excl<unsigned long long>(n, 0ull, OpAdd(), s_n, &tn);
+  if (threadIdx.x == 0) f.nl[blockIdx.x] = tn;
+}
+
+__global__ __launch_bounds__(kScanT) void k_fq_b(uint64_t NB, FqScratch f,
+                                                 unsigned long long *total) {
+  __shared__ unsigned long long s_n[kScanT / 64];
+  unsigned long long tn;
+  scan_array_excl<unsigned long long>(f.nl, NB, 0ull, OpAdd(), s_n, &tn);
+  if (threadIdx.x == 0) *total = tn;
+}
+
+__global__ __launch_bounds__(kIB) void k_fq_c(const uint8_t *__restrict__ R, uint64_t L,
+                                              FqScratch f) {
+  __shared__ unsigned long long s_n[kIB / 64];
+  const uint64_t b0 = (uint64_t)blockIdx.x * kIS + (uint64_t)threadIdx.x * kIPer;
+  unsigned long long n = 0;
+  for (int j = 0; j < kIPer; ++j)
+    if (b0 + j < L) n += R[b0 + j] == '\n';
+  unsigned long long tn;
+  unsigned long long at = block_scan_excl<unsigned long long>(n, 0ull, OpAdd(), s_n, &tn);
+  at += f.nl[blockIdx.x];
+  for (int j = 0; j < kIPer; ++j)
+    if (b0 + j < L && R[b0 + j] == '\n') f.nlpos[at++] = (uint32_t)(b0 + j);
+}
+
+// line l of the chunk: [start, end) without its '\n'
+__device__ __forceinline__ void fq_line(const FqScratch &f, uint64_t l, uint64_t nl_total,
+                                        uint64_t L, uint64_t *s, uint64_t *e) {
+  *s = l == 0 ? 0 : (uint64_t)f.nlpos[l - 1] + 1;
+  *e = l < nl_total ? (uint64_t)f.nlpos[l] : L;
+}
+
+__global__ void k_fq_d(const uint8_t *__restrict__ R, uint64_t L, uint64_t n_rec,
+                       const unsigned long long *__restrict__ nl_total_p, FqScratch f) {
+  const uint64_t nl_total = *nl_total_p;
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_rec;
+       r += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t s[4], e[4];
+    for (int q = 0; q < 4; ++q) {
+      fq_line(f, 4 * r + q, nl_total, L, &s[q], &e[q]);
+      if (e[q] > s[q] && R[e[q] - 1] == '\r') --e[q];  // read_line strips one trailing '\r'
+    }
+    uint8_t fl = 0;
+    if (e[0] == s[0] || R[s[0]] == '\r') fl = 2;            // blank line: the host skips it
+    else if (R[s[0]] != '@') fl = 1;                       // not a header
+    else if (e[2] == s[2] || R[s[2]] != '+') fl = 1;       // '+' line missing or empty
+    else if (e[3] - s[3] != e[1] - s[1]) fl = 1;           // quality length != sequence
+    f.flag[r] = fl;
+    f.seqlen[r] = (uint32_t)(e[1] - s[1]);
+  }
+}
+
+__global__ __launch_bounds__(kScanT) void k_fq_e(uint64_t n_rec, bool eof, uint64_t L,
+                                                 const unsigned long long *__restrict__ nl_total_p,
+                                                 IngestState *__restrict__ st,
+                                                 FqScratch *__restrict__ fs,
+                                                 uint64_t *__restrict__ offsets) {
+  __shared__ unsigned long long s_w[kScanT / 64];
+  __shared__ unsigned long long s_first;
+  if (threadIdx.x == 0) s_first = n_rec;
+  __syncthreads();
+  const FqScratch f = *fs;
+  const uint64_t per = (n_rec + kScanT - 1) / kScanT;
+  const uint64_t lo = threadIdx.x * per, hi = lo + per < n_rec ? lo + per : n_rec;
+  for (uint64_t r = lo; r < hi; ++r)
+    if (f.flag[r]) {
+      atomicMin(&s_first, (unsigned long long)r);
+      break;
+    }
+  __syncthreads();
+  const uint64_t ng = s_first;
+  // exclusive scan of the sequence lengths of the good records
+  unsigned long long loc = 0;
+  for (uint64_t r = lo; r < hi && r < ng; ++r) loc += f.seqlen[r];
+  unsigned long long tot;
+  unsigned long long run = block_scan_excl<unsigned long long>(loc, 0ull, OpAdd(), s_w, &tot);
+  IngestState S = *st;
+  for (uint64_t r = lo; r < hi && r < ng; ++r) {
+    f.pos[r] = S.data_end + run;
+    offsets[S.n_rec + r] = S.data_end + run;
+    run += f.seqlen[r];
+  }
+  if (threadIdx.x != 0) return;
+  const uint64_t nl_total = *nl_total_p;
+  fs->out_base = S.data_end;
+  fs->rec_base = S.n_rec;
+  fs->n_good = ng;
+  if (ng < n_rec) {
+    if (f.flag[ng] == 2) S.blank = 1;  // fall back to the host reader
+    else S.stop = 1;                   // truncated stream: drop the rest
+  }
+  S.data_end += tot;
+  S.n_rec += ng;
+  // bytes used by the complete records (4 lines each, '\n'-terminated)
+  const uint64_t last_nl = 4 * ng;
+  S.consumed = ng == 0 ? 0 : (last_nl <= nl_total ? (uint64_t)f.nlpos[last_nl - 1] + 1 : L);
+  *st = S;
+  offsets[S.n_rec] = S.data_end;
+  (void)eof;
+}
+
+__global__ void k_fq_f(const uint8_t *__restrict__ R, uint64_t L,
+                       const unsigned long long *__restrict__ nl_total_p,
+                       const FqScratch *__restrict__ fs, uint8_t *__restrict__ bases) {
+  const FqScratch f = *fs;
+  const uint64_t nl_total = *nl_total_p;
+  const int lane = threadIdx.x & 63;
+  for (uint64_t r = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < f.n_good;
+       r += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
+    uint64_t s, e;
+    fq_line(f, 4 * r + 1, nl_total, L, &s, &e);
+    const uint32_t n = f.seqlen[r];
+    const uint64_t dst = f.pos[r];
+    for (uint32_t i = lane; i < n; i += 64) bases[dst + i] = R[s + i];
+  }
+}
+
+unsigned blocks_for(uint64_t L) { return (unsigned)((L + kIS - 1) / kIS); }
+
+}  // namespace
+
+size_t ingest_scratch_bytes(size_t chunk_cap) {
+  const size_t NB = (chunk_cap + kIS - 1) / kIS + 1;
+  const size_t fa = NB * (8 + 8 + 8) + sizeof(FaScratch);
+  const size_t recs = chunk_cap / 4 + 2;
+  const size_t fq = NB * 8 + (chunk_cap + 1) * 4 + recs * (4 + 1 + 8) + sizeof(FqScratch) + 64;
+  return (fa > fq ? fa : fq) + 1024;
+}
+
+// scratch layout: [struct][arrays...]
+hipError_t ingest_fasta(const uint8_t *raw, size_t len, bool eof, const IngestBufs &bufs,
+                        IngestState *st, hipStream_t s) {
+  (void)eof;
+  const uint64_t NB = blocks_for(len ? len : 1);
+  uint8_t *p = (uint8_t *)bufs.scratch;
+  FaScratch *fs = (FaScratch *)p;
+  p += 256;
+  FaScratch f{};
+  f.ls = (long long *)p;
+  p += NB * 8;
+  f.hdr = (unsigned long long *)p;
+  p += NB * 8;
+  f.keep = (unsigned long long *)p;
+  // the state the chunk starts from is needed by pass E after D updates it
+  IngestState *before = (IngestState *)(p + NB * 8);
+  hipError_t e = hipMemcpyAsync(fs, &f, sizeof f, hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) return e;
+  e = hipMemcpyAsync(before, st, sizeof(IngestState), hipMemcpyDeviceToDevice, s);
+  if (e != hipSuccess) return e;
+  if (!len) return hipSuccess;
+  hipLaunchKernelGGL(k_fa_a, dim3((unsigned)NB), dim3(kIB), 0, s, raw, (uint64_t)len, st, f);
+  hipLaunchKernelGGL(k_fa_b, dim3(1), dim3(kScanT), 0, s, NB, f);
+  hipLaunchKernelGGL(k_fa_c, dim3((unsigned)NB), dim3(kIB), 0, s, raw, (uint64_t)len, st, f);
+  hipLaunchKernelGGL(k_fa_d, dim3(1), dim3(kScanT), 0, s, raw, (uint64_t)len, NB, st, fs,
+                     bufs.offsets);
+  hipLaunchKernelGGL(k_fa_e, dim3((unsigned)NB), dim3(kIB), 0, s, raw, (uint64_t)len, before, fs,
+                     f, bufs.bases, bufs.offsets);
+  return hipGetLastError();
+}
+
+hipError_t ingest_fastq(const uint8_t *raw, size_t len, bool eof, const IngestBufs &bufs,
+                        IngestState *st, hipStream_t s) {
+  const uint64_t NB = blocks_for(len ? len : 1);
+  uint8_t *p = (uint8_t *)bufs.scratch;
+  FqScratch *fs = (FqScratch *)p;
+  p += 256;
+  unsigned long long *nl_total = (unsigned long long *)p;
+  p += 64;
+  FqScratch f{};
+  f.nl = (unsigned long long *)p;
+  p += NB * 8;
+  f.nlpos = (uint32_t *)p;
+  p += (len + 1) * 4;
+  p = (uint8_t *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
+  const uint64_t max_rec = len / 4 + 2;
+  f.pos = (unsigned long long *)p;
+  p += max_rec * 8;
+  f.seqlen = (uint32_t *)p;
+  p += max_rec * 4;
+  f.flag = (uint8_t *)p;
+  hipError_t e = hipMemcpyAsync(fs, &f, sizeof f, hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) return e;
+  // newline count first: the number of candidate records follows from it
+  hipLaunchKernelGGL(k_fq_a, dim3((unsigned)NB), dim3(kIB), 0, s, raw, (uint64_t)len, f);
+  hipLaunchKernelGGL(k_fq_b, dim3(1), dim3(kScanT), 0, s, NB, f, nl_total);
+  unsigned long long nl = 0;
+  e = hipMemcpyAsync(&nl, nl_total, 8, hipMemcpyDeviceToHost, s);
+  if (e != hipSuccess) return e;
+  e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return e;
+  // lines: '\n'-terminated ones, plus an unterminated last line at the end of input
+  uint64_t lines = nl;
+  if (eof && len) {
+    uint8_t last = 0;
+    e = hipMemcpy(&last, raw + len - 1, 1, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return e;
+    if (last != '\n') ++lines;
+  }
+  const uint64_t n_rec = lines / 4;  // complete 4-line records
+  hipLaunchKernelGGL(k_fq_c, dim3((unsigned)NB), dim3(kIB), 0, s, raw, (uint64_t)len, f);
+  if (n_rec) {
+    const unsigned g = (unsigned)((n_rec + 255) / 256 < 65535 ? (n_rec + 255) / 256 : 65535);
+    hipLaunchKernelGGL(k_fq_d, dim3(g), dim3(256), 0, s, raw, (uint64_t)len, n_rec, nl_total, f);
+  }
+  hipLaunchKernelGGL(k_fq_e, dim3(1), dim3(kScanT), 0, s, n_rec, eof, (uint64_t)len, nl_total,
+                     st, fs, bufs.offsets);
+  if (n_rec) {
+    const uint64_t waves = n_rec < 65536 ? n_rec : 65536;
+    hipLaunchKernelGGL(k_fq_f, dim3((unsigned)((waves * 64 + 255) / 256)), dim3(256), 0, s, raw,
+                       (uint64_t)len, nl_total, fs, bufs.bases);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace nk

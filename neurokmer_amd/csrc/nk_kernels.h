@@ -95,8 +95,13 @@ struct KmerInput {
   const uint64_t *offsets;
   uint64_t n_recs;
   uint64_t n_bases;
-  const uint32_t *tile_rec;  // first record of every tile
-  uint64_t n_tiles;
+  const uint32_t *tile_rec;  // first record of each launched tile (index: tile - tile_base)
+  uint64_t n_tiles;          // tiles launched
+  // chunked input (streaming ingest): the launch covers tiles tile_base ..
+  // tile_base + n_tiles - 1 and counts only windows starting in [pos_lo, pos_hi)
+  uint64_t tile_base = 0;
+  uint64_t pos_lo = 0;
+  uint64_t pos_hi = ~0ull;
 };
 
 struct PartArgs {

@@ -37,10 +37,11 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 // first record of each tile: largest r < n_recs with offsets[r] <= tile start
 // ---------------------------------------------------------------------------
 __global__ void k_tile_rec(const uint64_t *__restrict__ offsets, uint64_t n_recs,
-                           uint64_t n_tiles, uint64_t tile_size, uint32_t *__restrict__ tile_rec) {
+                           uint64_t n_tiles, uint64_t tile_size, uint64_t tile_base,
+                           uint32_t *__restrict__ tile_rec) {
   uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_tiles) return;
-  uint64_t pos = t * tile_size;
+  uint64_t pos = (tile_base + t) * tile_size;
   uint64_t lo = 0, hi = n_recs;  // invariant: offsets[lo] <= pos, answer in [lo, hi)
   while (hi - lo > 1) {
     uint64_t mid = (lo + hi) >> 1;
@@ -144,13 +145,14 @@ __global__ __launch_bounds__(kBlock) void k_kmers(KmerInput in, int k, FastMod f
     seen_init(seen);
     build_top_tbl(u, tbl_idx, tbl_slot);  // contains __syncthreads
   }
-  const uint64_t T0 = (uint64_t)blockIdx.x * kTile;
-  stage_tile<kTile, kBlock, !CANON>(L, in, blockIdx.x, k);
+  const uint64_t tile = in.tile_base + blockIdx.x;
+  const uint64_t T0 = tile * kTile;
+  stage_tile<kTile, kBlock, !CANON>(L, in, tile, k);
 #pragma unroll 4
   for (int j = 0; j < kPerThread; ++j) {
     const int q = j * kBlock + threadIdx.x;
     if (T0 + (uint64_t)q + (uint64_t)k > in.n_bases) break;
-    if (!window_valid(L, T0, q, k, in.n_bases)) continue;
+    if (!window_valid(L, T0, q, k, in.n_bases, in.pos_lo, in.pos_hi)) continue;
     const uint64_t key = window_key<kTile, !CANON, CANON>(L, q, k);
     const uint64_t idx = fastmod(sip13_u64(key), fm);
     if (MODE == 0) {
@@ -182,11 +184,12 @@ __global__ __launch_bounds__(kBlock) void k_kmers_compat(KmerInput in, int k, Fa
     build_top_tbl(u, tbl_idx, tbl_slot);
   }
 
-  const uint64_t T0 = (uint64_t)blockIdx.x * kTile;
+  const uint64_t T0 = (in.tile_base + blockIdx.x) * kTile;
   uint64_t r = in.tile_rec[blockIdx.x];
   for (int j = 0; j < kPerThread; ++j) {
     const uint64_t p = T0 + (uint64_t)j * kBlock + threadIdx.x;
     if (p >= in.n_bases) break;
+    if (p < in.pos_lo || p >= in.pos_hi) continue;
     while (r + 1 < in.n_recs && in.offsets[r + 1] <= p) ++r;
     const uint64_t s0 = in.offsets[r], e0 = in.offsets[r + 1];
     if (p < s0 || p + (uint64_t)k > e0) continue;
@@ -268,13 +271,14 @@ __global__ __launch_bounds__(kBlock) void k_kmers128(KmerInput in, int k, FastMo
   uint64_t *tbl_idx = dyn;
   uint32_t *tbl_slot = reinterpret_cast<uint32_t *>(dyn + (MODE == 1 ? u.tbl_size : 0));
   if (MODE == 1) build_top_tbl(u, tbl_idx, tbl_slot);  // contains __syncthreads
-  const uint64_t T0 = (uint64_t)blockIdx.x * kTile;
-  stage_tile<kTile, kBlock, !CANON>(L, in, blockIdx.x, k);
+  const uint64_t tile = in.tile_base + blockIdx.x;
+  const uint64_t T0 = tile * kTile;
+  stage_tile<kTile, kBlock, !CANON>(L, in, tile, k);
 #pragma unroll 2
   for (int j = 0; j < kPerThread; ++j) {
     const int q = j * kBlock + threadIdx.x;
     if (T0 + (uint64_t)q + (uint64_t)k > in.n_bases) break;
-    if (!window_valid(L, T0, q, k, in.n_bases)) continue;
+    if (!window_valid(L, T0, q, k, in.n_bases, in.pos_lo, in.pos_hi)) continue;
     const Key128 key = window_key128<kTile, !CANON, CANON>(L, q, k);
     const uint64_t idx = fastmod(sip13_u128(key.lo, key.hi), fm);
     if (MODE == 0) {
@@ -358,7 +362,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
   __shared__ uint8_t s_gmap[kGroups];  // store group -> bucket
 
   const int tid = threadIdx.x;
-  const uint64_t tile = blockIdx.x;
+  const uint64_t tile = in.tile_base + blockIdx.x;
   const uint64_t T0 = tile * (uint64_t)kPartTile;
   const uint32_t B = pa.n_buckets;
   for (uint32_t b = tid; b <= B; b += kPartBlock) s_cnt[b] = 0;
@@ -375,6 +379,12 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
   uint32_t ok = ~(L.WIN[q0 >> 5] >> (q0 & 31)) & 0xFFFFu;
   if (nrange < (uint64_t)q0 + kPartPerThread)
     ok &= nrange > (uint64_t)q0 ? (1u << (uint32_t)(nrange - q0)) - 1u : 0u;
+  {  // chunked input: only windows starting in [pos_lo, pos_hi) (uniform per launch)
+    const uint64_t p0 = T0 + (uint64_t)q0;
+    if (in.pos_lo > p0) ok &= in.pos_lo - p0 >= 16 ? 0u : ~((1u << (uint32_t)(in.pos_lo - p0)) - 1u);
+    if (in.pos_hi < p0 + kPartPerThread)
+      ok &= in.pos_hi > p0 ? (1u << (uint32_t)(in.pos_hi - p0)) - 1u : 0u;
+  }
   const int twok = 2 * k;
   const uint64_t mask2k = (k >= 32) ? ~0ULL : ((1ULL << twok) - 1ULL);
   uint64_t fwd, rev;
@@ -456,9 +466,12 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
       unsigned long long ret = atomicAdd(&pa.fill[b], (unsigned long long)c | (1ull << 40));
       uint64_t eb = ret & ((1ull << 40) - 1);
       uint64_t seg = ret >> 40;
-      pa.desc[(uint64_t)b * pa.max_segs + seg] = make_uint2((uint32_t)tile, (uint32_t)eb);
+      if (seg < pa.max_segs)
+        pa.desc[(uint64_t)b * pa.max_segs + seg] = make_uint2((uint32_t)tile, (uint32_t)eb);
       fit = eb >= pa.cap ? 0u : (uint32_t)(pa.cap - eb < c ? pa.cap - eb : c);
-      if (fit < c) pa.overflow[b] = 1u;
+      // past the region, or past the descriptor table (chunked input: a tile can
+      // add a segment per launch): the uniques of this bucket fall back to a rescan
+      if (fit < c || seg >= pa.max_segs) pa.overflow[b] = 1u;
       base = (uint32_t)eb;
     }
     s_base[b] = base;
@@ -1498,7 +1511,7 @@ hipError_t launch_tile_rec(const KmerInput &in, uint64_t tile_size, uint32_t *ti
   if (!in.n_tiles) return hipSuccess;
   unsigned g = (unsigned)((in.n_tiles + 255) / 256);
   hipLaunchKernelGGL(k_tile_rec, dim3(g), dim3(256), 0, s, in.offsets, in.n_recs, in.n_tiles,
-                     tile_size, tile_rec);
+                     tile_size, in.tile_base, tile_rec);
   return hipGetLastError();
 }
 
@@ -1761,12 +1774,12 @@ __global__ void k_zero(ZeroList z) {
 
 // tile -> first record (blocks [0, tr_blocks)) + the zero list (the rest)
 __global__ void k_prep(const uint64_t *__restrict__ offsets, uint64_t n_recs, uint64_t n_tiles,
-                       uint64_t tile_size, uint32_t *__restrict__ tile_rec, unsigned tr_blocks,
-                       ZeroList z) {
+                       uint64_t tile_size, uint64_t tile_base, uint32_t *__restrict__ tile_rec,
+                       unsigned tr_blocks, ZeroList z) {
   if (blockIdx.x < tr_blocks) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n_tiles) return;
-    const uint64_t pos = t * tile_size;
+    const uint64_t pos = (tile_base + t) * tile_size;
     uint64_t lo = 0, hi = n_recs;
     while (hi - lo > 1) {
       const uint64_t mid = (lo + hi) >> 1;
@@ -1796,7 +1809,7 @@ hipError_t launch_prep(const KmerInput &in, uint64_t tile_size, uint32_t *tile_r
   if (g > 1024) g = 1024;
   if (!g) g = 1;
   hipLaunchKernelGGL(k_prep, dim3(tr + g), dim3(256), 0, s, in.offsets, in.n_recs, in.n_tiles,
-                     tile_size, tile_rec, tr, z);
+                     tile_size, in.tile_base, tile_rec, tr, z);
   return hipGetLastError();
 }
 

@@ -112,7 +112,7 @@ __device__ __forceinline__ void stage_tile(TileLds<TILE, RAW> &L, const KmerInpu
   __syncthreads();
   // windows crossing a record end (or running past the input) are not k-mers
   const uint64_t limit = T0 + TILE + (uint64_t)k - 1;
-  const uint64_t r0 = in.tile_rec[tile];
+  const uint64_t r0 = in.tile_rec[tile - in.tile_base];
   for (uint64_t r = r0 + 1 + tid; r <= in.n_recs; r += BLOCK) {
     uint64_t b = in.offsets[r];
     if (b >= limit) break;
@@ -134,8 +134,11 @@ __device__ __forceinline__ void stage_tile(TileLds<TILE, RAW> &L, const KmerInpu
 // true if local position q starts a k-mer of some record
 template <int TILE, bool RAW>
 __device__ __forceinline__ bool window_valid(const TileLds<TILE, RAW> &L, uint64_t T0, int q,
-                                             int k, uint64_t n_bases) {
-  return T0 + (uint64_t)q + (uint64_t)k <= n_bases && !((L.WIN[q >> 5] >> (q & 31)) & 1u);
+                                             int k, uint64_t n_bases, uint64_t pos_lo = 0,
+                                             uint64_t pos_hi = ~0ull) {
+  const uint64_t p = T0 + (uint64_t)q;
+  return p + (uint64_t)k <= n_bases && p >= pos_lo && p < pos_hi &&
+         !((L.WIN[q >> 5] >> (q & 31)) & 1u);
 }
 
 // The reference's key for the window at local position q (k <= 32):

@@ -493,3 +493,101 @@ def test_process_sequence_matches_reference(canon):
         keys2.update(int(x) for x in cbind.kmer_keys(rd, k, canon))
     assert_same(g, r2)
     assert_exact_same(g, r2, keys2, pool)
+
+
+# ---- GPU FASTX ingest: chunked device parse ---------------
+from neurokmer_amd.fastx import stream_sequences  # noqa: E402
+
+
+def _ingest_check(path, k, pool, canon, streaming, chunk, exact=False):
+    old = os.environ.get("NK_INGEST_CHUNK")
+    os.environ["NK_INGEST_CHUNK"] = str(chunk)
+    try:
+        g = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, canon, exact_counts=exact)
+        (g.process_file_streaming if streaming else g.process_file_parallel)(path)
+    finally:
+        if old is None:
+            os.environ.pop("NK_INGEST_CHUNK", None)
+        else:
+            os.environ["NK_INGEST_CHUNK"] = old
+    recs = list(stream_sequences(path))  # the host reader's records (mirror)
+    r = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, canon)
+    (r.process_streaming if streaming else r.process_parallel)(recs)
+    assert_same(g, r)
+    if exact:
+        np.testing.assert_array_equal(g.kmer_per_neuron(), r.kmer_per_neuron())
+        assert g.distinct_kmers() == r.distinct_kmers()
+    return recs
+
+
+def _crlf(data: bytes) -> bytes:
+    return data.replace(b"\n", b"\r\n")
+
+
+@pytest.mark.parametrize("k,canon", [(5, True), (31, True), (31, False), (33, True), (63, False)])
+@pytest.mark.parametrize("chunk", [4099, 65536, 1 << 26])
+def test_ingest_fasta_chunks(tmp_path, k, canon, chunk):
+    bases, offs = synth.make_records(120_000, 9, seed=k + chunk % 97, n_rate=0.01, mixed_case=True,
+                                     repeats_per_mb=20_000, motif_len=60)
+    p = tmp_path / "a.fa"
+    synth.write_fasta(str(p), bases, offs, width=61)
+    data = p.read_bytes()
+    # an empty record and a record whose single line spans several chunks
+    data = data.replace(b">s3\n", b">empty\n>s3\n", 1) + b">long\n" + b"ACGTTGCA" * 3000 + b"\n"
+    p.write_bytes(_crlf(data) if k == 31 else data)
+    recs = _ingest_check(str(p), k, 7001, canon, (k + chunk) % 2 == 1, chunk)
+    assert len(recs) == 11
+
+
+@pytest.mark.parametrize("chunk", [1000, 30000, 1 << 26])
+@pytest.mark.parametrize("streaming", [True, False])
+def test_ingest_fastq_chunks(tmp_path, chunk, streaming):
+    reads, roffs = synth.make_reads(400, 150, seed=5, n_rate=0.005, repeats_per_mb=40_000,
+                                    motif_len=50)
+    longr, loffs = synth.make_reads(3, 2500, seed=6)  # records longer than a chunk
+    p = tmp_path / "r.fq"
+    synth.write_fastq(str(p), np.concatenate([reads, longr]),
+                      np.concatenate([roffs, loffs[1:] + roffs[-1]]).astype(np.uint64))
+    data = p.read_bytes()
+    p.write_bytes(_crlf(data) if chunk == 30000 else data.rstrip(b"\n"))  # CRLF / no final '\n'
+    recs = _ingest_check(str(p), 21, 5003, True, streaming, chunk, exact=chunk == 1000)
+    assert len(recs) == 403
+
+
+def test_ingest_fastq_stops_at_malformed_record(tmp_path):
+    reads, roffs = synth.make_reads(300, 120, seed=7)
+    p = tmp_path / "bad.fq"
+    synth.write_fastq(str(p), reads, roffs)
+    lines = p.read_bytes().split(b"\n")
+    lines[4 * 150 + 3] = lines[4 * 150 + 3][:-1]  # record 150: quality one byte short
+    p.write_bytes(b"\n".join(lines))
+    recs = _ingest_check(str(p), 19, 3001, True, True, 2000)
+    assert len(recs) == 150
+
+
+def test_ingest_fastq_blank_lines_use_host_reader(tmp_path):
+    reads, roffs = synth.make_reads(200, 100, seed=8)
+    p = tmp_path / "blank.fq"
+    synth.write_fastq(str(p), reads, roffs)
+    lines = p.read_bytes().split(b"\n")
+    lines.insert(4 * 77, b"")  # a blank line between records: skipped by the reader
+    p.write_bytes(b"\n".join(lines))
+    recs = _ingest_check(str(p), 17, 2003, True, False, 3000)
+    assert len(recs) == 200
+
+
+def test_ingest_gzip(tmp_path):
+    import gzip
+    bases, offs = synth.make_records(200_000, 5, seed=12, n_rate=0.002, repeats_per_mb=10_000,
+                                     motif_len=80)
+    p = tmp_path / "g.fa.gz"
+    raw = tmp_path / "g.fa"
+    synth.write_fasta(str(raw), bases, offs, width=70)
+    p.write_bytes(gzip.compress(raw.read_bytes()))
+    _ingest_check(str(p), 27, 9001, True, False, 50_000)
+    q = tmp_path / "g.fq.gz"
+    rq = tmp_path / "g.fq"
+    reads, roffs = synth.make_reads(500, 130, seed=13)
+    synth.write_fastq(str(rq), reads, roffs)
+    q.write_bytes(gzip.compress(rq.read_bytes()))
+    _ingest_check(str(q), 23, 4001, False, True, 20_000)
