@@ -11,6 +11,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <future>
 #include <string>
 #include <vector>
 
@@ -18,6 +19,7 @@
 #include "nk_exact.h"
 #include "nk_fastx.h"
 #include "nk_ingest.h"
+#include "nk_reader.h"
 #include "nk_kernels.h"
 
 using namespace nk;
@@ -1102,53 +1104,54 @@ static size_t ingest_chunk_bytes() {
 // FASTQ records).
 static int ingest_file(nk_counter *c, const char *path, bool *fallback) {
   *fallback = false;
-  gzFile f = gzopen(path, "rb");
-  if (!f) return fail(NK_E_IO, "cannot open %s", path);
-  gzbuffer(f, 1 << 20);
-  struct FileCloser {
-    gzFile f;
-    ~FileCloser() { gzclose(f); }
-  } closer{f};
-  uint64_t fsize = 0;
-  bool gz = false;
-  {
-    FILE *raw = fopen(path, "rb");
-    if (raw) {
-      unsigned char m[2] = {0, 0};
-      gz = fread(m, 1, 2, raw) == 2 && m[0] == 0x1f && m[1] == 0x8b;
-      fseeko(raw, 0, SEEK_END);
-      fsize = (uint64_t)ftello(raw);
-      fclose(raw);
-    }
-  }
+  ChunkSource src;
+  std::string err;
+  int rc = src.open(path, err);
+  if (rc) return fail(rc, "%s", err.c_str());
   (void)hipSetDevice(c->device);
   hipStream_t s = c->own_stream;
-  int rc;
+  // two pinned host buffers: [room for a FASTQ carry | chunk]; the reader
+  // thread fills one while the device copies and parses the other
   size_t chunk = ingest_chunk_bytes();
-  std::vector<uint8_t> hb;  // carry + chunk (host)
-  hb.resize(chunk);
-  size_t have = 0;
-  auto read_more = [&](size_t want) -> size_t {
-    if (hb.size() < have + want) hb.resize(have + want);
-    size_t got = 0;
-    while (got < want) {
-      const int n = gzread(f, hb.data() + have + got, (unsigned)std::min<size_t>(want - got, 1u << 30));
-      if (n <= 0) break;
-      got += (size_t)n;
+  size_t room = std::max<size_t>(chunk / 8, 1 << 16);
+  struct Pinned {
+    uint8_t *p = nullptr;
+    size_t n = 0;
+    ~Pinned() {
+      if (p) (void)hipHostFree(p);
     }
-    have += got;
-    return got;
-  };
-  bool eof = read_more(chunk) < chunk;
+    int ensure(size_t want) {
+      if (want <= n) return NK_OK;
+      if (p) (void)hipHostFree(p);
+      p = nullptr;
+      n = 0;
+      if (hipHostMalloc((void **)&p, want) != hipSuccess) {
+        p = nullptr;
+        return fail(NK_E_OOM, "hipHostMalloc of %zu bytes failed", want);
+      }
+      n = want;
+      return NK_OK;
+    }
+  } hb[2];
+  if ((rc = hb[0].ensure(room + chunk)) || (rc = hb[1].ensure(room + chunk))) return rc;
+  int cur = 0;
+  size_t start = room, have = src.read(hb[0].p + room, chunk);
+  bool eof = have < chunk;
   if (!have) return fail(NK_E_PARSE, "empty file");
-  const bool fastq = hb[0] == '@';
-  if (hb[0] != '>' && !fastq)
+  const bool fastq = hb[0].p[room] == '@';
+  if (hb[0].p[room] != '>' && !fastq)
     return fail(NK_E_PARSE, "unknown format: first byte is neither '>' nor '@'");
+  std::future<size_t> next;
+  auto prefetch = [&](int b) {
+    next = std::async(std::launch::async, [&src, &hb, b, room, chunk] {
+      return src.read(hb[b].p + room, chunk);
+    });
+  };
+  if (!eof) prefetch(1);
   // resident input: the file size bounds the bases of a plain file
-  uint64_t cap_bases = (gz ? 4 * fsize : fsize) + 64;
-  uint64_t cap_recs = 1024;
-  if ((rc = c->in_bases.ensure(cap_bases + 16)) || (rc = c->in_offs.ensure(cap_recs + 1)))
-    return rc;
+  const uint64_t fsize = src.file_size();
+  uint64_t cap_bases = (src.gz() ? 4 * fsize : fsize) + 64;
+  if ((rc = c->in_bases.ensure(cap_bases + 16)) || (rc = c->in_offs.ensure(1025))) return rc;
   DevBuf<uint8_t> draw, scratch;
   DevBuf<IngestState> dst;
   if ((rc = draw.ensure(chunk)) || (rc = scratch.ensure(ingest_scratch_bytes(chunk))) ||
@@ -1161,6 +1164,7 @@ static int ingest_file(nk_counter *c, const char *path, bool *fallback) {
   if ((rc = acc_begin(c, fastq ? cap_bases / 2 : cap_bases, sa, s))) return rc;
   uint64_t counted = 0;  // windows below this start were counted
   for (;;) {
+    const uint8_t *data = hb[cur].p + start;
     const size_t len = have;
     // capacity of the resident buffers for this chunk (grow: wait, copy, free)
     const uint64_t need_b = st.data_end + len + 64, need_r = st.n_rec + len / 2 + 4;
@@ -1187,13 +1191,14 @@ static int ingest_file(nk_counter *c, const char *path, bool *fallback) {
       HIPCHK(hipStreamSynchronize(s));
       if ((rc = draw.ensure(len)) || (rc = scratch.ensure(ingest_scratch_bytes(len)))) return rc;
     }
-    HIPCHK(hipMemcpyAsync(draw.p, hb.data(), len, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(draw.p, data, len, hipMemcpyHostToDevice, s));
     IngestBufs ib{c->in_bases.p, c->in_offs.p, c->in_bases.n, c->in_offs.n - 1, scratch.p};
     HIPCHK(fastq ? ingest_fastq(draw.p, len, eof, ib, dst.p, s)
                  : ingest_fasta(draw.p, len, eof, ib, dst.p, s));
     HIPCHK(hipMemcpyAsync(&st, dst.p, sizeof st, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     if (fastq && st.blank) {
+      if (next.valid()) next.get();
       *fallback = true;
       return NK_OK;
     }
@@ -1212,19 +1217,34 @@ static int ingest_file(nk_counter *c, const char *path, bool *fallback) {
       counted = hi;
     }
     if (last) {
+      if (next.valid()) next.get();
       if ((rc = acc_end(c, sa, whole, s))) return rc;
       break;
     }
-    // next chunk: FASTQ carries its unfinished record's bytes
-    size_t keep = 0;
-    if (fastq) {
-      keep = len - (size_t)st.consumed;
-      if (st.consumed == 0 && keep >= hb.size() / 2) chunk *= 2;  // a record longer than the chunk
-      memmove(hb.data(), hb.data() + st.consumed, keep);
+    // next chunk: the prefetched bytes, behind this chunk's FASTQ carry
+    const int nxt = cur ^ 1;
+    const size_t got = next.get();
+    const size_t carry = fastq ? len - (size_t)st.consumed : 0;
+    size_t nstart = room;
+    if (carry) {
+      if (carry <= room) {
+        nstart = room - carry;
+        memcpy(hb[nxt].p + nstart, data + st.consumed, carry);
+      } else {  // a record longer than the carry room: grow both buffers
+        std::vector<uint8_t> cv(data + st.consumed, data + len);
+        std::vector<uint8_t> tmp(hb[nxt].p + room, hb[nxt].p + room + got);
+        room = carry;
+        if ((rc = hb[nxt].ensure(room + chunk)) || (rc = hb[cur].ensure(room + chunk))) return rc;
+        memcpy(hb[nxt].p, cv.data(), carry);
+        memcpy(hb[nxt].p + room, tmp.data(), got);
+        nstart = 0;
+      }
     }
-    have = keep;
-    const size_t want = chunk > keep ? chunk - keep : chunk;
-    eof = read_more(want) < want;
+    eof = got < chunk;
+    cur = nxt;
+    start = nstart;
+    have = carry + got;
+    if (!eof) prefetch(cur ^ 1);
   }
   return NK_OK;
 }
