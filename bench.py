@@ -61,7 +61,8 @@ def load_pmc_traffic():
         return None, None
 
 
-def cpu_baseline(bases: np.ndarray, offsets: np.ndarray, per_record: int = 2_000_000):
+def cpu_baseline(bases: np.ndarray, offsets: np.ndarray, per_record: int = 2_000_000,
+                 pool: int = POOL):
     """The C restatement of process_parallel (oracle/nk_oracle.c, 'port') on a
     bounded sample of the same workload: the first `per_record` bases of each
     of the 7 records, parallel over records like rayon (src/spiking_hash.rs:
@@ -74,7 +75,7 @@ def cpu_baseline(bases: np.ndarray, offsets: np.ndarray, per_record: int = 2_000
     np.cumsum([x.size for x in segs], out=offs[1:])
     b = np.concatenate(segs)
     threads = offsets.size - 1  # one rayon work unit per record
-    ref = cbind.OracleCounter(K, 1.0, 0.95, 2, 1.0, POOL, True)
+    ref = cbind.OracleCounter(K, 1.0, 0.95, 2, 1.0, pool, True)
     t0 = time.perf_counter()
     ref.process_parallel_arrays(b, offs, threads)
     dt = time.perf_counter() - t0
@@ -90,10 +91,13 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--bases", type=int, default=BASES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    # side measurements only (the metric is pool 2M): e.g. config 3's 16 M pool
+    ap.add_argument("--pool", type=int, default=POOL)
     # test-only: rehearse the multi-rank path on a 1-GPU box (gloo, all ranks on cuda:0)
     ap.add_argument("--dist-backend", default="nccl")
     ap.add_argument("--same-device", action="store_true")
     args = ap.parse_args()
+    pool = args.pool
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -119,8 +123,8 @@ def main() -> int:
     d_offs = torch.from_numpy(offsets.view(np.int64)).to(dev)
     torch.cuda.synchronize()
 
-    ctr = SpikingKmerCounter(K, 1.0, 0.95, 2, 1.0, POOL, True, device=local)
-    cur_t = torch.as_tensor(_CAI(ctr.device_currents_ptr(), POOL), device=dev)
+    ctr = SpikingKmerCounter(K, 1.0, 0.95, 2, 1.0, pool, True, device=local)
+    cur_t = torch.as_tensor(_CAI(ctr.device_currents_ptr(), pool), device=dev)
 
     def step():
         s = torch.cuda.current_stream().cuda_stream
@@ -178,12 +182,12 @@ def main() -> int:
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
             "data": "synthetic (splitmix64 i.i.d. ACGT, seed 0x4E4B4D52^rank, 64x200-bp planted "
                     "repeats per MB)",
-            "config": {"workload": "config 2: 115,000,000 bases in 7 records per GPU, k=31, "
-                                   "pool_size=2,000,000, --canonical, process_parallel",
-                       "k": K, "pool_size": POOL, "bases_per_gpu": int(bases.size),
+            "config": {"workload": (f"config 2: {bases.size:,} bases in 7 records per GPU, k=31, "
+                                    f"pool_size={pool:,}, --canonical, process_parallel"),
+                       "k": K, "pool_size": pool, "bases_per_gpu": int(bases.size),
                        "records_per_gpu": RECS, "kmers_per_gpu": nk,
                        "parallelism": f"dp{world}"},
-            "roofline": {"bound": "hbm", "kernel": "k_kmers<canonical,count>",
+            "roofline": {"bound": "hbm", "kernel": "k_part<canonical> (K1a)",
                          "achieved": round(achieved / 1e9, 2), "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
@@ -192,10 +196,10 @@ def main() -> int:
             "total_spikes": total_spikes,
         }
         if world == 1 and not args.no_cpu_baseline:
-            cb = cpu_baseline(bases, offsets)
+            cb = cpu_baseline(bases, offsets, pool=pool)
             # parity on the same sample: GPU vs the restatement, bit-exact
             sb, so = cb["sample"]
-            g = SpikingKmerCounter(K, 1.0, 0.95, 2, 1.0, POOL, True, device=local)
+            g = SpikingKmerCounter(K, 1.0, 0.95, 2, 1.0, pool, True, device=local)
             g.process_parallel_arrays(sb, so)
             ref = cb["ref"]
             parity = {
@@ -213,9 +217,9 @@ def main() -> int:
                 "kind": "port",
                 "sample": f"first {cb['per_record']} bases of each of the {RECS} records of "
                           f"rank 0's workload ({cb['bases']} bases, {cb['kmers']} k-mers, "
-                          f"pool 2M, k=31, canonical) in {cb['seconds']:.2f} s: oracle/nk_oracle.c "
+                          f"pool {pool:,}, k=31, canonical) in {cb['seconds']:.2f} s: oracle/nk_oracle.c "
                           f"process_parallel restatement (parallel over records, exact k-mer "
-                          f"map, serial merge and 2M x 1000-step LIF)"}
+                          f"map, serial merge and 1000-step LIF)"}
             out["parity_on_cpu_sample"] = parity
         print(json.dumps(out), flush=True)
     ctr.close()

@@ -15,7 +15,7 @@ constexpr int kPartTile = 8192;       // positions per K1a workgroup
 constexpr int kPartBlock = 512;       // threads per K1a workgroup
 constexpr int kBinBits = 15;
 constexpr int kBinsPerBucket = 1 << kBinBits;  // 32768 u32 bins = 128 KiB LDS
-constexpr int kMaxBuckets = 256;      // pool <= 8,388,608 takes the partitioned path
+constexpr int kMaxBuckets = 512;      // pool <= 16,777,216 takes the partitioned path
 constexpr int kHistBlock = 1024;
 
 struct LifParams {

@@ -17,6 +17,7 @@
 //   K4 k_topn_*     exact top-N by (spikes desc, index asc).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 #include "nk_device.h"
 #include "nk_kernels.h"
@@ -328,7 +329,7 @@ __global__ void k_set_merge128(const uint64_t *__restrict__ keys, uint64_t n, Fa
 }
 
 // ---------------------------------------------------------------------------
-// K1 partitioned (k <= 32, pool <= 256 * 32768): the MI355X-native count.
+// K1 partitioned (k <= 32, pool <= kMaxBuckets * 32768): the MI355X-native count.
 //
 // Random per-k-mer global atomics run at the memory side (~20 G/s chip-wide),
 // 10x below what the hash rate allows.  Instead:
@@ -347,19 +348,29 @@ __global__ void k_set_merge128(const uint64_t *__restrict__ keys, uint64_t n, Fa
 // ---------------------------------------------------------------------------
 constexpr int kPartPerThread = kPartTile / kPartBlock;  // 16
 constexpr uint32_t kPadOff = 0xFFFFu;                    // sentinel bin of a pad record
-constexpr int kSortSlots = kPartTile + 7 * kMaxBuckets;  // records + worst-case padding
-constexpr int kGroups = kSortSlots / 8;                  // 8-record store groups
-constexpr int kGroupIters = (kGroups + kPartBlock - 1) / kPartBlock;
+// MAXB: bucket capacity of the launch (256 for pools <= 8.4 M, 512 up to
+// 16.7 M); the LDS sort area holds the tile plus the worst-case padding
+template <int MAXB>
+struct PartShape {
+  static constexpr int kSortSlots = kPartTile + 7 * MAXB;  // records + worst-case padding
+  static constexpr int kGroups = kSortSlots / 8;           // 8-record store groups
+  static constexpr int kGroupIters = (kGroups + kPartBlock - 1) / kPartBlock;
+  using GMap = typename std::conditional<(MAXB > 256), uint16_t, uint8_t>::type;
+};
 
-template <bool CANON>
+template <bool CANON, int MAXB>
 __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMod fm, PartArgs pa) {
+  using S = PartShape<MAXB>;
+  constexpr int kSortSlots = S::kSortSlots;
+  constexpr int kGroups = S::kGroups;
+  constexpr int kGroupIters = S::kGroupIters;
   __shared__ TileLds<kPartTile, !CANON> L;
-  __shared__ uint32_t s_cnt[kMaxBuckets + 1];  // + a dummy bucket for non-k-mer positions
-  __shared__ uint32_t s_start[kMaxBuckets + 1];
-  __shared__ uint32_t s_base[kMaxBuckets];
-  __shared__ uint32_t s_fit[kMaxBuckets];
+  __shared__ uint32_t s_cnt[MAXB + 1];  // + a dummy bucket for non-k-mer positions
+  __shared__ uint32_t s_start[MAXB + 1];
+  __shared__ uint32_t s_base[MAXB];
+  __shared__ uint32_t s_fit[MAXB];
   __shared__ __align__(16) uint32_t s_sorted[kSortSlots];
-  __shared__ uint8_t s_gmap[kGroups];  // store group -> bucket
+  __shared__ typename S::GMap s_gmap[kGroups];  // store group -> bucket
 
   const int tid = threadIdx.x;
   const uint64_t tile = in.tile_base + blockIdx.x;
@@ -492,7 +503,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
   for (uint32_t b = tid; b < B; b += kPartBlock) {
     const uint32_t c = s_cnt[b], st = s_start[b], cp = (c + 7u) & ~7u;
     for (uint32_t i = c; i < cp; ++i) s_sorted[st + i] = 0xFFFFFFFFu;
-    for (uint32_t g = st >> 3; g < (st + cp) >> 3; ++g) s_gmap[g] = (uint8_t)b;
+    for (uint32_t g = st >> 3; g < (st + cp) >> 3; ++g) s_gmap[g] = (typename S::GMap)b;
   }
   __syncthreads();
   // phase 3: each thread moves 8-record groups -> one 16-B store into the
@@ -654,11 +665,37 @@ __device__ uint64_t wave_search_le(const uint2 *d, uint64_t n, uint64_t x) {
 //      (16-B loads), test each bin offset against an LDS bitmap of the
 //      bucket's top bins, collect hits {bucket, top row, record index} in LDS
 //      and publish them with one global reservation per workgroup;
-//   U2 k_uniq_hits: one lane per hit: record -> segment -> tile (binary
-//      search of the segment descriptors), recompute the key from the bases,
+//      At the end each workgroup resolves its hits to base positions
+//      (record -> segment through an LDS table of the slice's segments);
+//   U2 k_uniq_hits: one lane per hit: recompute the key from the bases,
 //      per-workgroup dedup in LDS, insert into the global hash set.
 // Hits never serialise inside a wave and no lane waits on another's latency.
 constexpr int kScanBuf = 4096;
+
+// A scan hit {bucket | top row | record index} as k_uniq_hits takes it:
+// top row << 48 | base position of the k-mer (segment a holds the record).
+__device__ __forceinline__ unsigned long long hit_at(const PartArgs &pa, uint32_t b, uint64_t a,
+                                                     unsigned long long e) {
+  const uint64_t i = e & ((1ull << 38) - 1);
+  const uint64_t slot = (e >> 38) & 0x3FFu;
+  const uint64_t p = (uint64_t)pa.desc[(uint64_t)b * pa.max_segs + a].x * kPartTile +
+                     pa.pos[(uint64_t)b * pa.cap + i];
+  return (slot << 48) | p;
+}
+
+// Same, the segment found by a binary search of descriptors [a, z) in global
+// memory (d[a].y <= the record index).
+__device__ unsigned long long resolve_hit(const PartArgs &pa, uint32_t b, uint64_t a, uint64_t z,
+                                          unsigned long long e) {
+  const uint64_t i = e & ((1ull << 38) - 1);
+  const uint2 *d = pa.desc + (uint64_t)b * pa.max_segs;
+  while (z - a > 1) {
+    const uint64_t m = (a + z) >> 1;
+    if (d[m].y <= i) a = m;
+    else z = m;
+  }
+  return hit_at(pa, b, a, e);
+}
 
 __global__ __launch_bounds__(kHistBlock) void k_uniq_scan(PartArgs pa, UniqArgs u,
                                                           const uint32_t *__restrict__ tbuckets,
@@ -675,6 +712,7 @@ __global__ __launch_bounds__(kHistBlock) void k_uniq_scan(PartArgs pa, UniqArgs 
   __shared__ unsigned long long buf[kScanBuf];
   __shared__ uint32_t t_n, s_nh;
   __shared__ unsigned long long s_base;
+  __shared__ uint64_t s_seg[2];
   {  // every block first empties its share of the uniques hash set (k_uniq_hits fills it)
     const uint64_t cap = *set_mask + 1;
     const uint64_t nthr = (uint64_t)gridDim.x * gridDim.y * kHistBlock;
@@ -701,6 +739,8 @@ __global__ __launch_bounds__(kHistBlock) void k_uniq_scan(PartArgs pa, UniqArgs 
   uint64_t n = pa.fill[b] & ((1ull << 40) - 1);
   if (n > pa.cap) n = pa.cap;
   const uint64_t lo = n * r / slices, hi = n * (r + 1) / slices;
+  uint64_t n_seg = pa.fill[b] >> 40;
+  if (n_seg > pa.max_segs) n_seg = pa.max_segs;
   const uint32_t tn = t_n;
   const uint16_t *src = pa.off + (uint64_t)b * pa.cap;
   // one hit record: bucket | top row | record index (< 2^38)
@@ -713,24 +753,30 @@ __global__ __launch_bounds__(kHistBlock) void k_uniq_scan(PartArgs pa, UniqArgs 
     const uint32_t at = atomicAdd(&s_nh, 1u);
     if (at < kScanBuf) {
       buf[at] = e;
-    } else {  // LDS list full (very hit-dense slice): publish this one directly
+    } else {  // LDS list full (very hit-dense slice): resolve and publish this one directly
       const unsigned long long g = atomicAdd(n_hits, 1ull);
-      if (g < hit_cap) hits[g] = e;
+      if (g < hit_cap) hits[g] = resolve_hit(pa, b, 0, n_seg, e);
     }
   };
-  // 8 records per 16-B load, two loads in flight per lane, no barrier in the loop
+  // 8 records per 16-B load, eight loads in flight per lane (the slice is a
+  // few dozen loads per lane: latency, not bandwidth, bounds a shallow loop);
+  // no barrier in the loop
+  constexpr int kU = 8;
   const uint64_t lo8 = lo & ~7ull;
   const uint64_t step = 8ull * kHistBlock;
-  for (uint64_t c0 = lo8 + 8ull * threadIdx.x; c0 < hi; c0 += 2 * step) {
-    const uint64_t c1 = c0 + step;
-    const uint4 v0 = *reinterpret_cast<const uint4 *>(src + c0);
-    uint4 v1 = make_uint4(0, 0, 0, 0);
-    if (c1 < hi) v1 = *reinterpret_cast<const uint4 *>(src + c1);
+  for (uint64_t c0 = lo8 + 8ull * threadIdx.x; c0 < hi; c0 += kU * step) {
+    uint4 v[kU];
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      const uint4 v = half ? v1 : v0;
-      const uint64_t base = half ? c1 : c0;
-      const uint64_t w01 = ((uint64_t)v.y << 32) | v.x, w23 = ((uint64_t)v.w << 32) | v.z;
+    for (int u = 0; u < kU; ++u) {  // unconditional (clamped) loads: one round trip
+      const uint64_t c = c0 + u * step;
+      v[u] = *reinterpret_cast<const uint4 *>(src + (c < hi ? c : lo8));
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const uint64_t base = c0 + u * step;
+      if (base >= hi) break;
+      const uint64_t w01 = ((uint64_t)v[u].y << 32) | v[u].x;
+      const uint64_t w23 = ((uint64_t)v[u].w << 32) | v[u].z;
       uint32_t hm = 0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -748,12 +794,44 @@ __global__ __launch_bounds__(kHistBlock) void k_uniq_scan(PartArgs pa, UniqArgs 
   }
   __syncthreads();
   const uint32_t nh = s_nh < (uint32_t)kScanBuf ? s_nh : (uint32_t)kScanBuf;
-  if (nh) {
-    if (threadIdx.x == 0) s_base = atomicAdd(n_hits, (unsigned long long)nh);
-    __syncthreads();
-    const unsigned long long gb = s_base;
-    for (uint32_t h = threadIdx.x; h < nh; h += kHistBlock)
-      if (gb + h < hit_cap) hits[gb + h] = buf[h];
+  if (!nh) return;
+  // resolve the buffered hits to base positions here (k_uniq_hits then only
+  // recomputes keys): the slice's segments, found by two waves with 64-ary
+  // searches, have their first-record indices staged in LDS (the bitmap is
+  // done with), so each hit costs an LDS search plus two parallel loads
+  // instead of a chain of ~log2(segments) dependent global loads
+  const uint2 *d = pa.desc + (uint64_t)b * pa.max_segs;
+  if (threadIdx.x < 128) {
+    const uint64_t x = threadIdx.x < 64 ? lo : hi - 1;
+    const uint64_t a = wave_search_le(d, n_seg, x);
+    if ((threadIdx.x & 63) == 0) s_seg[threadIdx.x >> 6] = a;
+  }
+  __syncthreads();
+  const uint64_t s0 = s_seg[0], ns = s_seg[1] - s0 + 1;
+  uint32_t *tab = bits;
+  const bool staged = ns <= (uint64_t)(65536 / 32);
+  if (staged)
+    for (uint32_t j = threadIdx.x; j < ns; j += kHistBlock) tab[j] = d[s0 + j].y;
+  if (threadIdx.x == 0) s_base = atomicAdd(n_hits, (unsigned long long)nh);
+  __syncthreads();
+  const unsigned long long gb = s_base;
+  for (uint32_t h = threadIdx.x; h < nh; h += kHistBlock) {
+    if (gb + h >= hit_cap) break;
+    const unsigned long long e = buf[h];
+    unsigned long long out;
+    if (staged) {
+      const uint64_t i = e & ((1ull << 38) - 1);
+      uint32_t a = 0, z = (uint32_t)ns;  // last j with tab[j] <= i (tab[0] <= lo <= i)
+      while (z - a > 1) {
+        const uint32_t m = (a + z) >> 1;
+        if (tab[m] <= i) a = m;
+        else z = m;
+      }
+      out = hit_at(pa, b, s0 + a, e);
+    } else {
+      out = resolve_hit(pa, b, s0, s0 + ns, e);
+    }
+    hits[gb + h] = out;
   }
 }
 
@@ -770,17 +848,8 @@ __global__ __launch_bounds__(256) void k_uniq_hits(KmerInput in, int k, PartArgs
   for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < nh;
        h += (uint64_t)gridDim.x * blockDim.x) {
     const unsigned long long e = hits[h];
-    const uint32_t b = (uint32_t)(e >> 48);
-    const uint32_t slot = (uint32_t)((e >> 38) & 0x3FFu);
-    const uint64_t i = e & ((1ull << 38) - 1);
-    const uint2 *d = pa.desc + (uint64_t)b * pa.max_segs;
-    uint64_t a = 0, z = pa.fill[b] >> 40;  // last segment with first record <= i
-    while (z - a > 1) {
-      const uint64_t m = (a + z) >> 1;
-      if (d[m].y <= i) a = m;
-      else z = m;
-    }
-    const uint64_t p = (uint64_t)d[a].x * kPartTile + pa.pos[(uint64_t)b * pa.cap + i];
+    const uint32_t slot = (uint32_t)(e >> 48);
+    const uint64_t p = e & ((1ull << 48) - 1);
     const uint64_t key = vec_window_key<CANON>(in.bases, in.n_bases, p, k);
     if (key == kEmpty || !seen_before(seen, key)) set_insert(u, slot, key);
   }
@@ -1692,10 +1761,15 @@ hipError_t launch_part(const KmerInput &in, int k, int canonical, uint64_t pool,
                        const PartArgs &pa, hipStream_t s) {
   if (!in.n_tiles) return hipSuccess;
   FastMod fm = make_fastmod(pool);
-  if (canonical)
-    hipLaunchKernelGGL(k_part<true>, dim3((unsigned)in.n_tiles), dim3(kPartBlock), 0, s, in, k, fm, pa);
-  else
-    hipLaunchKernelGGL(k_part<false>, dim3((unsigned)in.n_tiles), dim3(kPartBlock), 0, s, in, k, fm, pa);
+  const dim3 g((unsigned)in.n_tiles), bl(kPartBlock);
+  if (pa.n_buckets > (uint32_t)kMaxBuckets) return hipErrorInvalidValue;
+  if (pa.n_buckets <= 256) {
+    if (canonical) hipLaunchKernelGGL((k_part<true, 256>), g, bl, 0, s, in, k, fm, pa);
+    else hipLaunchKernelGGL((k_part<false, 256>), g, bl, 0, s, in, k, fm, pa);
+  } else {
+    if (canonical) hipLaunchKernelGGL((k_part<true, kMaxBuckets>), g, bl, 0, s, in, k, fm, pa);
+    else hipLaunchKernelGGL((k_part<false, kMaxBuckets>), g, bl, 0, s, in, k, fm, pa);
+  }
   return hipGetLastError();
 }
 

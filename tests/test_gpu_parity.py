@@ -84,10 +84,22 @@ def test_parity_mixed_bytes(k, canon):
     assert_same(g, r)
 
 
-@pytest.mark.parametrize("pool", [1, 2, 7, 64, 100_003, (1 << 20) + 7])
+# 8_388_609 .. 1 << 24: the 512-bucket partition (config 3's 16 M pool);
+# (1 << 24) + 1: past it (direct-atomic count)
+@pytest.mark.parametrize("pool", [1, 2, 7, 64, 100_003, (1 << 20) + 7, 8_388_609, 16_000_000,
+                                  1 << 24, (1 << 24) + 1])
 def test_parity_pools(pool):
     bases, offs = ragged_records(total=120_000, repeats_per_mb=3000, motif_len=150, seed=3)
     g, r = run_both(bases, offs, 31, pool, True)
+    assert_same(g, r)
+
+
+@pytest.mark.parametrize("canon", [True, False])
+def test_parity_wide_partition(canon):
+    # several tiles per bucket at 489 buckets, N bytes, ragged records
+    bases, offs = ragged_records(total=2_000_000, n_rate=0.002, repeats_per_mb=4000,
+                                 motif_len=120, seed=23)
+    g, r = run_both(bases, offs, 27, 16_000_000, canon)
     assert_same(g, r)
 
 
