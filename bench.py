@@ -93,11 +93,14 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     # side measurements only (the metric is pool 2M): e.g. config 3's 16 M pool
     ap.add_argument("--pool", type=int, default=POOL)
+    ap.add_argument("--k", type=int, default=K)
+    ap.add_argument("--kmer-width", type=int, default=64, choices=(64, 128))
     # test-only: rehearse the multi-rank path on a 1-GPU box (gloo, all ranks on cuda:0)
     ap.add_argument("--dist-backend", default="nccl")
     ap.add_argument("--same-device", action="store_true")
     args = ap.parse_args()
     pool = args.pool
+    k = args.k
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -118,12 +121,13 @@ def main() -> int:
     # ---- this rank's shard of the synthetic input (resident in HBM) --------
     bases, offsets = synth.make_records(args.bases, RECS, seed=synth.SEED ^ (rank * 0x9E37),
                                         repeats_per_mb=64, motif_len=200)
-    nk = n_kmers(offsets, K)
+    nk = n_kmers(offsets, k)
     d_bases = torch.from_numpy(bases).to(dev)
     d_offs = torch.from_numpy(offsets.view(np.int64)).to(dev)
     torch.cuda.synchronize()
 
-    ctr = SpikingKmerCounter(K, 1.0, 0.95, 2, 1.0, pool, True, device=local)
+    ctr = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, True, device=local,
+                             kmer_width=args.kmer_width)
     cur_t = torch.as_tensor(_CAI(ctr.device_currents_ptr(), pool), device=dev)
 
     def step():
@@ -182,9 +186,9 @@ def main() -> int:
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
             "data": "synthetic (splitmix64 i.i.d. ACGT, seed 0x4E4B4D52^rank, 64x200-bp planted "
                     "repeats per MB)",
-            "config": {"workload": (f"config 2: {bases.size:,} bases in 7 records per GPU, k=31, "
+            "config": {"workload": (f"config 2: {bases.size:,} bases in 7 records per GPU, k={k}, "
                                     f"pool_size={pool:,}, --canonical, process_parallel"),
-                       "k": K, "pool_size": pool, "bases_per_gpu": int(bases.size),
+                       "k": k, "kmer_width": args.kmer_width, "pool_size": pool, "bases_per_gpu": int(bases.size),
                        "records_per_gpu": RECS, "kmers_per_gpu": nk,
                        "parallelism": f"dp{world}"},
             "roofline": {"bound": "hbm", "kernel": "k_part<canonical> (K1a)",
@@ -195,7 +199,7 @@ def main() -> int:
             "stage_ms": {k2: round(v, 4) for k2, v in timings.items()},
             "total_spikes": total_spikes,
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and k == K and args.kmer_width == 64:
             cb = cpu_baseline(bases, offsets, pool=pool)
             # parity on the same sample: GPU vs the restatement, bit-exact
             sb, so = cb["sample"]

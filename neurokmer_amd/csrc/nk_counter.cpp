@@ -128,6 +128,9 @@ struct nk_counter {
   DevBuf<uint2> p_desc;
   DevBuf<uint32_t> p_over, partials, tbuckets;
   PartArgs last_pa{};
+  // wide partition (pool > 16.7 M or big-key modes past it): coarse buckets
+  DevBuf<uint32_t> w_rec, w_over;
+  DevBuf<unsigned long long> w_fill;
   uint32_t pend_slices = 0;  // K1b partials not yet folded into cur (fused into LIF)
   bool lif_zeroed = false;   // hist/stats already zeroed by this call's prep kernel
   bool state_fresh = true;   // spikes/v/r are logically zero (lazy reset)
@@ -149,6 +152,7 @@ struct nk_counter {
   DevBuf<uint64_t> bcand;
   DevBuf<uint32_t> bcnt;
   bool part_used = false;
+  int gen_km = -1;  // key mode of the last count when it ran k_part_gen (Gen/Wide), else -1
   // input of the last accumulate (for the uniques pass)
   KmerInput last_in{};
   bool have_input = false;
@@ -400,6 +404,120 @@ static int build_exact(nk_counter *c, const KmerInput &in0, hipStream_t s) {
   return NK_OK;
 }
 
+// How one count batch runs:
+//   Part   k <= 32 keys, pool <= 16.7 M: k_part (rolled keys) + k_bucket_hist;
+//          the records are kept for the uniques scan
+//   Gen    k > 32 compat / 128-bit keys, pool <= 16.7 M: k_part_gen (narrow)
+//          + k_bucket_hist
+//   Wide   pool <= 2^31, k <= 64: k_part_gen (coarse) + k_split + k_bucket_hist
+//   Atomic the direct-atomic kernels (k > 64 compat keys, pool > 2^31)
+enum class CountPath { Atomic, Part, Gen, Wide };
+struct CountPlan {
+  CountPath path = CountPath::Atomic;
+  int km = 0;               // key mode of k_part_gen
+  uint64_t tile = kTile;
+  uint32_t slices = 0;      // K1b slices (Part, or > 1: partials; else adds into cur)
+  PartArgs pa{};            // the 32768-bin buckets k_bucket_hist reads
+  GenPartArgs ga{};         // Gen: same arrays as pa; Wide: the coarse buckets
+};
+
+// tests: NK_WIDE_BITS=b forces the wide path with coarse buckets of 2^b bins
+static int wide_bits_forced() {
+  const char *e = getenv("NK_WIDE_BITS");
+  return e ? atoi(e) : 0;
+}
+
+// Sizes the buffers for a batch of about est_bases bases (slack: extra
+// records per bucket region; max_segs: Part's descriptors per bucket) and
+// lists the arrays to zero before the first batch.
+static int plan_count(nk_counter *c, uint64_t est_bases, uint64_t slack, uint64_t max_segs,
+                      CountPlan &cp, ZeroList &z) {
+  cp = CountPlan{};
+  const uint64_t P = c->pool;
+  if (!P) return NK_OK;
+  const int k = (int)c->k;
+  const uint64_t B = (P + kBinsPerBucket - 1) >> kBinBits;
+  cp.km = c->w128 ? 2 : (k > 32 ? 1 : 0);
+  const bool keys_ok = cp.km == 0 || k <= 64;
+  const bool wide_ok = keys_ok && P <= (1ull << 31);
+  const int forced = wide_bits_forced();
+  if (forced > 0 && wide_ok) cp.path = CountPath::Wide;
+  else if (cp.km == 0 && B <= (uint64_t)kMaxBuckets) cp.path = CountPath::Part;
+  else if (keys_ok && B <= (uint64_t)kMaxBuckets) cp.path = CountPath::Gen;
+  else if (wide_ok) cp.path = CountPath::Wide;
+  if (cp.path == CountPath::Atomic) return NK_OK;
+  cp.tile = kPartTile;
+  const uint64_t est = std::max<uint64_t>(est_bases, 1);
+  int rc;
+  uint64_t cap;
+  if (cp.path == CountPath::Wide) {
+    int bits = kBinBits;
+    while (((P + (1ull << bits) - 1) >> bits) > (uint64_t)kWideMaxBuckets) ++bits;
+    if (forced > bits) bits = std::min(forced, kBinBits + kMaxSplitBits);
+    const uint64_t C = (P + (1ull << bits) - 1) >> bits;
+    uint64_t cap_c = est / C * 5 / 4 + slack;
+    cap_c = (cap_c + 63) & ~63ull;
+    if ((rc = c->w_rec.ensure(C * cap_c)) || (rc = c->w_fill.ensure(C)) || (rc = c->w_over.ensure(C)))
+      return rc;
+    cp.ga = GenPartArgs{(uint32_t)C, bits, cap_c, c->w_rec.p, c->w_fill.p, c->w_over.p,
+                        (unsigned long long *)c->cur.p};
+    z.ptr[z.n] = c->w_fill.p; z.bytes[z.n++] = C * 8;
+    z.ptr[z.n] = c->w_over.p; z.bytes[z.n++] = C * 4;
+    // a fine bucket takes up to 7 pad records per split tile of its coarse bucket
+    cap = est / B * 5 / 4 + 8 * ((cap_c + kPartTile - 1) / kPartTile) + 1024;
+  } else {
+    cap = est / B * 5 / 4 + slack;
+  }
+  cap = (cap + 63) & ~63ull;
+  // one round of 1-per-CU workgroups (128 KiB LDS each) on 256 CUs
+  cp.slices = (uint32_t)std::max<uint64_t>(1, 256 / B);
+  if ((rc = c->p_off.ensure(B * cap)) || (rc = c->p_fill.ensure(B)) || (rc = c->p_over.ensure(B)) ||
+      ((cp.path == CountPath::Part || cp.slices > 1) && (rc = c->partials.ensure(cp.slices * P))))
+    return rc;
+  PartArgs &pa = cp.pa;
+  pa.n_buckets = (uint32_t)B;
+  pa.cap = cap;
+  pa.off = c->p_off.p;
+  pa.fill = c->p_fill.p;
+  pa.overflow = c->p_over.p;
+  pa.currents = (unsigned long long *)c->cur.p;
+  if (cp.path == CountPath::Part) {
+    if ((rc = c->p_pos.ensure(B * cap)) || (rc = c->p_desc.ensure(B * max_segs))) return rc;
+    pa.pos = c->p_pos.p;
+    pa.desc = c->p_desc.p;
+    pa.max_segs = max_segs;
+  }
+  if (cp.path == CountPath::Gen)
+    cp.ga = GenPartArgs{(uint32_t)B, kBinBits, cap, c->p_off.p, c->p_fill.p, c->p_over.p,
+                        (unsigned long long *)c->cur.p};
+  z.ptr[z.n] = c->p_fill.p; z.bytes[z.n++] = B * 8;
+  z.ptr[z.n] = c->p_over.p; z.bytes[z.n++] = B * 4;
+  return NK_OK;
+}
+
+// K1b of a Gen/Wide batch: partials (several slices per bucket) or straight
+// into the currents
+static hipError_t gen_hist(nk_counter *c, const CountPlan &cp, bool defer_partials, hipStream_t s) {
+  if (cp.slices > 1) {
+    hipError_t e = launch_bucket_hist(cp.pa, c->pool, cp.slices, c->partials.p, s);
+    if (e != hipSuccess) return e;
+    if (defer_partials) {
+      c->pend_slices = cp.slices;
+      return hipSuccess;
+    }
+    return launch_partials_add(c->partials.p, cp.slices, c->pool, c->cur.p, s);
+  }
+  return launch_bucket_hist(cp.pa, c->pool, 1, nullptr, s);
+}
+
+// Gen/Wide count kernels of one batch (before K1b)
+static hipError_t gen_count(nk_counter *c, const CountPlan &cp, const KmerInput &in, hipStream_t s) {
+  const bool wide = cp.path == CountPath::Wide;
+  hipError_t e = launch_part_gen(in, (int)c->k, c->canonical, cp.km, c->pool, cp.ga, wide ? 1 : 0, s);
+  if (e != hipSuccess || !wide) return e;
+  return launch_split(cp.ga, cp.pa, s);
+}
+
 // defer_partials: leave K1c (currents += partials) to the LIF kernel of the
 // same process call instead of a separate pass
 static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_offs,
@@ -417,61 +535,43 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
   in.offsets = d_offs;
   in.n_recs = n_recs;
   in.n_bases = n_bases;
-  const uint64_t B = (c->pool + kBinsPerBucket - 1) >> kBinBits;
-  const bool part = !c->w128 && c->k <= 32 && c->pool > 0 && B <= (uint64_t)kMaxBuckets;
-  const uint64_t tile = part ? kPartTile : kTile;
-  in.n_tiles = n_tiles_for(n_bases, tile);
-  int rc = c->tile_rec.ensure(std::max<uint64_t>(in.n_tiles, 1));
-  if (rc) return rc;
-  in.tile_rec = c->tile_rec.p;
-  c->part_used = part && in.n_tiles > 0;
   // one prep kernel: tile -> first record index, and every buffer the count
   // (and, for a process call, the LIF) accumulates into zeroed
   ZeroList z{};
   z.ptr[z.n] = c->cur.p; z.bytes[z.n++] = c->pool * 8;
-  PartArgs pa{};
-  uint32_t slices = 0;
-  if (c->part_used) {
-    // bucket regions: 1.25x the fair share + one tile of slack (overflow is
-    // still exact: the excess is counted with direct atomics)
-    uint64_t cap = n_bases / B * 5 / 4 + kPartTile;
-    cap = (cap + 63) & ~63ull;
-    // one round of 1-per-CU workgroups (128 KiB LDS each) on 256 CUs
-    slices = (uint32_t)std::max<uint64_t>(1, 256 / B);
-    if ((rc = c->p_off.ensure(B * cap)) || (rc = c->p_pos.ensure(B * cap)) ||
-        (rc = c->p_fill.ensure(B)) || (rc = c->p_desc.ensure(B * in.n_tiles)) ||
-        (rc = c->p_over.ensure(B)) || (rc = c->partials.ensure(slices * c->pool)))
-      return rc;
-    pa.n_buckets = (uint32_t)B;
-    pa.cap = cap;
-    pa.off = c->p_off.p;
-    pa.pos = c->p_pos.p;
-    pa.fill = c->p_fill.p;
-    pa.desc = c->p_desc.p;
-    pa.max_segs = in.n_tiles;
-    pa.overflow = c->p_over.p;
-    pa.currents = (unsigned long long *)c->cur.p;
-    z.ptr[z.n] = c->p_fill.p; z.bytes[z.n++] = B * 8;
-    z.ptr[z.n] = c->p_over.p; z.bytes[z.n++] = B * 4;
-  }
+  CountPlan cp;
+  // bucket regions: 1.25x the fair share + one tile of slack (overflow is
+  // still exact: the excess is counted with direct atomics)
+  int rc = plan_count(c, n_bases, kPartTile, n_tiles_for(n_bases, kPartTile), cp, z);
+  if (rc) return rc;
+  in.n_tiles = n_tiles_for(n_bases, cp.tile);
+  if ((rc = c->tile_rec.ensure(std::max<uint64_t>(in.n_tiles, 1)))) return rc;
+  in.tile_rec = c->tile_rec.p;
+  const bool counted = cp.path != CountPath::Atomic && in.n_tiles > 0;
+  c->part_used = counted && cp.path == CountPath::Part;
+  c->gen_km = (cp.path == CountPath::Gen || cp.path == CountPath::Wide) ? cp.km : -1;
   if (defer_partials) {  // the LIF of this process call accumulates into these
     z.ptr[z.n] = c->hist.p;  z.bytes[z.n++] = kHistBins * kHistCopies * 4;
     z.ptr[z.n] = c->stats.p; z.bytes[z.n++] = 16;
     c->lif_zeroed = true;
   }
   HIPCHK(mark(c, 0, s));
-  HIPCHK(launch_prep(in, tile, c->tile_rec.p, z, s));
+  HIPCHK(launch_prep(in, cp.tile, c->tile_rec.p, z, s));
   c->cur_fresh = false;
   HIPCHK(mark(c, 1, s));
   if (c->part_used) {
-    HIPCHK(launch_part(in, (int)c->k, c->canonical, c->pool, pa, s));
+    HIPCHK(launch_part(in, (int)c->k, c->canonical, c->pool, cp.pa, s));
     HIPCHK(mark(c, 2, s));
-    HIPCHK(launch_bucket_hist(pa, c->pool, slices, c->partials.p, s));
+    HIPCHK(launch_bucket_hist(cp.pa, c->pool, cp.slices, c->partials.p, s));
     if (defer_partials)
-      c->pend_slices = slices;
+      c->pend_slices = cp.slices;
     else
-      HIPCHK(launch_partials_add(c->partials.p, slices, c->pool, c->cur.p, s));
-    c->last_pa = pa;
+      HIPCHK(launch_partials_add(c->partials.p, cp.slices, c->pool, c->cur.p, s));
+    c->last_pa = cp.pa;
+  } else if (counted) {
+    HIPCHK(gen_count(c, cp, in, s));
+    HIPCHK(mark(c, 2, s));
+    HIPCHK(gen_hist(c, cp, defer_partials, s));
   } else {
     if (c->w128)
       HIPCHK(launch_count128(in, (int)c->k, c->canonical, c->pool, c->cur.p, s));
@@ -614,11 +714,14 @@ static int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, bool post_don
                                s));
   } else {
     KmerInput in = c->last_in;
-    in.n_tiles = n_tiles_for(in.n_bases, kTile);
+    const uint64_t tile = c->gen_km >= 0 ? kPartTile : kTile;
+    in.n_tiles = n_tiles_for(in.n_bases, tile);
     if ((rc = c->tile_rec.ensure(std::max<uint64_t>(in.n_tiles, 1)))) return rc;
     in.tile_rec = c->tile_rec.p;
-    HIPCHK(launch_tile_rec(in, kTile, c->tile_rec.p, s));
-    if (c->w128)
+    HIPCHK(launch_tile_rec(in, tile, c->tile_rec.p, s));
+    if (c->gen_km >= 0)
+      HIPCHK(launch_uniq_gen(in, (int)c->k, c->canonical, c->gen_km, c->pool, u, s));
+    else if (c->w128)
       HIPCHK(launch_uniques128(in, (int)c->k, c->canonical, c->pool, u, s));
     else
       HIPCHK(launch_uniques(in, (int)c->k, c->canonical, c->pool, u, s));
@@ -1007,48 +1110,30 @@ static int need_exact(nk_counter *c) {
 // Chunked accumulate over a growing resident input (GPU FASTX ingest)
 // ---------------------------------------------------------------------------
 struct StreamAcc {
-  bool part = false;
-  uint64_t tile = kTile;
-  uint32_t slices = 0;
-  PartArgs pa{};
+  CountPlan cp;
 };
 
-// zero the accumulators and size the partition arena for ~est_bases bases
-static int acc_begin(nk_counter *c, uint64_t est_bases, StreamAcc &sa, hipStream_t s) {
+// zero the accumulators and size the partition arena: Part keeps every
+// record until acc_end (~est_bases bases), Gen/Wide histogram each batch
+// (<= batch_bases bases) as it is counted
+static int acc_begin(nk_counter *c, uint64_t est_bases, uint64_t batch_bases, StreamAcc &sa,
+                     hipStream_t s) {
   int rc;
-  const uint64_t B = (c->pool + kBinsPerBucket - 1) >> kBinBits;
-  sa.part = !c->w128 && c->k <= 32 && c->pool > 0 && B <= (uint64_t)kMaxBuckets;
-  sa.tile = sa.part ? kPartTile : kTile;
   ZeroList z{};
   z.ptr[z.n] = c->cur.p; z.bytes[z.n++] = c->pool * 8;
-  if (sa.part) {
-    uint64_t cap = std::max<uint64_t>(est_bases, 1) / B * 5 / 4 + 4 * kPartTile;
-    cap = (cap + 63) & ~63ull;
-    sa.slices = (uint32_t)std::max<uint64_t>(1, 256 / B);
-    // segments per bucket: one per tile per launch; chunk-straddling tiles add a few
-    const uint64_t max_segs = n_tiles_for(std::max<uint64_t>(est_bases, 1), kPartTile) + 4096;
-    if ((rc = c->p_off.ensure(B * cap)) || (rc = c->p_pos.ensure(B * cap)) ||
-        (rc = c->p_fill.ensure(B)) || (rc = c->p_desc.ensure(B * max_segs)) ||
-        (rc = c->p_over.ensure(B)) || (rc = c->partials.ensure(sa.slices * c->pool)))
-      return rc;
-    sa.pa.n_buckets = (uint32_t)B;
-    sa.pa.cap = cap;
-    sa.pa.off = c->p_off.p;
-    sa.pa.pos = c->p_pos.p;
-    sa.pa.fill = c->p_fill.p;
-    sa.pa.desc = c->p_desc.p;
-    sa.pa.max_segs = max_segs;
-    sa.pa.overflow = c->p_over.p;
-    sa.pa.currents = (unsigned long long *)c->cur.p;
-    z.ptr[z.n] = c->p_fill.p; z.bytes[z.n++] = B * 8;
-    z.ptr[z.n] = c->p_over.p; z.bytes[z.n++] = B * 4;
-  }
+  const uint64_t B = (c->pool + kBinsPerBucket - 1) >> kBinBits;
+  const bool part_like = !c->w128 && c->k <= 32 && B <= (uint64_t)kMaxBuckets && !wide_bits_forced();
+  const uint64_t est = part_like ? est_bases : std::min(est_bases, batch_bases);
+  // segments per bucket: one per tile per launch; chunk-straddling tiles add a few
+  const uint64_t max_segs = n_tiles_for(std::max<uint64_t>(est, 1), kPartTile) + 4096;
+  if ((rc = plan_count(c, est, 4 * kPartTile, max_segs, sa.cp, z))) return rc;
   z.ptr[z.n] = c->hist.p;  z.bytes[z.n++] = kHistBins * kHistCopies * 4;
   z.ptr[z.n] = c->stats.p; z.bytes[z.n++] = 16;
   c->lif_zeroed = true;
   if (c->pool) HIPCHK(launch_zero(z, s));
   c->cur_fresh = false;
-  c->part_used = sa.part;
+  c->part_used = sa.cp.path == CountPath::Part;
+  c->gen_km = (sa.cp.path == CountPath::Gen || sa.cp.path == CountPath::Wide) ? sa.cp.km : -1;
   return NK_OK;
 }
 
@@ -1056,21 +1141,39 @@ static int acc_begin(nk_counter *c, uint64_t est_bases, StreamAcc &sa, hipStream
 static int acc_batch(nk_counter *c, StreamAcc &sa, const KmerInput &whole, uint64_t pos_lo,
                      uint64_t pos_hi, hipStream_t s) {
   if (pos_hi <= pos_lo || !c->pool) return NK_OK;
+  const CountPlan &cp = sa.cp;
   KmerInput in = whole;
-  in.tile_base = pos_lo / sa.tile;
-  in.n_tiles = (pos_hi + sa.tile - 1) / sa.tile - in.tile_base;
+  in.tile_base = pos_lo / cp.tile;
+  in.n_tiles = (pos_hi + cp.tile - 1) / cp.tile - in.tile_base;
   in.pos_lo = pos_lo;
   in.pos_hi = pos_hi;
   int rc = c->tile_rec.ensure(in.n_tiles);
   if (rc) return rc;
   in.tile_rec = c->tile_rec.p;
-  HIPCHK(launch_tile_rec(in, sa.tile, c->tile_rec.p, s));
-  if (sa.part)
-    HIPCHK(launch_part(in, (int)c->k, c->canonical, c->pool, sa.pa, s));
-  else if (c->w128)
-    HIPCHK(launch_count128(in, (int)c->k, c->canonical, c->pool, c->cur.p, s));
-  else
-    HIPCHK(launch_count(in, (int)c->k, c->canonical, c->pool, c->cur.p, s));
+  HIPCHK(launch_tile_rec(in, cp.tile, c->tile_rec.p, s));
+  switch (cp.path) {
+    case CountPath::Part:
+      HIPCHK(launch_part(in, (int)c->k, c->canonical, c->pool, cp.pa, s));
+      break;
+    case CountPath::Gen:
+    case CountPath::Wide: {
+      HIPCHK(gen_count(c, cp, in, s));
+      HIPCHK(gen_hist(c, cp, false, s));
+      ZeroList z{};  // empty the regions for the next batch
+      z.ptr[z.n] = cp.pa.fill; z.bytes[z.n++] = (uint64_t)cp.pa.n_buckets * 8;
+      if (cp.path == CountPath::Wide) {
+        z.ptr[z.n] = cp.ga.fill; z.bytes[z.n++] = (uint64_t)cp.ga.n_buckets * 8;
+      }
+      HIPCHK(launch_zero(z, s));
+      break;
+    }
+    case CountPath::Atomic:
+      if (c->w128)
+        HIPCHK(launch_count128(in, (int)c->k, c->canonical, c->pool, c->cur.p, s));
+      else
+        HIPCHK(launch_count(in, (int)c->k, c->canonical, c->pool, c->cur.p, s));
+      break;
+  }
   return NK_OK;
 }
 
@@ -1078,13 +1181,13 @@ static int acc_batch(nk_counter *c, StreamAcc &sa, const KmerInput &whole, uint6
 // bookkeeping of a finished input
 static int acc_end(nk_counter *c, StreamAcc &sa, const KmerInput &whole, hipStream_t s) {
   int rc;
-  if (sa.part) {
-    HIPCHK(launch_bucket_hist(sa.pa, c->pool, sa.slices, c->partials.p, s));
-    c->pend_slices = sa.slices;
-    c->last_pa = sa.pa;
+  if (sa.cp.path == CountPath::Part) {
+    HIPCHK(launch_bucket_hist(sa.cp.pa, c->pool, sa.cp.slices, c->partials.p, s));
+    c->pend_slices = sa.cp.slices;
+    c->last_pa = sa.cp.pa;
   }
   c->last_in = whole;
-  c->last_in.n_tiles = n_tiles_for(whole.n_bases, sa.tile);
+  c->last_in.n_tiles = n_tiles_for(whole.n_bases, sa.cp.tile);
   c->have_input = true;
   c->top_valid = false;
   if (c->opts.exact_counts && (rc = build_exact(c, whole, s))) return rc;
@@ -1161,7 +1264,7 @@ static int ingest_file(nk_counter *c, const char *path, bool *fallback) {
   st.at_line_start = 1;
   HIPCHK(hipMemcpyAsync(dst.p, &st, sizeof st, hipMemcpyHostToDevice, s));
   StreamAcc sa;
-  if ((rc = acc_begin(c, fastq ? cap_bases / 2 : cap_bases, sa, s))) return rc;
+  if ((rc = acc_begin(c, fastq ? cap_bases / 2 : cap_bases, chunk + room + 64, sa, s))) return rc;
   uint64_t counted = 0;  // windows below this start were counted
   for (;;) {
     const uint8_t *data = hb[cur].p + start;

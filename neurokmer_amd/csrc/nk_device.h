@@ -86,6 +86,13 @@ struct FastMod {
   uint64_t magic;
 };
 
+inline FastMod make_fastmod(uint64_t p) {
+  FastMod f;
+  f.p = p;
+  f.magic = p ? (~0ULL) / p : 0;
+  return f;
+}
+
 __device__ __forceinline__ uint64_t fastmod(uint64_t h, FastMod fm) {
   uint64_t q = __umul64hi(h, fm.magic);
   uint64_t r = h - q * fm.p;

@@ -116,6 +116,22 @@ struct PartArgs {
   unsigned long long *currents;   // overflow target
 };
 
+// Generic partition (nk_wide.hip): any key mode; narrow (u16 offsets into
+// 32768-bin buckets, bin_bits 15) or wide (u32 offsets into <= 256 coarse
+// buckets of 2^bin_bits bins, split into fine buckets by k_split).
+constexpr int kWideMaxBuckets = 256;
+constexpr int kMaxSplitBits = 9;
+constexpr int kMaxSplit = 1 << kMaxSplitBits;  // fine buckets per coarse bucket
+struct GenPartArgs {
+  uint32_t n_buckets;
+  int bin_bits;
+  uint64_t cap;                   // records per bucket region (multiple of 64)
+  void *rec;                      // [bucket][cap] u16 (narrow) or u32 (wide) bin offsets
+  unsigned long long *fill;       // [bucket] records reserved
+  uint32_t *overflow;             // [bucket] region overflowed (counted directly)
+  unsigned long long *currents;   // overflow target
+};
+
 struct UniqArgs {
   const TopCand *top;  // top-N rows (sorted)
   uint32_t n_top;
@@ -187,6 +203,13 @@ hipError_t launch_set_merge(const uint64_t *keys, uint64_t n, uint64_t pool, con
 
 hipError_t launch_part(const KmerInput &in, int k, int canonical, uint64_t pool,
                        const PartArgs &pa, hipStream_t s);
+// key mode km: 0 k <= 32 u64, 1 k > 32 compat, 2 --kmer-width=128
+hipError_t launch_part_gen(const KmerInput &in, int k, int canonical, int km, uint64_t pool,
+                           const GenPartArgs &ga, int wide, hipStream_t s);
+// uniques rescan over kPartTile tiles for the Gen/Wide count paths
+hipError_t launch_uniq_gen(const KmerInput &in, int k, int canonical, int km, uint64_t pool,
+                           const UniqArgs &u, hipStream_t s);
+hipError_t launch_split(const GenPartArgs &ga, const PartArgs &fine, hipStream_t s);
 hipError_t launch_bucket_hist(const PartArgs &pa, uint64_t pool, uint32_t slices,
                               uint32_t *partials, hipStream_t s);
 hipError_t launch_partials_add(const uint32_t *partials, uint32_t slices, uint64_t pool,

@@ -20,6 +20,7 @@
 #include <type_traits>
 
 #include "nk_device.h"
+#include "nk_gen.h"
 #include "nk_kernels.h"
 #include "nk_tile.h"
 
@@ -291,6 +292,39 @@ __global__ __launch_bounds__(kBlock) void k_kmers128(KmerInput in, int k, FastMo
   }
 }
 
+// Uniques rescan for the generic count paths (nk_wide.hip: k > 32 compat,
+// 128-bit keys, pools past the narrow partition): the same 8192-position
+// tiles and LDS keys as k_part_gen; a window whose neuron is a top row goes
+// into the uniques set.
+template <int KM, bool CANON>
+__global__ __launch_bounds__(kPartBlock) void k_uniq_gen(KmerInput in, int k, FastMod fm,
+                                                         UniqArgs u) {
+  constexpr bool kRaw = !CANON;
+  __shared__ TileLds<kPartTile, kRaw> L;
+  __shared__ unsigned long long seen[KM == 2 ? 1 : kSeen];
+  extern __shared__ uint64_t dyn[];  // probe table
+  uint64_t *tbl_idx = dyn;
+  uint32_t *tbl_slot = reinterpret_cast<uint32_t *>(dyn + u.tbl_size);
+  if (KM != 2) seen_init(seen);
+  build_top_tbl(u, tbl_idx, tbl_slot);  // contains __syncthreads
+  const uint64_t tile = in.tile_base + blockIdx.x;
+  const uint64_t T0 = tile * (uint64_t)kPartTile;
+  stage_tile<kPartTile, kPartBlock, kRaw>(L, in, tile, k);
+  const int q0 = threadIdx.x * kPer;
+  RecCursor rc;
+  rec_cursor_init<KM>(rc, in, T0 + (uint64_t)q0);
+  for (int j = 0; j < kPer; ++j) {
+    const int q = q0 + j;
+    if (!window_valid(L, T0, q, k, in.n_bases, in.pos_lo, in.pos_hi)) continue;
+    const Key128 key = gen_key<KM, CANON>(L, in, q, T0 + (uint64_t)q, k, rc);
+    const uint64_t idx = fastmod(gen_hash<KM>(key), fm);
+    const int slot = probe_top(tbl_idx, tbl_slot, u.tbl_size - 1, idx);
+    if (slot < 0) continue;
+    if (KM == 2) set_insert128(u, (uint32_t)slot, key);
+    else if (key.lo == kEmpty || !seen_before(seen, key.lo)) set_insert(u, (uint32_t)slot, key.lo);
+  }
+}
+
 __global__ void k_set_fill128(unsigned long long *__restrict__ S, const uint64_t *__restrict__ mask) {
   const uint64_t n = 3 * (*mask + 1);
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -539,11 +573,14 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
   }
 }
 
+// partials == nullptr: add the histogram into pa.currents instead (u64; plain
+// read-modify-write of the bins this workgroup owns when slices == 1, atomics
+// otherwise; bins that stayed zero are not touched)
 __global__ __launch_bounds__(kHistBlock) void k_bucket_hist(PartArgs pa, uint64_t pool,
                                                             uint32_t slices,
                                                             uint32_t *__restrict__ partials) {
   __shared__ uint32_t h[kBinsPerBucket + 1];  // + a spill bin for pad records
-  const uint32_t b = blockIdx.y, r = blockIdx.x;
+  const uint32_t b = blockIdx.x, r = blockIdx.y;  // buckets on x: up to 65536 of them
   for (int i = threadIdx.x; i <= kBinsPerBucket; i += kHistBlock) h[i] = 0;
   auto bin = [](uint32_t off) { return off < (uint32_t)kBinsPerBucket ? off : (uint32_t)kBinsPerBucket; };
   __syncthreads();
@@ -590,6 +627,16 @@ __global__ __launch_bounds__(kHistBlock) void k_bucket_hist(PartArgs pa, uint64_
   __syncthreads();
   const uint64_t nb0 = (uint64_t)b << kBinBits;
   const uint64_t nbins = pool - nb0 < (uint64_t)kBinsPerBucket ? pool - nb0 : kBinsPerBucket;
+  if (!partials) {
+    unsigned long long *cur = pa.currents + nb0;
+    for (uint32_t t = threadIdx.x; t < nbins; t += kHistBlock) {
+      const uint32_t x = h[t];
+      if (!x) continue;
+      if (slices == 1) cur[t] += x;
+      else atomicAdd(&cur[t], (unsigned long long)x);
+    }
+    return;
+  }
   uint32_t *dst = partials + (uint64_t)r * pool + nb0;
   for (uint32_t t = threadIdx.x; t < nbins; t += kHistBlock) dst[t] = h[t];
 }
@@ -1431,20 +1478,31 @@ __global__ __launch_bounds__(kBlock) void k_topn_count(const uint64_t *__restric
   if (threadIdx.x == 0) tie_cnt[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
 }
 
+// in-place exclusive scan of the per-block tie counts (one block; the counts
+// sum to <= pool < 2^32)
+__global__ __launch_bounds__(1024) void k_tie_scan(uint32_t *__restrict__ cnt, uint32_t n) {
+  __shared__ uint32_t s_w[16];
+  const uint32_t per = (n + 1023) / 1024;
+  const uint32_t lo = threadIdx.x * per, hi = lo + per < n ? lo + per : n;
+  uint32_t sum = 0;
+  for (uint32_t i = lo; i < hi; ++i) sum += cnt[i];
+  uint32_t tot;
+  uint32_t run = block_excl_scan<uint32_t>(sum, s_w, &tot);
+  for (uint32_t i = lo; i < hi; ++i) {
+    const uint32_t x = cnt[i];
+    cnt[i] = run;
+    run += x;
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_topn_emit(const uint64_t *__restrict__ sc,
                                                       uint64_t pool, TopState *__restrict__ st,
                                                       const uint32_t *__restrict__ tie_cnt,
                                                       TopCand *__restrict__ cand) {
-  __shared__ unsigned long long s_pre[kBlock / 64];
   __shared__ uint32_t s_scan[kBlock];
   const uint64_t T = st->T, need = st->need, n_above = st->n_above;
-  // ties in earlier blocks
-  unsigned long long pre = 0;
-  for (uint32_t b = threadIdx.x; b < blockIdx.x; b += kBlock) pre += tie_cnt[b];
-  for (int o = 32; o > 0; o >>= 1) pre += __shfl_down(pre, o, 64);
-  if ((threadIdx.x & 63) == 0) s_pre[threadIdx.x >> 6] = pre;
-  __syncthreads();
-  const unsigned long long prefix = s_pre[0] + s_pre[1] + s_pre[2] + s_pre[3];
+  // ties in earlier blocks (k_tie_scan turned the counts into an exclusive scan)
+  const unsigned long long prefix = tie_cnt[blockIdx.x];
   // thread t owns 8 consecutive neurons -> ranks in index order
   const uint64_t base = (uint64_t)blockIdx.x * kTopChunk + (uint64_t)threadIdx.x * 8;
   uint32_t ties = 0;
@@ -1558,13 +1616,6 @@ __global__ void k_set_merge(const uint64_t *__restrict__ keys, uint64_t n, FastM
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-static FastMod make_fastmod(uint64_t p) {
-  FastMod f;
-  f.p = p;
-  f.magic = p ? (~0ULL) / p : 0;
-  return f;
-}
-
 uint64_t n_tiles_for(uint64_t n_bases, uint64_t tile) { return (n_bases + tile - 1) / tile; }
 
 uint64_t top_tbl_size(uint32_t n_top) {
@@ -1661,6 +1712,7 @@ hipError_t launch_topn_count(const uint64_t *sc, uint64_t pool, const TopState *
   if (!pool) return hipSuccess;
   hipLaunchKernelGGL(k_topn_count, dim3(topn_blocks(pool)), dim3(kBlock), 0, s, sc, pool, st,
                      tie_cnt);
+  hipLaunchKernelGGL(k_tie_scan, dim3(1), dim3(1024), 0, s, tie_cnt, (uint32_t)topn_blocks(pool));
   return hipGetLastError();
 }
 
@@ -1701,6 +1753,26 @@ static hipError_t launch_kmers128(const KmerInput &in, int k, int canonical, uin
   else hipLaunchKernelGGL((k_kmers128<false, MODE>), g, b, dyn, s, in, k, fm, cur, u);
   return hipGetLastError();
 }
+hipError_t launch_uniq_gen(const KmerInput &in, int k, int canonical, int km, uint64_t pool,
+                           const UniqArgs &u, hipStream_t s) {
+  if (!in.n_tiles) return hipSuccess;
+  if (km < 0 || km > 2 || k < 1 || k > 64 || (km == 0 && k > 32) || (km == 1 && k <= 32))
+    return hipErrorInvalidValue;
+  const FastMod fm = make_fastmod(pool);
+  const dim3 g((unsigned)in.n_tiles), b(kPartBlock);
+  const size_t dyn = tbl_bytes(u);
+  if (canonical) {
+    if (km == 0) hipLaunchKernelGGL((k_uniq_gen<0, true>), g, b, dyn, s, in, k, fm, u);
+    else if (km == 1) hipLaunchKernelGGL((k_uniq_gen<1, true>), g, b, dyn, s, in, k, fm, u);
+    else hipLaunchKernelGGL((k_uniq_gen<2, true>), g, b, dyn, s, in, k, fm, u);
+  } else {
+    if (km == 0) hipLaunchKernelGGL((k_uniq_gen<0, false>), g, b, dyn, s, in, k, fm, u);
+    else if (km == 1) hipLaunchKernelGGL((k_uniq_gen<1, false>), g, b, dyn, s, in, k, fm, u);
+    else hipLaunchKernelGGL((k_uniq_gen<2, false>), g, b, dyn, s, in, k, fm, u);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_count128(const KmerInput &in, int k, int canonical, uint64_t pool,
                            uint64_t *currents, hipStream_t s) {
   UniqArgs u{};
@@ -1775,7 +1847,8 @@ hipError_t launch_part(const KmerInput &in, int k, int canonical, uint64_t pool,
 
 hipError_t launch_bucket_hist(const PartArgs &pa, uint64_t pool, uint32_t slices,
                               uint32_t *partials, hipStream_t s) {
-  hipLaunchKernelGGL(k_bucket_hist, dim3(slices, pa.n_buckets), dim3(kHistBlock), 0, s, pa, pool,
+  if (!pa.n_buckets) return hipSuccess;
+  hipLaunchKernelGGL(k_bucket_hist, dim3(pa.n_buckets, slices), dim3(kHistBlock), 0, s, pa, pool,
                      slices, partials);
   return hipGetLastError();
 }

@@ -1,0 +1,266 @@
+// nk_wide.hip — the partitioned count for every key mode and pool size.
+//
+// k_part (nk_kernels.hip) is the fast path of the metric: k <= 32 keys rolled
+// in registers, pool <= 16.7 M (bucket = neuron >> 15, 512 buckets of 32768
+// bins).  This file covers the rest of SURVEY.md §8a without global atomics
+// per k-mer (the direct-atomic kernels run at ~20 G adds/s chip-wide):
+//
+//   key modes   KM 0  k <= 32 u64 keys at a position (pools past 16.7 M)
+//               KM 1  k > 32, the reference's release-build u64 semantics
+//                     (NK_KMER_COMPAT, src/models.rs:188,192-194,260-266)
+//               KM 2  --kmer-width=128 (u128 keys, SipHash over 16 bytes)
+//   narrow      pool <= 512 * 32768: k_part_gen writes u16 bin offsets
+//               straight into the 32768-bin buckets k_bucket_hist reads
+//   wide        pool <= 2^31: k_part_gen sorts into <= 256 coarse buckets of
+//               2^S bins (u32 offsets), k_split re-sorts each coarse bucket
+//               into its 2^(S-15) fine buckets (u16 offsets), and the same
+//               k_bucket_hist histograms them (two LDS counting sorts, both
+//               with one HBM reservation atomic per (tile, bucket))
+//
+// Records past a bucket's region are counted with direct atomics (exact).  No
+// positions are kept: the uniques of these modes come from the rescan pass.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "nk_device.h"
+#include "nk_kernels.h"
+#include "nk_gen.h"
+#include "nk_tile.h"
+
+namespace nk {
+
+namespace {
+
+template <bool WIDE>
+struct GenShape {
+  static constexpr int kMaxB = WIDE ? kWideMaxBuckets : kMaxBuckets;
+  static constexpr int kSlots = kPartTile + 7 * kMaxB;
+  static constexpr int kGroups = kSlots / 8;
+  static constexpr int kGroupIters = (kGroups + kPartBlock - 1) / kPartBlock;
+  using Rec = typename std::conditional<WIDE, uint32_t, uint16_t>::type;
+  using GMap = typename std::conditional<(kMaxB > 256), uint16_t, uint8_t>::type;
+  static constexpr uint32_t kPad = WIDE ? 0xFFFFFFFFu : 0xFFFFu;
+};
+
+// LDS counting sort of one tile's records by bucket, one HBM reservation per
+// (tile, bucket), 16-B stores of 8-record groups (shared by k_part_gen and
+// k_split).  E[j] = bucket << 16 | rank (bucket == nb: no record), O[j] = the
+// record.  Ends the kernel.
+template <bool WIDE, int PER>
+__device__ __forceinline__ void sort_and_store(const uint32_t (&E)[PER], const uint32_t (&O)[PER],
+                                               uint32_t nb, uint32_t *s_cnt, uint32_t *s_start,
+                                               uint32_t *s_base, uint32_t *s_fit,
+                                               typename GenShape<WIDE>::Rec *s_rec,
+                                               typename GenShape<WIDE>::GMap *s_gmap,
+                                               unsigned long long *__restrict__ fill,
+                                               uint32_t *__restrict__ overflow, uint64_t cap,
+                                               typename GenShape<WIDE>::Rec *__restrict__ dst_rec,
+                                               uint64_t bucket_base, int bin_bits,
+                                               unsigned long long *__restrict__ currents) {
+  using S = GenShape<WIDE>;
+  using Rec = typename S::Rec;
+  const int tid = threadIdx.x;
+  __syncthreads();
+  if (tid < 64) {  // exclusive scan of the padded counts (one wave)
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < nb; b0 += 64) {
+      const uint32_t b = b0 + tid;
+      const uint32_t c = b < nb ? (s_cnt[b] + 7u) & ~7u : 0;
+      uint32_t x = c;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (tid >= o) x += y;
+      }
+      if (b < nb) s_start[b] = carry + x - c;
+      carry += __shfl(x, 63, 64);
+    }
+    if (tid == 0) s_start[nb] = carry;
+  }
+  for (uint32_t b = tid; b < nb; b += kPartBlock) {
+    const uint32_t c = (s_cnt[b] + 7u) & ~7u;
+    uint32_t fit = 0, base = 0;
+    if (c) {
+      const uint64_t eb = atomicAdd(&fill[bucket_base + b], (unsigned long long)c);
+      fit = eb >= cap ? 0u : (uint32_t)(cap - eb < c ? cap - eb : c);
+      if (fit < c) overflow[bucket_base + b] = 1u;
+      base = (uint32_t)eb;
+    }
+    s_base[b] = base;
+    s_fit[b] = fit;
+  }
+  __syncthreads();
+  {
+    uint32_t st[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) st[j] = s_start[E[j] >> 16];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const uint32_t slot = st[j] + (E[j] & 0xFFFFu);
+      if (slot < (uint32_t)S::kSlots) s_rec[slot] = (Rec)O[j];  // the no-record bucket may run past
+    }
+  }
+  for (uint32_t b = tid; b < nb; b += kPartBlock) {
+    const uint32_t c = s_cnt[b], st = s_start[b], cp = (c + 7u) & ~7u;
+    for (uint32_t i = c; i < cp; ++i) s_rec[st + i] = (Rec)S::kPad;
+    for (uint32_t g = st >> 3; g < (st + cp) >> 3; ++g) s_gmap[g] = (typename S::GMap)b;
+  }
+  __syncthreads();
+  const uint32_t n_groups = s_start[nb] >> 3;
+#pragma unroll
+  for (int it = 0; it < S::kGroupIters; ++it) {
+    const uint32_t g = (uint32_t)tid + (uint32_t)it * kPartBlock;
+    if (g >= n_groups) break;
+    const uint32_t b = s_gmap[g];
+    const uint32_t j8 = g * 8 - s_start[b];
+    const uint64_t bg = bucket_base + b;
+    if (j8 < s_fit[b]) {
+      Rec *d = dst_rec + bg * cap + s_base[b] + j8;
+      const uint4 *src = reinterpret_cast<const uint4 *>(&s_rec[g * 8]);
+      if (WIDE) {
+        reinterpret_cast<uint4 *>(d)[0] = src[0];
+        reinterpret_cast<uint4 *>(d)[1] = src[1];
+      } else {
+        reinterpret_cast<uint4 *>(d)[0] = src[0];
+      }
+    } else {  // region full: count directly (exact, slow, rare)
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t o = (uint32_t)s_rec[g * 8 + i];
+        if (o != S::kPad) atomicAdd(&currents[(bg << bin_bits) | o], 1ULL);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// K1g: hash + partition for key modes KM 0/1/2 (see the file comment).
+// Lane = 16 consecutive positions of an 8192-position tile.
+template <int KM, bool CANON, bool WIDE>
+__global__ __launch_bounds__(kPartBlock) void k_part_gen(KmerInput in, int k, FastMod fm,
+                                                         GenPartArgs ga) {
+  using S = GenShape<WIDE>;
+  constexpr bool kRaw = !CANON;
+  __shared__ TileLds<kPartTile, kRaw> L;
+  __shared__ uint32_t s_cnt[S::kMaxB + 1];
+  __shared__ uint32_t s_start[S::kMaxB + 1];
+  __shared__ uint32_t s_base[S::kMaxB];
+  __shared__ uint32_t s_fit[S::kMaxB];
+  __shared__ __align__(16) typename S::Rec s_rec[S::kSlots];
+  __shared__ typename S::GMap s_gmap[S::kGroups];
+
+  const int tid = threadIdx.x;
+  const uint64_t tile = in.tile_base + blockIdx.x;
+  const uint64_t T0 = tile * (uint64_t)kPartTile;
+  const uint32_t nb = ga.n_buckets;
+  const int bb = ga.bin_bits;
+  const uint32_t omask = (uint32_t)((1ull << bb) - 1ull);
+  for (uint32_t b = tid; b <= nb; b += kPartBlock) s_cnt[b] = 0;
+  stage_tile<kPartTile, kPartBlock, kRaw>(L, in, tile, k);  // syncs
+
+  const int q0 = tid * kPer;
+  RecCursor rc;
+  rec_cursor_init<KM>(rc, in, T0 + (uint64_t)q0);
+  uint32_t E[kPer], O[kPer];
+#pragma unroll 2
+  for (int j = 0; j < kPer; ++j) {
+    const int q = q0 + j;
+    const bool ok = window_valid(L, T0, q, k, in.n_bases, in.pos_lo, in.pos_hi);
+    uint64_t h = 0;
+    if (ok) h = gen_hash<KM>(gen_key<KM, CANON>(L, in, q, T0 + (uint64_t)q, k, rc));
+    const uint32_t idx = (uint32_t)fastmod(h, fm);
+    const uint32_t b = ok ? (idx >> bb) : nb;
+    E[j] = (b << 16) | atomicAdd(&s_cnt[b], 1u);
+    O[j] = idx & omask;
+  }
+  sort_and_store<WIDE, kPer>(E, O, nb, s_cnt, s_start, s_base, s_fit, s_rec, s_gmap, ga.fill,
+                             ga.overflow, ga.cap, reinterpret_cast<typename S::Rec *>(ga.rec), 0,
+                             bb, ga.currents);
+}
+
+// K1s: one 8192-record tile of a coarse bucket (u32 offsets of 2^S bins) ->
+// its 2^(S-15) fine buckets (u16 offsets), the layout k_bucket_hist reads.
+__global__ __launch_bounds__(kPartBlock) void k_split(GenPartArgs ga, PartArgs pa) {
+  using S = GenShape<false>;
+  __shared__ uint32_t s_cnt[kMaxSplit + 1];
+  __shared__ uint32_t s_start[kMaxSplit + 1];
+  __shared__ uint32_t s_base[kMaxSplit];
+  __shared__ uint32_t s_fit[kMaxSplit];
+  __shared__ __align__(16) uint16_t s_rec[S::kSlots];
+  __shared__ S::GMap s_gmap[S::kGroups];
+  const int tid = threadIdx.x;
+  const uint32_t cb = blockIdx.y;
+  uint64_t n = ga.fill[cb];
+  if (n > ga.cap) n = ga.cap;
+  const uint64_t t0 = (uint64_t)blockIdx.x * kPartTile;
+  if (t0 >= n) return;  // uniform
+  const uint32_t F = 1u << (ga.bin_bits - kBinBits);
+  for (uint32_t f = tid; f <= F; f += kPartBlock) s_cnt[f] = 0;
+  __syncthreads();
+  const uint32_t *src = reinterpret_cast<const uint32_t *>(ga.rec) + (uint64_t)cb * ga.cap;
+  // 16 records per lane: four 16-B loads (the region is a multiple of 8 records
+  // and 64-record aligned; records past n are ignored)
+  uint4 v[4];
+  const uint64_t i0 = t0 + (uint64_t)tid * kPer;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const uint64_t i = i0 + 4 * t;
+    v[t] = i < n ? *reinterpret_cast<const uint4 *>(src + i) : make_uint4(~0u, ~0u, ~0u, ~0u);
+  }
+  uint32_t E[kPer], O[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const uint4 &w = v[j >> 2];
+    const uint32_t o = (j & 3) == 0 ? w.x : (j & 3) == 1 ? w.y : (j & 3) == 2 ? w.z : w.w;
+    const bool ok = o != 0xFFFFFFFFu && i0 + j < n;
+    const uint32_t f = ok ? (o >> kBinBits) : F;
+    E[j] = (f << 16) | atomicAdd(&s_cnt[f], 1u);
+    O[j] = o & (kBinsPerBucket - 1);
+  }
+  sort_and_store<false, kPer>(E, O, F, s_cnt, s_start, s_base, s_fit, s_rec, s_gmap, pa.fill,
+                              pa.overflow, pa.cap, pa.off, (uint64_t)cb * F, kBinBits,
+                              pa.currents);
+}
+
+// ---------------------------------------------------------------------------
+hipError_t launch_part_gen(const KmerInput &in, int k, int canonical, int km, uint64_t pool,
+                           const GenPartArgs &ga, int wide, hipStream_t s) {
+  if (!in.n_tiles) return hipSuccess;
+  if (pool == 0 || pool > (1ull << 31) || km < 0 || km > 2) return hipErrorInvalidValue;
+  if (wide ? (ga.n_buckets > (uint32_t)kWideMaxBuckets || ga.bin_bits < kBinBits ||
+              ga.bin_bits - kBinBits > kMaxSplitBits)
+           : (ga.n_buckets > (uint32_t)kMaxBuckets || ga.bin_bits != kBinBits))
+    return hipErrorInvalidValue;
+  if ((km == 0 && k > 32) || (km == 1 && (k <= 32 || k > 64)) || (km == 2 && k > 64) || k < 1)
+    return hipErrorInvalidValue;
+  const FastMod fm = make_fastmod(pool);
+  const dim3 g((unsigned)in.n_tiles), b(kPartBlock);
+#define NK_GEN(KM_, C_, W_) hipLaunchKernelGGL((k_part_gen<KM_, C_, W_>), g, b, 0, s, in, k, fm, ga)
+#define NK_GEN_W(KM_, C_) \
+  do {                    \
+    if (wide) NK_GEN(KM_, C_, true); else NK_GEN(KM_, C_, false); \
+  } while (0)
+  if (canonical) {
+    if (km == 0) NK_GEN_W(0, true);
+    else if (km == 1) NK_GEN_W(1, true);
+    else NK_GEN_W(2, true);
+  } else {
+    if (km == 0) NK_GEN_W(0, false);
+    else if (km == 1) NK_GEN_W(1, false);
+    else NK_GEN_W(2, false);
+  }
+#undef NK_GEN_W
+#undef NK_GEN
+  return hipGetLastError();
+}
+
+hipError_t launch_split(const GenPartArgs &ga, const PartArgs &pa, hipStream_t s) {
+  if (!ga.n_buckets) return hipSuccess;
+  if (ga.bin_bits < kBinBits || ga.bin_bits - kBinBits > kMaxSplitBits) return hipErrorInvalidValue;
+  const unsigned tx = (unsigned)((ga.cap + kPartTile - 1) / kPartTile);
+  hipLaunchKernelGGL(k_split, dim3(tx, ga.n_buckets), dim3(kPartBlock), 0, s, ga, pa);
+  return hipGetLastError();
+}
+
+}  // namespace nk

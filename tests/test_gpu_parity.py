@@ -5,6 +5,7 @@ Every comparison is bit-exact: u64 currents, u64 spike counts, f32 voltages
 "unique k-mers colliding".  Inputs are seeded synthetic records with N runs,
 lowercase bases, other IUPAC bytes, empty records and records shorter than k.
 """
+import contextlib
 import json
 import os
 import subprocess
@@ -250,6 +251,55 @@ def test_split_phase_two_shards_equals_whole():
     r = cbind.OracleCounter(21, 1.0, 0.95, 2, 1.0, 9001, True)
     r.process_parallel_arrays(bases, offs)
     assert_same(a, r)
+
+
+# ---- generic / wide partition (nk_wide.hip) ---------------------------------
+@contextlib.contextmanager
+def wide_bits(bits):
+    """Force the wide (coarse -> fine) partition with 2^bits-bin coarse buckets."""
+    old = os.environ.get("NK_WIDE_BITS")
+    os.environ["NK_WIDE_BITS"] = str(bits)
+    try:
+        yield
+    finally:
+        if old is None:
+            os.environ.pop("NK_WIDE_BITS", None)
+        else:
+            os.environ["NK_WIDE_BITS"] = old
+
+
+@pytest.mark.parametrize("canon", [True, False])
+@pytest.mark.parametrize("k,width,bits", [(21, 64, 16), (31, 64, 18), (33, 64, 17), (63, 64, 24),
+                                          (45, 128, 17), (64, 128, 19)])
+def test_wide_partition_forced(k, width, bits, canon):
+    # several coarse buckets, each split into 2..512 fine buckets; ragged
+    # records, N bytes and mixed case (compat keys near record starts)
+    bases, offs = ragged_records(total=400_000, n_rate=0.01, mixed_case=True, seed=300 + k,
+                                 repeats_per_mb=5000, motif_len=90)
+    with wide_bits(bits):
+        g, r = run_both(bases, offs, k, 700_001, canon, width=width)
+    assert_same(g, r)
+
+
+@pytest.mark.parametrize("k,width", [(31, 64), (40, 64), (63, 128)])
+def test_wide_partition_large_pool(k, width):
+    # past the 512-bucket narrow partition: coarse buckets of 2^17 bins
+    bases, offs = synth.make_records(1_500_000, 5, seed=77 + k, n_rate=0.001,
+                                     repeats_per_mb=8000, motif_len=100)
+    g, r = run_both(bases, offs, k, 20_000_003, True, width=width)
+    assert_same(g, r)
+
+
+@pytest.mark.parametrize("k", [31, 40])
+def test_wide_partition_streaming_ingest(tmp_path, k):
+    # per-batch histograms of the generic/wide partition over FASTQ chunks
+    reads, roffs = synth.make_reads(3000, 150, seed=k, n_rate=0.005, repeats_per_mb=40_000,
+                                    motif_len=50)
+    p = tmp_path / "w.fq"
+    synth.write_fastq(str(p), reads, roffs)
+    with wide_bits(17):
+        _ingest_check(str(p), k, 400_009, True, True, 50_000)
+    _ingest_check(str(p), k, 400_009, False, False, 50_000)  # Gen (k=40) / Part (k=31)
 
 
 # ---- --kmer-width=128 (SURVEY.md §8 A5: the build's true k <= 64 mode) -------
