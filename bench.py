@@ -139,7 +139,9 @@ def main() -> int:
             ctr.process_parallel_device(d_bases.data_ptr(), d_offs.data_ptr(), RECS, bases.size, s)
             return
         ctr.accumulate_device(d_bases.data_ptr(), d_offs.data_ptr(), RECS, bases.size, s)
-        nkdist.allreduce_currents_(cur_t)  # RCCL over xGMI: u64 currents (int64, same bits)
+        # RCCL over xGMI: the u64 currents (int32 on the wire while every rank's
+        # k-mers together stay below 2^31)
+        nkdist.allreduce_currents_(cur_t, total_kmers=world * args.bases)
         ctr.finalize(False, s)
         ptr, n = ctr.top_kmers_device()
         mine = (torch.as_tensor(_CAI(ptr, n), device=dev) if n

@@ -157,6 +157,30 @@ long nk_distinct_kmers(nk_counter *c);
  * for every neuron i < pool (n must equal pool_size).  Needs exact_counts. */
 int nk_copy_kmer_per_neuron(nk_counter *c, uint32_t *out, size_t n);
 
+/* Multi-GPU exact table (hash partition + all-to-all), after
+ * an accumulate/process call with exact_counts on every rank (one process per
+ * GPU; replaces the reference's single DashMap, src/spiking_hash.rs:27,
+ * 157-165):
+ *   nk_exact_partition  — this rank's (key, count) pairs grouped by owner rank
+ *                         (device buffers owned by the handle, valid until the
+ *                         next call; send_counts[r] = pairs for rank r, host)
+ *   <caller: all-to-all of the keys (u64) and counts (u32) with those splits>
+ *   nk_exact_adopt      — the received pairs become this rank's table (sorted,
+ *                         counts of equal keys summed, u32 wrapping) and
+ *                         kmer_per_neuron = the owned keys' contribution
+ *   <caller: allreduce(nk_device_kmer_per_neuron(c), pool_size u32, sum)>
+ *   nk_finalize         — the uniques column comes from kmer_per_neuron
+ * Afterwards nk_get_count(s) answers for the keys this rank owns
+ * (nk_exact_owner(key, world) == rank) and nk_distinct_kmers counts them; the
+ * caller routes queries (neurokmer_amd/dist.py).  COMPAT keys only. */
+uint32_t nk_exact_owner(uint64_t kmer, uint32_t world);
+int nk_exact_partition(nk_counter *c, uint32_t world, uint64_t *send_counts,
+                       const uint64_t **d_keys, const uint32_t **d_counts, void *stream);
+int nk_exact_adopt(nk_counter *c, const uint64_t *d_keys, const uint32_t *d_counts,
+                   size_t n, void *stream);
+/* Device pointer of kmer_per_neuron (u32, pool_size entries; exact_counts). */
+uint32_t *nk_device_kmer_per_neuron(nk_counter *c);
+
 /* EnergyTracker / accessors — src/models.rs:145-173, src/spiking_hash.rs:684-695 */
 uint64_t nk_total_spikes(const nk_counter *c);        /* energy.total_spikes() */
 double nk_energy_used(const nk_counter *c);           /* energy_used() */

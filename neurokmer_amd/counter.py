@@ -130,6 +130,22 @@ class SpikingKmerCounter:
     def merge_top_kmers(self, d_keys: int, n_keys: int, stream: int = 0) -> None:
         check(self._L.nk_merge_top_kmers(self._h, d_keys, n_keys, stream or None))
 
+    # multi-GPU exact table (include/neurokmer.h: nk_exact_partition / _adopt)
+    def exact_partition(self, world: int, stream: int = 0):
+        """-> (send_counts per rank, device ptr of the u64 keys, device ptr of
+        the u32 counts): this rank's table grouped by owner rank."""
+        cnt = (C.c_uint64 * world)()
+        kp, cp = C.c_void_p(), C.c_void_p()
+        check(self._L.nk_exact_partition(self._h, world, cnt, C.byref(kp), C.byref(cp),
+                                         stream or None))
+        return [int(x) for x in cnt], (kp.value or 0), (cp.value or 0)
+
+    def exact_adopt(self, d_keys: int, d_counts: int, n: int, stream: int = 0) -> None:
+        check(self._L.nk_exact_adopt(self._h, d_keys or None, d_counts or None, n, stream or None))
+
+    def device_kmer_per_neuron_ptr(self) -> int:
+        return self._L.nk_device_kmer_per_neuron(self._h) or 0
+
     def device_currents_ptr(self) -> int:
         return self._L.nk_device_currents(self._h) or 0
 

@@ -137,7 +137,11 @@ struct nk_counter {
   bool cur_fresh = true;     // currents are logically zero (lazy reset)
   // exact k-mer table (opts.exact_counts, nk_exact.h)
   DevBuf<uint64_t> x_keys, x_sorted, x_uniq, x_q;
-  DevBuf<uint32_t> x_cnt, x_tile_rec, kpn, x_out, x_pres;
+  DevBuf<uint32_t> x_cnt, x_tile_rec, kpn, x_out, x_pres, x_cs;
+  // multi-GPU exact table: pairs grouped by owner rank
+  DevBuf<uint64_t> xp_keys;
+  DevBuf<uint32_t> xp_cnt;
+  DevBuf<unsigned long long> xp_ctr;
   DevBuf<uint8_t> x_tmp;
   DevBuf<unsigned long long> x_n;  // [0] keys of the last input, [1] distinct keys
   bool exact_built = false;        // the sorted table holds the last process/accumulate input
@@ -148,6 +152,7 @@ struct nk_counter {
   uint64_t d_cap = 0, d_bound = 0;  // delta capacity, upper bound of its distinct keys
   bool d_dirty = true;              // delta must be cleared before use
   bool kpn_valid = false;           // kpn holds kmer_per_neuron (else it is all zero)
+  bool kpn_global = false;          // table adopted across ranks: nk_finalize's uniques from kpn
   // top-N selection fused into the LIF kernel (TopFuse)
   DevBuf<uint64_t> bcand;
   DevBuf<uint32_t> bcnt;
@@ -196,6 +201,7 @@ static int zero_state_on(nk_counter *c, hipStream_t) {
   c->state_fresh = true;
   c->cur_fresh = true;
   c->exact_built = false;  // a fresh counter's `counts` is empty
+  c->kpn_global = false;
   c->d_dirty = true;
   c->d_bound = 0;
   c->kpn_valid = false;
@@ -399,6 +405,7 @@ static int build_exact(nk_counter *c, const KmerInput &in0, hipStream_t s) {
   HIPCHK(exact_kpn(c->x_uniq.p, c->x_n.p + 1, n, c->pool, c->kpn.p, s));
   c->exact_built = true;
   c->kpn_valid = true;
+  c->kpn_global = false;
   c->d_dirty = true;  // counts.clear() (src/spiking_hash.rs:157,426)
   c->d_bound = 0;
   return NK_OK;
@@ -858,7 +865,9 @@ int nk_finalize(nk_counter *c, int streaming, void *stream) {
   (void)hipSetDevice(c->device);
   hipStream_t s = pick_stream(c, stream);
   HIPCHK(mark(c, 7, s));
-  int rc = lif_top_uniques(c, streaming, false, s);
+  // after nk_exact_adopt (+ the caller's all-reduce) kmer_per_neuron is global:
+  // the uniques column comes from it; else from this shard's k-mers
+  int rc = lif_top_uniques(c, streaming, c->opts.exact_counts && c->exact_built && c->kpn_global, s);
   if (rc) return rc;
   c->top_valid = true;
   // an accumulate on this handle precedes: report its stages too
@@ -1455,6 +1464,86 @@ long nk_distinct_kmers(nk_counter *c) {
   // meta[1]: keys process_sequence added that the sorted table did not hold
   // (k_seq_accumulate; the ~0 key included)
   return (long)(n + m[1]);
+}
+
+uint32_t nk_exact_owner(uint64_t kmer, uint32_t world) { return world ? exact_owner(kmer, world) : 0; }
+
+int nk_exact_partition(nk_counter *c, uint32_t world, uint64_t *send_counts,
+                       const uint64_t **d_keys, const uint32_t **d_counts, void *stream) {
+  int rc = need_exact(c);
+  if (rc) return rc;
+  if (!world || world > 4096) return fail(NK_E_INVALID, "world must be in 1..4096");
+  if (!send_counts || !d_keys || !d_counts) return fail(NK_E_INVALID, "null argument");
+  if (!c->exact_built) return fail(NK_E_INVALID, "no exact table: run a process/accumulate call first");
+  if (c->d_bound)
+    return fail(NK_E_UNSUPPORTED, "process_sequence additions are not partitioned across ranks");
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  unsigned long long n = 0;
+  HIPCHK(hipMemcpyAsync(&n, c->x_n.p + 1, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if ((rc = c->xp_keys.ensure(std::max<uint64_t>(n, 1))) || (rc = c->xp_cnt.ensure(std::max<uint64_t>(n, 1))) ||
+      (rc = c->xp_ctr.ensure(world)))
+    return rc;
+  std::vector<unsigned long long> cnt(world, 0);
+  if (n) {
+    HIPCHK(hipMemsetAsync(c->xp_ctr.p, 0, world * 8, s));
+    HIPCHK(exact_owner_hist(c->x_uniq.p, c->x_n.p + 1, n, world, c->xp_ctr.p, s));
+    HIPCHK(hipMemcpyAsync(cnt.data(), c->xp_ctr.p, world * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::vector<unsigned long long> cur(world);
+    unsigned long long run = 0;
+    for (uint32_t r = 0; r < world; ++r) {
+      cur[r] = run;
+      run += cnt[r];
+    }
+    HIPCHK(hipMemcpyAsync(c->xp_ctr.p, cur.data(), world * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(exact_owner_scatter(c->x_uniq.p, c->x_cnt.p, c->x_n.p + 1, n, world, c->xp_ctr.p,
+                               c->xp_keys.p, c->xp_cnt.p, s));
+    HIPCHK(hipStreamSynchronize(s));  // cur[] is host memory the copy reads
+  }
+  for (uint32_t r = 0; r < world; ++r) send_counts[r] = cnt[r];
+  *d_keys = c->xp_keys.p;
+  *d_counts = c->xp_cnt.p;
+  return NK_OK;
+}
+
+int nk_exact_adopt(nk_counter *c, const uint64_t *d_keys, const uint32_t *d_counts, size_t n,
+                   void *stream) {
+  int rc = need_exact(c);
+  if (rc) return rc;
+  if (n && (!d_keys || !d_counts)) return fail(NK_E_INVALID, "null argument");
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  const int end_bit = c->k <= 32 ? (int)(2 * c->k) : 64;
+  const uint64_t nn = std::max<uint64_t>(n, 1);
+  if ((rc = c->x_n.ensure(2)) || (rc = c->x_sorted.ensure(nn)) || (rc = c->x_cs.ensure(nn)) ||
+      (rc = c->x_uniq.ensure(nn)) || (rc = c->x_cnt.ensure(nn)) || (rc = c->kpn.ensure(c->pool)) ||
+      (rc = c->x_tmp.ensure(exact_merge_temp_bytes(nn, end_bit))))
+    return rc;
+  HIPCHK(exact_merge_pairs(d_keys, d_counts, n, end_bit, c->x_sorted.p, c->x_cs.p, c->x_uniq.p,
+                           c->x_cnt.p, c->x_n.p + 1, c->x_tmp.p, c->x_tmp.n, s));
+  if (c->pool) {
+    HIPCHK(hipMemsetAsync(c->kpn.p, 0, c->pool * 4, s));
+    HIPCHK(exact_kpn(c->x_uniq.p, c->x_n.p + 1, n, c->pool, c->kpn.p, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));  // the caller may free the received buffers
+  c->exact_built = true;
+  c->kpn_valid = true;
+  c->kpn_global = true;
+  c->d_dirty = true;
+  c->d_bound = 0;
+  return NK_OK;
+}
+
+uint32_t *nk_device_kmer_per_neuron(nk_counter *c) {
+  if (!c || !c->opts.exact_counts || !c->pool) return nullptr;
+  if (!c->kpn_valid) {
+    (void)hipSetDevice(c->device);
+    if (c->kpn.ensure(c->pool) || hipMemset(c->kpn.p, 0, c->pool * 4) != hipSuccess) return nullptr;
+    c->kpn_valid = true;
+  }
+  return c->kpn.p;
 }
 
 int nk_copy_kmer_per_neuron(nk_counter *c, uint32_t *out, size_t n) {

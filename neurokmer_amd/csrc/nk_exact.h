@@ -64,6 +64,36 @@ hipError_t exact_lookup2(const uint64_t *uniq, const uint32_t *cnt,
                          const unsigned long long *n_uniq, const DeltaArgs &d, const uint64_t *q,
                          size_t nq, uint32_t *out, uint32_t *present, hipStream_t s);
 
+// ---- multi-GPU table (hash partition + all-to-all) --------------------------
+// Owner rank of a key: every rank computes the same owner without
+// communication, so each distinct key ends up in exactly one rank's table and
+// the per-rank kmer_per_neuron contributions add up (all-reduce) to the
+// global one.
+__host__ __device__ inline uint32_t exact_owner(uint64_t key, uint32_t world) {
+  uint64_t x = key + 0x9E3779B97F4A7C15ull;  // splitmix64 finaliser
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return (uint32_t)(((x >> 32) * (uint64_t)world) >> 32);
+}
+// per-owner key counts of the table (cnt zeroed by the caller, world <= 4096)
+hipError_t exact_owner_hist(const uint64_t *uniq, const unsigned long long *n_uniq, size_t max_n,
+                            uint32_t world, unsigned long long *cnt, hipStream_t s);
+// (key, count) pairs grouped by owner: cursor[r] = the start of owner r's range
+// on entry (advanced by the kernel)
+hipError_t exact_owner_scatter(const uint64_t *uniq, const uint32_t *cnt,
+                               const unsigned long long *n_uniq, size_t max_n, uint32_t world,
+                               unsigned long long *cursor, uint64_t *out_keys, uint32_t *out_cnt,
+                               hipStream_t s);
+// scratch bytes for exact_merge_pairs over n pairs
+size_t exact_merge_temp_bytes(size_t n, int end_bit);
+// sort (key, count) pairs and sum the counts of equal keys (u32, wrapping):
+// sorted unique keys + counts, *n_uniq (device)
+hipError_t exact_merge_pairs(const uint64_t *keys, const uint32_t *cnt, size_t n, int end_bit,
+                             uint64_t *keys_sorted, uint32_t *cnt_sorted, uint64_t *uniq,
+                             uint32_t *uniq_cnt, unsigned long long *n_uniq, void *tmp,
+                             size_t tmp_bytes, hipStream_t s);
+
 // uniques column of the top rows from kmer_per_neuron
 hipError_t exact_top_uniques(const TopCand *cand, uint32_t m, const uint32_t *kpn, uint32_t *uniq,
                              hipStream_t s);

@@ -4,6 +4,7 @@
 #include <cstring>  // before rocprim: its texture_cache_iterator uses memset
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_reduce_by_key.hpp>
 #include <rocprim/device/device_run_length_encode.hpp>
 
 #include "nk_device.h"
@@ -344,6 +345,108 @@ hipError_t exact_sort_rle(uint64_t *keys, uint64_t *keys_sorted, size_t n, int e
   tb = tmp_bytes;
   return rocprim::run_length_encode(tmp, tb, (const uint64_t *)keys_sorted, n, uniq, cnt, n_uniq,
                                     s);
+}
+
+// ---- multi-GPU table ---------------------------------------------------------
+constexpr int kOwnerMax = 4096;
+constexpr int kOwnerPer = 16;  // entries per thread (4096 per 256-thread block)
+
+__global__ __launch_bounds__(256) void k_owner_hist(const uint64_t *__restrict__ uniq,
+                                                    const unsigned long long *__restrict__ n_uniq,
+                                                    uint32_t world,
+                                                    unsigned long long *__restrict__ cnt) {
+  __shared__ uint32_t h[kOwnerMax];
+  for (uint32_t r = threadIdx.x; r < world; r += 256) h[r] = 0;
+  __syncthreads();
+  const uint64_t n = *n_uniq;
+  const uint64_t base = (uint64_t)blockIdx.x * 256 * kOwnerPer;
+  for (int j = 0; j < kOwnerPer; ++j) {
+    const uint64_t i = base + (uint64_t)j * 256 + threadIdx.x;
+    if (i < n) atomicAdd(&h[exact_owner(uniq[i], world)], 1u);
+  }
+  __syncthreads();
+  for (uint32_t r = threadIdx.x; r < world; r += 256)
+    if (h[r]) atomicAdd(&cnt[r], (unsigned long long)h[r]);
+}
+
+// block-aggregated scatter: LDS ranks per owner, one global reservation per
+// (block, owner)
+__global__ __launch_bounds__(256) void k_owner_scatter(const uint64_t *__restrict__ uniq,
+                                                       const uint32_t *__restrict__ cnt,
+                                                       const unsigned long long *__restrict__ n_uniq,
+                                                       uint32_t world,
+                                                       unsigned long long *__restrict__ cursor,
+                                                       uint64_t *__restrict__ out_keys,
+                                                       uint32_t *__restrict__ out_cnt) {
+  __shared__ uint32_t h[kOwnerMax];
+  __shared__ unsigned long long b0[kOwnerMax];
+  for (uint32_t r = threadIdx.x; r < world; r += 256) h[r] = 0;
+  __syncthreads();
+  const uint64_t n = *n_uniq;
+  const uint64_t base = (uint64_t)blockIdx.x * 256 * kOwnerPer;
+  uint32_t own[kOwnerPer], rk[kOwnerPer];
+  for (int j = 0; j < kOwnerPer; ++j) {
+    const uint64_t i = base + (uint64_t)j * 256 + threadIdx.x;
+    own[j] = i < n ? exact_owner(uniq[i], world) : world;
+    rk[j] = i < n ? atomicAdd(&h[own[j]], 1u) : 0u;
+  }
+  __syncthreads();
+  for (uint32_t r = threadIdx.x; r < world; r += 256)
+    b0[r] = h[r] ? atomicAdd(&cursor[r], (unsigned long long)h[r]) : 0ull;
+  __syncthreads();
+  for (int j = 0; j < kOwnerPer; ++j) {
+    const uint64_t i = base + (uint64_t)j * 256 + threadIdx.x;
+    if (i >= n) continue;
+    const uint64_t at = b0[own[j]] + rk[j];
+    out_keys[at] = uniq[i];
+    out_cnt[at] = cnt[i];
+  }
+}
+
+hipError_t exact_owner_hist(const uint64_t *uniq, const unsigned long long *n_uniq, size_t max_n,
+                            uint32_t world, unsigned long long *cnt, hipStream_t s) {
+  if (!max_n) return hipSuccess;
+  if (!world || world > (uint32_t)kOwnerMax) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_owner_hist, dim3(grid_for(max_n, 256 * kOwnerPer)), dim3(256), 0, s, uniq,
+                     n_uniq, world, cnt);
+  return hipGetLastError();
+}
+
+hipError_t exact_owner_scatter(const uint64_t *uniq, const uint32_t *cnt,
+                               const unsigned long long *n_uniq, size_t max_n, uint32_t world,
+                               unsigned long long *cursor, uint64_t *out_keys, uint32_t *out_cnt,
+                               hipStream_t s) {
+  if (!max_n) return hipSuccess;
+  if (!world || world > (uint32_t)kOwnerMax) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_owner_scatter, dim3(grid_for(max_n, 256 * kOwnerPer)), dim3(256), 0, s,
+                     uniq, cnt, n_uniq, world, cursor, out_keys, out_cnt);
+  return hipGetLastError();
+}
+
+size_t exact_merge_temp_bytes(size_t n, int end_bit) {
+  size_t a = 0, b = 0;
+  (void)rocprim::radix_sort_pairs(nullptr, a, (const uint64_t *)nullptr, (uint64_t *)nullptr,
+                                  (const uint32_t *)nullptr, (uint32_t *)nullptr, n, 0, end_bit);
+  (void)rocprim::reduce_by_key(nullptr, b, (const uint64_t *)nullptr, (const uint32_t *)nullptr, n,
+                               (uint64_t *)nullptr, (uint32_t *)nullptr,
+                               (unsigned long long *)nullptr, rocprim::plus<uint32_t>(),
+                               rocprim::equal_to<uint64_t>());
+  return (a > b ? a : b) + 256;
+}
+
+hipError_t exact_merge_pairs(const uint64_t *keys, const uint32_t *cnt, size_t n, int end_bit,
+                             uint64_t *keys_sorted, uint32_t *cnt_sorted, uint64_t *uniq,
+                             uint32_t *uniq_cnt, unsigned long long *n_uniq, void *tmp,
+                             size_t tmp_bytes, hipStream_t s) {
+  if (!n) return hipMemsetAsync(n_uniq, 0, sizeof(unsigned long long), s);
+  size_t tb = tmp_bytes;
+  hipError_t e = rocprim::radix_sort_pairs(tmp, tb, keys, keys_sorted, cnt, cnt_sorted, n, 0,
+                                           end_bit, s);
+  if (e != hipSuccess) return e;
+  tb = tmp_bytes;
+  return rocprim::reduce_by_key(tmp, tb, (const uint64_t *)keys_sorted, (const uint32_t *)cnt_sorted,
+                                n, uniq, uniq_cnt, n_uniq, rocprim::plus<uint32_t>(),
+                                rocprim::equal_to<uint64_t>(), s);
 }
 
 hipError_t exact_kpn(const uint64_t *uniq, const unsigned long long *n_uniq, size_t max_n,

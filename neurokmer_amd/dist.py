@@ -11,6 +11,12 @@ its window (k <= 32), and currents are a commutative u64 sum.  So:
     of the top-N neurons: each rank contributes its (small) distinct key list,
     all-gathered and merged (nk_merge_top_kmers).
 
+With the exact k-mer table (nk_opts.exact_counts) the
+shards' tables are combined by hash partition + all-to-all
+(exchange_exact_table): every distinct key goes to one owner rank
+(exact_owner), owners merge the counts, and the per-rank kmer_per_neuron
+contributions are all-reduced; get_counts() routes queries to the owners.
+
 shard_records() splits one input into world shards at record boundaries and,
 where a record is longer than a shard, inside the record with a k-1 base halo,
 so every window is counted by exactly one rank.  k > 32 (compat mode) keeps
@@ -60,25 +66,131 @@ def shard_records(offsets: np.ndarray, world: int, k: int) -> List[Tuple[int, in
     return out
 
 
-def allreduce_currents_(t, group=None) -> None:
-    """In-place sum of a u64 currents vector held as int64 (same bits mod 2^64)."""
+def allreduce_currents_(t, group=None, total_kmers=None) -> None:
+    """In-place sum of a u64 currents vector held as int64 (same bits mod 2^64).
+
+    total_kmers: an upper bound on the k-mers of ALL ranks together, the same
+    on every rank.  Below 2^31 no neuron's summed current can leave int32, so
+    the vector crosses xGMI as int32 (half the bytes of the ring all-reduce)."""
+    import torch
     import torch.distributed as dist
+    if total_kmers is not None and 0 <= total_kmers < (1 << 31):
+        n = t.to(torch.int32)
+        dist.all_reduce(n, op=dist.ReduceOp.SUM, group=group)
+        t.copy_(n)
+        return
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
 
 
 def gather_union(keys, group=None):
     """All-gather variable-length int64 key lists -> one concatenated tensor
-    (the merge deduplicates)."""
+    (the merge deduplicates).  Two collectives into single tensors and one
+    host synchronisation (the sizes)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     n = torch.tensor([keys.numel()], dtype=torch.int64, device=keys.device)
-    sizes = [torch.zeros(1, dtype=torch.int64, device=keys.device) for _ in range(world)]
-    dist.all_gather(sizes, n, group=group)
-    sizes = [int(s.item()) for s in sizes]
-    mx = max(sizes) if sizes else 0
-    pad = torch.full((max(mx, 1),), -1, dtype=torch.int64, device=keys.device)
+    sizes_t = torch.empty(world, dtype=torch.int64, device=keys.device)
+    dist.all_gather_into_tensor(sizes_t, n, group=group)
+    sizes = sizes_t.tolist()
+    width = max(max(sizes), 1)
+    pad = torch.full((width,), -1, dtype=torch.int64, device=keys.device)
     pad[:keys.numel()] = keys
-    parts = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(parts, pad, group=group)
-    return torch.cat([p[:s] for p, s in zip(parts, sizes)])
+    parts = torch.empty(world * width, dtype=torch.int64, device=keys.device)
+    dist.all_gather_into_tensor(parts, pad, group=group)
+    return torch.cat([parts[r * width:r * width + s] for r, s in enumerate(sizes)])
+
+
+class _CAI:
+    """Wraps a raw device pointer for torch.as_tensor (no copy)."""
+
+    def __init__(self, ptr: int, n: int, typestr: str):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr,
+                                         "data": (ptr, False), "version": 3}
+
+
+def _dev_view(ptr: int, n: int, typestr: str, dev):
+    import torch
+    if not n or not ptr:
+        return torch.empty(0, dtype=torch.int64 if typestr == "<i8" else torch.int32, device=dev)
+    return torch.as_tensor(_CAI(ptr, n, typestr), device=dev)
+
+
+def exact_owner(keys: np.ndarray, world: int) -> np.ndarray:
+    """Owner rank of each u64 key (the library's nk_exact_owner: splitmix64
+    finaliser, then a multiply-shift into [0, world))."""
+    x = np.asarray(keys, dtype=np.uint64) + np.uint64(0x9E3779B97F4A7C15)
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    x ^= x >> np.uint64(31)
+    return (((x >> np.uint64(32)) * np.uint64(world)) >> np.uint64(32)).astype(np.int64)
+
+
+def _all_to_all(out, inp, out_splits=None, in_splits=None, group=None):
+    """all_to_all_single; with gloo (CPU rehearsals of the multi-GPU path) the
+    device tensors are staged through host memory."""
+    import torch.distributed as dist
+    if dist.get_backend(group) == "gloo" and out.is_cuda:
+        o = out.cpu()
+        dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=group)
+        out.copy_(o)
+        return
+    dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+
+
+def exchange_exact_table(ctr, group=None) -> None:
+    """After every rank's accumulate (exact_counts on): hash partition + all-to-all
+    of the (key, count) pairs, merge on the owners, all-reduce kmer_per_neuron.
+    Then ctr.finalize() takes the uniques column from the global kmer_per_neuron."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    stream = torch.cuda.current_stream().cuda_stream
+    send, kp, cp = ctr.exact_partition(world, stream)
+    tot = sum(send)
+    send_k = _dev_view(kp, tot, "<i8", dev)
+    send_c = _dev_view(cp, tot, "<i4", dev)
+    sc = torch.tensor(send, dtype=torch.int64, device=dev)
+    rcnt = torch.empty_like(sc)
+    _all_to_all(rcnt, sc, group=group)
+    recv = rcnt.tolist()
+    rk = torch.empty(sum(recv), dtype=torch.int64, device=dev)
+    rc = torch.empty(sum(recv), dtype=torch.int32, device=dev)
+    _all_to_all(rk, send_k, recv, send, group=group)
+    _all_to_all(rc, send_c, recv, send, group=group)
+    ctr.exact_adopt(rk.data_ptr(), rc.data_ptr(), rk.numel(), stream)
+    kpn = _dev_view(ctr.device_kmer_per_neuron_ptr(), ctr.pool_size, "<i4", dev)
+    dist.all_reduce(kpn, op=dist.ReduceOp.SUM, group=group)
+
+
+def get_counts(ctr, keys: np.ndarray, group=None):
+    """get_count for this rank's query keys against the distributed table:
+    queries travel to their owners and the answers come back.  Collective:
+    every rank calls it (possibly with no keys).  -> (counts u32, present bool)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    keys = np.asarray(keys, dtype=np.uint64)
+    own = exact_owner(keys, world)
+    order = np.argsort(own, kind="stable")
+    send = np.bincount(own, minlength=world).tolist()
+    q = torch.from_numpy(keys[order].view(np.int64).copy()).to(dev)
+    rcnt = torch.empty(world, dtype=torch.int64, device=dev)
+    _all_to_all(rcnt, torch.tensor(send, dtype=torch.int64, device=dev), group=group)
+    recv = rcnt.tolist()
+    rq = torch.empty(sum(recv), dtype=torch.int64, device=dev)
+    _all_to_all(rq, q, recv, send, group=group)
+    mine = rq.cpu().numpy().view(np.uint64)
+    cnt, pres = ctr.get_counts(mine) if mine.size else (np.zeros(0, np.uint32),
+                                                       np.zeros(0, bool))
+    ans = np.asarray(cnt, dtype=np.int64) | (np.asarray(pres, dtype=np.int64) << 32)
+    back = torch.empty(keys.size, dtype=torch.int64, device=dev)
+    _all_to_all(back, torch.from_numpy(ans).to(dev), send, recv, group=group)
+    b = back.cpu().numpy()
+    counts = np.empty(keys.size, np.uint32)
+    present = np.empty(keys.size, bool)
+    counts[order] = (b & 0xFFFFFFFF).astype(np.uint32)
+    present[order] = (b >> 32) != 0
+    return counts, present

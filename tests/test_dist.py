@@ -38,7 +38,10 @@ def _worker(rank, world, port, k, pool, q):
         ctr = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, True)
         ctr.process_parallel_arrays(shard, soffs, 1)
         cur = torch.from_numpy(ctr.currents().view(np.int64).copy())
+        cur32 = cur.clone()
         nkdist.allreduce_currents_(cur)
+        nkdist.allreduce_currents_(cur32, total_kmers=int(offs[-1]))  # int32 on the wire
+        assert torch.equal(cur, cur32)
         # identical LIF + top-N on every rank: reuse the oracle on the summed
         # currents by comparing against a whole-input run below
         whole = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, True)
@@ -99,3 +102,42 @@ def test_shard_records_cover_every_window_once(world, k):
             got += [int(x) for x in cbind.kmer_keys(sh[int(so[i]):int(so[i + 1])].tobytes(), k,
                                                     False)]
     assert sorted(got) == sorted(want)
+
+
+def test_exact_table_partition_protocol():
+    """§8f-1 across ranks, the arithmetic of the protocol on the C restatement:
+    per-shard (key, count) tables, partitioned by exact_owner, merged on the
+    owners = the whole input's table; the owners' per-neuron distinct counts
+    add up to the whole input's kmer_per_neuron."""
+    from oracle import cbind
+    k, pool, world = 19, 4001, 3
+    bases, offs = synth.make_records(60_000, 5, seed=9, repeats_per_mb=20000, motif_len=40,
+                                     n_rate=0.003)
+
+    def table(b, o):
+        d = {}
+        for i in range(o.size - 1):
+            for key in cbind.kmer_keys(b[int(o[i]):int(o[i + 1])].tobytes(), k, True):
+                d[int(key)] = d.get(int(key), 0) + 1
+        return d
+
+    whole = table(bases, offs)
+    owned = [dict() for _ in range(world)]
+    for lo, hi, so in nkdist.shard_records(offs, world, k):
+        t = table(bases[lo:hi], so)
+        keys = np.array(sorted(t), dtype=np.uint64)
+        for key, r in zip(keys.tolist(), nkdist.exact_owner(keys, world).tolist()):
+            owned[r][key] = owned[r].get(key, 0) + t[key]
+    merged = {}
+    for r in range(world):
+        assert not set(merged) & set(owned[r])  # each key has one owner
+        merged.update(owned[r])
+    assert merged == whole
+    kpn = np.zeros(pool, np.int64)
+    for r in range(world):
+        for key in owned[r]:
+            kpn[int(cbind.lib().nko_map_kmer(key, pool))] += 1
+    ref = np.zeros(pool, np.int64)
+    for key in whole:
+        ref[int(cbind.lib().nko_map_kmer(key, pool))] += 1
+    assert np.array_equal(kpn, ref)

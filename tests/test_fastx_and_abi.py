@@ -104,6 +104,23 @@ def test_library_exports_every_header_symbol():
         assert re.search(rf"\bT {n}$", nm, re.M), n
 
 
+def test_exact_owner_matches_python_restatement():
+    # the owner rank of a key (multi-GPU exact table) is pure host arithmetic:
+    # the library and neurokmer_amd.dist.exact_owner must agree bit for bit
+    import numpy as np
+    from neurokmer_amd.dist import exact_owner
+    L = _lib.load()
+    rng = np.random.default_rng(5)
+    keys = np.concatenate([rng.integers(0, 2**63, 2000, dtype=np.uint64) * np.uint64(2) + 1,
+                           np.array([0, 1, 2**64 - 1, 2**63], np.uint64)])
+    for world in (1, 2, 3, 8, 64, 4096):
+        own = exact_owner(keys, world)
+        assert own.min() >= 0 and own.max() < world
+        assert [L.nk_exact_owner(int(x), world) for x in keys[:300]] == own[:300].tolist()
+    own8 = exact_owner(keys, 8)
+    assert np.bincount(own8, minlength=8).min() > 150  # spread over the ranks
+
+
 def test_no_cpu_fallback_without_gpu():
     import torch
     if torch.cuda.is_available():

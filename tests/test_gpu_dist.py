@@ -1,0 +1,100 @@
+"""Multi-process rehearsal of the multi-GPU protocol on the HIP path (two
+ranks on the one GPU of the test box, gloo for the collectives): shards,
+all-reduce of the currents, the exact table exchanged by hash partition +
+all-to-all (neurokmer_amd/dist.py), finalize, routed get_counts -> identical
+to the whole input on the C restatement.  The driver's 8-GPU runs use the
+same code with RCCL.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+K, POOL = 25, 7001
+
+
+def _input():
+    from neurokmer_amd import synth
+    return synth.make_records(400_000, 5, seed=44, repeats_per_mb=20000, motif_len=80,
+                              n_rate=0.002)
+
+
+class _CAI:
+    def __init__(self, ptr, n, typestr="<i8"):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr,
+                                         "data": (ptr, False), "version": 3}
+
+
+def _rank(rank, world, port, keys, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from neurokmer_amd import SpikingKmerCounter
+        from neurokmer_amd import dist as nkdist
+        bases, offs = _input()
+        lo, hi, so = nkdist.shard_records(offs, world, K)[rank]
+        b = bases[lo:hi]
+        d_b = torch.from_numpy(np.concatenate([b, np.zeros(16, np.uint8)])).cuda()
+        d_o = torch.from_numpy(so.astype(np.uint64).view(np.int64)).cuda()
+        torch.cuda.synchronize()
+        c = SpikingKmerCounter(K, 1.0, 0.95, 2, 1.0, POOL, True, exact_counts=True)
+        c.accumulate_device(d_b.data_ptr(), d_o.data_ptr(), so.size - 1, b.size)
+        cur = torch.as_tensor(_CAI(c.device_currents_ptr(), POOL), device="cuda")
+        nkdist.allreduce_currents_(cur, total_kmers=int(offs[-1]))
+        nkdist.exchange_exact_table(c)
+        torch.cuda.synchronize()
+        c.finalize(False)
+        mine = keys[rank::world]
+        cnt, pres = nkdist.get_counts(c, mine)
+        q.put((rank, c.top_abundant_neurons(20), c.distinct_kmers(), c.energy.total_spikes(),
+               mine.tolist(), cnt.tolist(), pres.tolist(), c.kmer_per_neuron().tolist()))
+        c.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_exact_table_and_uniques():
+    import torch.multiprocessing as mp
+    from oracle import cbind
+    bases, offs = _input()
+    ref = cbind.OracleCounter(K, 1.0, 0.95, 2, 1.0, POOL, True)
+    ref.process_parallel_arrays(bases, offs)
+    keys = np.unique(np.concatenate([cbind.kmer_keys(bases[int(offs[i]):int(offs[i + 1])]
+                                                     .tobytes(), K, True) for i in range(2)]))
+    keys = np.concatenate([keys[::97], np.array([3, 2**45 + 11], np.uint64)])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, keys, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    top = ref.top_abundant_neurons(20)
+    kpn = ref.kmer_per_neuron().tolist()
+    for rank, t, _, spikes, mine, cnt, pres, kp in res:
+        assert t == top
+        assert spikes == ref.total_spikes
+        assert kp == kpn
+        exp = [ref.get_count(int(x)) for x in mine]
+        assert pres == [x is not None for x in exp]
+        assert [c for c, p in zip(cnt, pres) if p] == [x for x in exp if x is not None]
+    assert sum(r[2] for r in res) == ref.distinct_kmers()

@@ -253,6 +253,69 @@ def test_split_phase_two_shards_equals_whole():
     assert_same(a, r)
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_exact_table_across_shards(world):
+    """Multi-GPU exact table on one device: `world` counters (ranks) with the
+    table on, currents summed, tables exchanged by owner (what the all-to-all
+    does), kmer_per_neuron summed (all-reduce) -> counts, distinct k-mers,
+    kmer_per_neuron and the top rows' uniques of the whole input."""
+    from neurokmer_amd import dist as nkdist
+    k, pool = 23, 6007
+    bases, offs = synth.make_records(300_000, 6, seed=31, repeats_per_mb=20000, motif_len=70,
+                                     n_rate=0.002)
+    ranks, keep = [], []
+    for lo, hi, so in nkdist.shard_records(offs, world, k):
+        b = bases[lo:hi]
+        d_b = torch.from_numpy(np.concatenate([b, np.zeros(16, np.uint8)])).cuda()
+        d_o = torch.from_numpy(so.astype(np.uint64).view(np.int64)).cuda()
+        c = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, True, exact_counts=True)
+        torch.cuda.synchronize()
+        c.accumulate_device(d_b.data_ptr(), d_o.data_ptr(), so.size - 1, b.size)
+        ranks.append(c)
+        keep += [d_b, d_o]
+    tot = sum(c.currents() for c in ranks)
+    t = torch.from_numpy(tot.view(np.int64)).cuda()
+    for c in ranks:
+        torch.as_tensor(_CAI(c.device_currents_ptr(), pool), device="cuda").copy_(t)
+    parts = []
+    for c in ranks:  # nk_exact_partition on every rank
+        cnt, kp, cp = c.exact_partition(world)
+        n = sum(cnt)
+        kk = torch.as_tensor(_CAI(kp, n), device="cuda").clone() if n else \
+            torch.zeros(0, dtype=torch.int64, device="cuda")
+        cc = torch.as_tensor(_CAI(cp, n, "<i4"), device="cuda").clone() if n else \
+            torch.zeros(0, dtype=torch.int32, device="cuda")
+        parts.append((np.concatenate([[0], np.cumsum(cnt)]), kk, cc))
+    for r, c in enumerate(ranks):  # all-to-all: rank r takes every source's slice r
+        rk = torch.cat([kk[int(o[r]):int(o[r + 1])] for o, kk, _ in parts])
+        rc = torch.cat([cc[int(o[r]):int(o[r + 1])] for o, _, cc in parts])
+        torch.cuda.synchronize()
+        c.exact_adopt(rk.data_ptr(), rc.data_ptr(), rk.numel())
+    kpn = sum(c.kmer_per_neuron().astype(np.int64) for c in ranks)
+    kt = torch.from_numpy(kpn.astype(np.int32)).cuda()
+    for c in ranks:  # all-reduce of kmer_per_neuron
+        torch.as_tensor(_CAI(c.device_kmer_per_neuron_ptr(), pool, "<i4"), device="cuda").copy_(kt)
+        torch.cuda.synchronize()
+        c.finalize(False)
+    r = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, True)
+    r.process_parallel_arrays(bases, offs)
+    assert_same(ranks[0], r)
+    np.testing.assert_array_equal(kpn, r.kmer_per_neuron())
+    assert sum(c.distinct_kmers() for c in ranks) == r.distinct_kmers()
+    keys = np.unique(np.concatenate([cbind.kmer_keys(bases[int(offs[i]):int(offs[i + 1])].tobytes(),
+                                                     k, True) for i in range(3)]))[:3000]
+    keys = np.concatenate([keys, np.array([12345, 2**40 + 7], np.uint64)])  # absent keys too
+    own = nkdist.exact_owner(keys, world)
+    got_c = np.zeros(keys.size, np.uint32)
+    got_p = np.zeros(keys.size, bool)
+    for rr, c in enumerate(ranks):
+        m = own == rr
+        got_c[m], got_p[m] = c.get_counts(keys[m])
+    ref = [r.get_count(int(x)) for x in keys]
+    assert got_p.tolist() == [x is not None for x in ref]
+    assert got_c[got_p].tolist() == [x for x in ref if x is not None]
+
+
 # ---- generic / wide partition (nk_wide.hip) ---------------------------------
 @contextlib.contextmanager
 def wide_bits(bits):
@@ -360,8 +423,8 @@ def test_width128_split_phase_two_shards():
 
 
 class _CAI:
-    def __init__(self, ptr, n):
-        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<i8", "data": (ptr, False),
+    def __init__(self, ptr, n, typestr="<i8"):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (ptr, False),
                                          "version": 3}
 
 
