@@ -143,11 +143,8 @@ def main() -> int:
         # k-mers together stay below 2^31)
         nkdist.allreduce_currents_(cur_t, total_kmers=world * args.bases)
         ctr.finalize(False, s)
-        ptr, n = ctr.top_kmers_device()
-        mine = (torch.as_tensor(_CAI(ptr, n), device=dev) if n
-                else torch.zeros(0, dtype=torch.int64, device=dev))
-        allk = nkdist.gather_union(mine)  # union of every shard's top-N k-mers
-        ctr.merge_top_kmers(allk.data_ptr(), allk.numel(), s)
+        # union of every shard's distinct top-N k-mers: one fixed-size all-gather
+        nkdist.union_top_kmers(ctr)
 
     per = float("inf")  # fastest warmup step (the first one allocates)
     for _ in range(max(args.warmup, 1 if args.settle > 0 else 0)):

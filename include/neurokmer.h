@@ -121,6 +121,17 @@ int nk_finalize(nk_counter *c, int streaming_semantics, void *stream);
  * NK_KMER_128: the buffer holds n_keys (lo, hi) pairs (2 * n_keys u64). */
 int nk_top_kmers(nk_counter *c, const uint64_t **d_keys, size_t *n_keys);
 int nk_merge_top_kmers(nk_counter *c, const uint64_t *d_keys, size_t n_keys, void *stream);
+/* The same exchange with one fixed-size all-gather and no host round trip:
+ * nk_top_kmers_padded writes [n, key 0 .. key min(n, cap)-1] (n = this
+ * shard's key count; NK_KMER_128 keys take two words) to d_out on `stream`;
+ * the caller all-gathers world such segments of `stride` u64 words (stride
+ * >= 1 + cap, or 1 + 2 cap for NK_KMER_128) and nk_merge_top_kmers_padded
+ * recomputes the uniques column from them.  *complete = 0 when a segment held
+ * more than cap keys (every rank sees the same headers): the top rows are left
+ * unchanged and the caller falls back to nk_top_kmers + nk_merge_top_kmers. */
+int nk_top_kmers_padded(nk_counter *c, uint64_t *d_out, size_t cap, void *stream);
+int nk_merge_top_kmers_padded(nk_counter *c, const uint64_t *d_buf, size_t world,
+                              size_t stride, size_t cap, int *complete, void *stream);
 
 /* SpikingKmerCounter::top_abundant_neurons(&self, n) — src/spiking_hash.rs:661-673.
  * Writes min(n, pool_size) rows into out (caller-allocated), returns the count

@@ -34,6 +34,7 @@ EXPORTS = (
     "nk_energy_used", "nk_set_steps", "nk_get_steps", "nk_pool_size", "nk_k",
     "nk_use_canonical", "nk_copy_currents", "nk_copy_spike_counts", "nk_copy_voltages",
     "nk_copy_refractory", "nk_device_currents", "nk_reset", "nk_reset_async", "nk_last_timings",
+    "nk_top_kmers_padded", "nk_merge_top_kmers_padded",
     "nk_exact_owner", "nk_exact_partition", "nk_exact_adopt", "nk_device_kmer_per_neuron",
     "nk_last_error",
     "nk_version",
@@ -95,6 +96,8 @@ def load(share_torch: bool = True):
         "nk_finalize": (C.c_int, [vp, C.c_int, vp]),
         "nk_top_kmers": (C.c_int, [vp, P(vp), P(sz)]),
         "nk_merge_top_kmers": (C.c_int, [vp, vp, sz, vp]),
+        "nk_top_kmers_padded": (C.c_int, [vp, vp, sz, vp]),
+        "nk_merge_top_kmers_padded": (C.c_int, [vp, vp, sz, sz, sz, P(C.c_int), vp]),
         "nk_top_abundant_neurons": (C.c_long, [vp, sz, P(NkTopRow)]),
         "nk_get_count": (C.c_int, [vp, u64, P(u32), P(C.c_int)]),
         "nk_get_counts": (C.c_int, [vp, vp, sz, vp, vp]),

@@ -146,6 +146,19 @@ class SpikingKmerCounter:
     def device_kmer_per_neuron_ptr(self) -> int:
         return self._L.nk_device_kmer_per_neuron(self._h) or 0
 
+    def top_kmers_padded(self, d_out: int, cap: int, stream: int = 0) -> None:
+        """[n, keys...] (at most cap keys) of this shard into d_out, no host sync."""
+        check(self._L.nk_top_kmers_padded(self._h, d_out, cap, stream or None))
+
+    def merge_top_kmers_padded(self, d_buf: int, world: int, stride: int, cap: int,
+                               stream: int = 0) -> bool:
+        """Uniques from an all-gather of world padded segments; False: a segment
+        was truncated (fall back to top_kmers_device + merge_top_kmers)."""
+        ok = C.c_int(0)
+        check(self._L.nk_merge_top_kmers_padded(self._h, d_buf, world, stride, cap,
+                                                C.byref(ok), stream or None))
+        return bool(ok.value)
+
     def device_currents_ptr(self) -> int:
         return self._L.nk_device_currents(self._h) or 0
 

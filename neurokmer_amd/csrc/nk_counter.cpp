@@ -104,6 +104,8 @@ struct nk_counter {
   DevBuf<unsigned long long> set_keys;
   DevBuf<uint64_t> top_keys;
   DevBuf<unsigned long long> top_keys_n;
+  DevBuf<uint32_t> trunc_d;  // a padded all-gather segment held more keys than its cap
+  bool top_keys_ready = false;  // top_keys holds this shard's compacted list (padded export)
   DevBuf<uint32_t> radix_h;
   uint64_t set_cap = 0;     // capacity used by the last uniques pass
   uint64_t set_alloc = 0;   // allocated capacity of set_keys (keys)
@@ -753,6 +755,7 @@ static int finish_top(nk_counter *c, uint64_t want, bool fused, bool uniq, bool 
 
 static int lif_top_uniques(nk_counter *c, int streaming, bool use_kpn, hipStream_t s) {
   int rc;
+  c->top_keys_ready = false;
   const uint64_t want = std::min<uint64_t>(c->opts.top_n, c->pool);
   const bool uniq = want && c->have_input && c->last_in.n_tiles;
   // top-N selection (and the uniques post step) inside the LIF kernel
@@ -987,13 +990,15 @@ int nk_top_kmers(nk_counter *c, const uint64_t **d_keys, size_t *n_keys) {
     return NK_OK;
   }
   int rc;
-  if ((rc = c->top_keys.ensure(c->w128 ? 2 * c->set_cap : c->set_cap + 1))) return rc;
-  HIPCHK(hipMemsetAsync(c->top_keys_n.p, 0, 8, s));
-  if (c->w128)  // (lo, hi) pairs
-    HIPCHK(launch_set_compact128(c->set_keys.p, c->set_cap, c->top_keys.p, c->top_keys_n.p, s));
-  else
-    HIPCHK(launch_set_compact(c->set_keys.p, c->set_cap, c->special.p, m, c->cand.p, c->pool,
-                              c->top_keys.p, c->top_keys_n.p, s));
+  if (!c->top_keys_ready) {  // else: the padded export already compacted this shard's list
+    if ((rc = c->top_keys.ensure(c->w128 ? 2 * c->set_cap : c->set_cap + 1))) return rc;
+    HIPCHK(hipMemsetAsync(c->top_keys_n.p, 0, 8, s));
+    if (c->w128)  // (lo, hi) pairs
+      HIPCHK(launch_set_compact128(c->set_keys.p, c->set_cap, c->top_keys.p, c->top_keys_n.p, s));
+    else
+      HIPCHK(launch_set_compact(c->set_keys.p, c->set_cap, c->special.p, m, c->cand.p, c->pool,
+                                c->top_keys.p, c->top_keys_n.p, s));
+  }
   unsigned long long n = 0;
   HIPCHK(hipMemcpyAsync(&n, c->top_keys_n.p, 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
@@ -1002,25 +1007,29 @@ int nk_top_kmers(nk_counter *c, const uint64_t **d_keys, size_t *n_keys) {
   return NK_OK;
 }
 
-int nk_merge_top_kmers(nk_counter *c, const uint64_t *d_keys, size_t n_keys, void *stream) {
-  if (!c) return fail(NK_E_INVALID, "null counter");
-  (void)hipSetDevice(c->device);
-  hipStream_t s = pick_stream(c, stream);
+// uniques column of the top rows from a union of key lists (flat or the
+// fixed-stride all-gather form); *complete = 0 if a segment was truncated
+// (the top rows are then left as they were)
+static int merge_keys(nk_counter *c, const MergeSrc &src, uint64_t max_keys, int *complete,
+                      hipStream_t s) {
   const uint32_t m = (uint32_t)c->top.size();
+  if (complete) *complete = 1;
   if (!m) return NK_OK;
   uint64_t cap = 64;
-  while (cap < 2 * (uint64_t)n_keys + 2) cap <<= 1;
+  while (cap < 2 * max_keys + 2) cap <<= 1;
   int rc;
   if (cap > c->set_alloc) {
     if ((rc = c->set_keys.ensure(c->w128 ? 3 * cap : cap))) return rc;
     c->set_alloc = cap;
   }
+  if ((rc = c->trunc_d.ensure(1))) return rc;
   c->set_cap = cap;
   HIPCHK(launch_set_word(c->set_mask_d.p, cap - 1, s));
   HIPCHK(c->w128 ? launch_set_fill128(c->set_keys.p, c->set_mask_d.p, c->set_alloc, s)
                  : launch_set_fill(c->set_keys.p, c->set_mask_d.p, c->set_alloc, s));
   HIPCHK(hipMemsetAsync(c->uniq.p, 0, m * 4, s));
   HIPCHK(hipMemsetAsync(c->special.p, 0, m * 4, s));
+  HIPCHK(hipMemsetAsync(c->trunc_d.p, 0, 4, s));
   UniqArgs u{};
   u.top = c->cand.p;
   u.n_top = m;
@@ -1029,15 +1038,68 @@ int nk_merge_top_kmers(nk_counter *c, const uint64_t *d_keys, size_t n_keys, voi
   u.set_mask = c->set_mask_d.p;
   u.uniq = c->uniq.p;
   u.special = c->special.p;
+  MergeSrc ms = src;
+  ms.trunc = c->trunc_d.p;
   if (c->w128)
-    HIPCHK(launch_set_merge128(d_keys, n_keys, c->pool, u, s));
+    HIPCHK(launch_set_merge128(ms, c->pool, u, s));
   else
-    HIPCHK(launch_set_merge(d_keys, n_keys, c->pool, u, s));
+    HIPCHK(launch_set_merge(ms, c->pool, u, s));
   uint32_t *hu = reinterpret_cast<uint32_t *>(c->res_h);
   HIPCHK(hipMemcpyAsync(hu, c->uniq.p, m * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(hu + m, c->trunc_d.p, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  if (hu[m]) {
+    if (complete) *complete = 0;
+    return NK_OK;
+  }
   for (uint32_t i = 0; i < m; ++i) c->top[i].uniques = hu[i];
   return NK_OK;
+}
+
+int nk_merge_top_kmers(nk_counter *c, const uint64_t *d_keys, size_t n_keys, void *stream) {
+  if (!c) return fail(NK_E_INVALID, "null counter");
+  (void)hipSetDevice(c->device);
+  MergeSrc src{};
+  src.keys = d_keys;
+  src.n = n_keys;
+  return merge_keys(c, src, n_keys, nullptr, pick_stream(c, stream));
+}
+
+int nk_top_kmers_padded(nk_counter *c, uint64_t *d_out, size_t cap, void *stream) {
+  if (!c || !d_out) return fail(NK_E_INVALID, "null argument");
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  const uint32_t m = (uint32_t)c->top.size();
+  if (!m || !c->set_cap) {
+    HIPCHK(hipMemsetAsync(d_out, 0, 8, s));
+    return NK_OK;
+  }
+  int rc;
+  if ((rc = c->top_keys.ensure(c->w128 ? 2 * c->set_cap : c->set_cap + 1))) return rc;
+  HIPCHK(hipMemsetAsync(c->top_keys_n.p, 0, 8, s));
+  if (c->w128)
+    HIPCHK(launch_set_compact128(c->set_keys.p, c->set_cap, c->top_keys.p, c->top_keys_n.p, s));
+  else
+    HIPCHK(launch_set_compact(c->set_keys.p, c->set_cap, c->special.p, m, c->cand.p, c->pool,
+                              c->top_keys.p, c->top_keys_n.p, s));
+  HIPCHK(launch_pad_keys(c->top_keys.p, c->top_keys_n.p, cap, c->w128 ? 2 : 1, d_out, s));
+  c->top_keys_ready = true;  // kept for the variable-length fallback (nk_top_kmers)
+  return NK_OK;
+}
+
+int nk_merge_top_kmers_padded(nk_counter *c, const uint64_t *d_buf, size_t world, size_t stride,
+                              size_t cap, int *complete, void *stream) {
+  if (!c || !d_buf || !complete) return fail(NK_E_INVALID, "null argument");
+  if (!world || world > (1u << 20) || stride < 1 + (c->w128 ? 2 : 1) * cap)
+    return fail(NK_E_INVALID, "bad all-gather layout (world %zu, stride %zu, cap %zu)", world,
+                stride, cap);
+  (void)hipSetDevice(c->device);
+  MergeSrc src{};
+  src.keys = d_buf;
+  src.world = (uint32_t)world;
+  src.stride = stride;
+  src.cap = cap;
+  return merge_keys(c, src, (uint64_t)world * cap, complete, pick_stream(c, stream));
 }
 
 long nk_top_abundant_neurons(nk_counter *c, size_t n, nk_top_row *out) {

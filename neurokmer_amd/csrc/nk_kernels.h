@@ -132,6 +132,17 @@ struct GenPartArgs {
   unsigned long long *currents;   // overflow target
 };
 
+// keys handed to the uniques merge: a flat list (world == 0) or the
+// fixed-stride segments [n_r, keys...] of an all-gather buffer
+struct MergeSrc {
+  const uint64_t *keys;
+  uint64_t n;          // flat: number of keys
+  uint32_t world;      // segments (0: flat)
+  uint64_t stride;     // u64 words per segment
+  uint64_t cap;        // keys stored per segment
+  uint32_t *trunc;     // set when a segment's n_r > cap
+};
+
 struct UniqArgs {
   const TopCand *top;  // top-N rows (sorted)
   uint32_t n_top;
@@ -185,8 +196,7 @@ hipError_t launch_set_fill128(unsigned long long *set3, const uint64_t *mask, ui
                               hipStream_t s);
 hipError_t launch_set_compact128(const unsigned long long *set3, uint64_t cap, uint64_t *out,
                                  unsigned long long *count, hipStream_t s);
-hipError_t launch_set_merge128(const uint64_t *keys, uint64_t n, uint64_t pool, const UniqArgs &u,
-                               hipStream_t s);
+hipError_t launch_set_merge128(const MergeSrc &m, uint64_t pool, const UniqArgs &u, hipStream_t s);
 hipError_t launch_set_word(uint64_t *w, uint64_t v, hipStream_t s);
 // tile -> first record index for the count kernels, fused with a zero list
 hipError_t launch_prep(const KmerInput &in, uint64_t tile_size, uint32_t *tile_rec,
@@ -198,8 +208,10 @@ hipError_t launch_gather(const TopState *st, const uint64_t *stats, const uint64
 hipError_t launch_set_compact(const unsigned long long *keys, uint64_t cap, const uint32_t *special,
                               uint32_t n_top, const TopCand *top, uint64_t pool,
                               uint64_t *out, unsigned long long *count, hipStream_t s);
-hipError_t launch_set_merge(const uint64_t *keys, uint64_t n, uint64_t pool, const UniqArgs &u,
-                            hipStream_t s);
+hipError_t launch_set_merge(const MergeSrc &m, uint64_t pool, const UniqArgs &u, hipStream_t s);
+// [n, min(n, cap) keys of wpk u64 words] from a compacted key list (n on the device)
+hipError_t launch_pad_keys(const uint64_t *src, const unsigned long long *n_src, uint64_t cap,
+                           int wpk, uint64_t *dst, hipStream_t s);
 
 hipError_t launch_part(const KmerInput &in, int k, int canonical, uint64_t pool,
                        const PartArgs &pa, hipStream_t s);

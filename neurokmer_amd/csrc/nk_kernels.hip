@@ -347,15 +347,36 @@ __global__ void k_set_compact128(const unsigned long long *__restrict__ S, uint6
 }
 
 // the union of several ranks' top k-mers ((lo, hi) pairs) into the set
-__global__ void k_set_merge128(const uint64_t *__restrict__ keys, uint64_t n, FastMod fm,
-                               UniqArgs u) {
+// Keys to merge: a flat list (world == 0), or `world` rank segments of a
+// fixed-stride all-gather buffer, each [n_r, key 0, key 1, ...] with at most
+// cap keys stored (a larger n_r sets *trunc: the caller falls back to the
+// variable-length exchange).  wpk: u64 words per key (2 for 128-bit keys).
+__device__ __forceinline__ bool merge_src_key(const MergeSrc &m, uint64_t i, int wpk,
+                                              const uint64_t **at) {
+  if (!m.world) {
+    *at = m.keys + (uint64_t)wpk * i;
+    return true;
+  }
+  const uint64_t r = i / m.cap, j = i - r * m.cap;
+  const uint64_t *seg = m.keys + r * m.stride;
+  const uint64_t nr = seg[0];
+  if (j == 0 && nr > m.cap) *m.trunc = 1u;
+  if (j >= nr) return false;
+  *at = seg + 1 + (uint64_t)wpk * j;
+  return true;
+}
+
+__global__ void k_set_merge128(MergeSrc m, FastMod fm, UniqArgs u) {
   extern __shared__ uint64_t dyn[];
   uint64_t *tbl_idx = dyn;
   uint32_t *tbl_slot = reinterpret_cast<uint32_t *>(dyn + u.tbl_size);
   build_top_tbl(u, tbl_idx, tbl_slot);
+  const uint64_t n = m.world ? (uint64_t)m.world * m.cap : m.n;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * blockDim.x) {
-    const Key128 key{keys[2 * i], keys[2 * i + 1]};
+    const uint64_t *at;
+    if (!merge_src_key(m, i, 2, &at)) continue;
+    const Key128 key{at[0], at[1]};
     const uint64_t idx = fastmod(sip13_u128(key.lo, key.hi), fm);
     const int slot = probe_top(tbl_idx, tbl_slot, u.tbl_size - 1, idx);
     if (slot >= 0) set_insert128(u, (uint32_t)slot, key);
@@ -1597,20 +1618,34 @@ __global__ void k_set_compact(const unsigned long long *__restrict__ keys, uint6
   }
 }
 
-__global__ void k_set_merge(const uint64_t *__restrict__ keys, uint64_t n, FastMod fm, UniqArgs u) {
+__global__ void k_set_merge(MergeSrc m, FastMod fm, UniqArgs u) {
   extern __shared__ uint64_t dyn[];
   __shared__ unsigned long long seen[kSeen];
   uint64_t *tbl_idx = dyn;
   uint32_t *tbl_slot = reinterpret_cast<uint32_t *>(dyn + u.tbl_size);
   seen_init(seen);
   build_top_tbl(u, tbl_idx, tbl_slot);
+  const uint64_t n = m.world ? (uint64_t)m.world * m.cap : m.n;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t key = keys[i];
+    const uint64_t *at;
+    if (!merge_src_key(m, i, 1, &at)) continue;
+    uint64_t key = *at;
     uint64_t idx = fastmod(sip13_u64(key), fm);
     int slot = probe_top(tbl_idx, tbl_slot, u.tbl_size - 1, idx);
     if (slot >= 0 && (key == kEmpty || !seen_before(seen, key))) set_insert(u, (uint32_t)slot, key);
   }
+}
+
+// [n, keys...] with min(n, cap) keys of wpk words each (the all-gather form)
+__global__ void k_pad_keys(const uint64_t *__restrict__ src, const unsigned long long *__restrict__ n_src,
+                           uint64_t cap, int wpk, uint64_t *__restrict__ dst) {
+  const uint64_t n = *n_src;
+  const uint64_t w = (n < cap ? n : cap) * (uint64_t)wpk;
+  if (blockIdx.x == 0 && threadIdx.x == 0) dst[0] = n;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < w;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    dst[1 + i] = src[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -1798,13 +1833,12 @@ hipError_t launch_set_compact128(const unsigned long long *set3, uint64_t cap, u
   hipLaunchKernelGGL(k_set_compact128, dim3(g), dim3(256), 0, s, set3, cap, out, count);
   return hipGetLastError();
 }
-hipError_t launch_set_merge128(const uint64_t *keys, uint64_t n, uint64_t pool, const UniqArgs &u,
-                               hipStream_t s) {
+hipError_t launch_set_merge128(const MergeSrc &m, uint64_t pool, const UniqArgs &u, hipStream_t s) {
+  const uint64_t n = m.world ? (uint64_t)m.world * m.cap : m.n;
   if (!n) return hipSuccess;
   unsigned g = (unsigned)((n + 255) / 256);
   if (g > 2048) g = 2048;
-  hipLaunchKernelGGL(k_set_merge128, dim3(g), dim3(256), tbl_bytes(u), s, keys, n,
-                     make_fastmod(pool), u);
+  hipLaunchKernelGGL(k_set_merge128, dim3(g), dim3(256), tbl_bytes(u), s, m, make_fastmod(pool), u);
   return hipGetLastError();
 }
 
@@ -1819,13 +1853,21 @@ hipError_t launch_set_compact(const unsigned long long *keys, uint64_t cap, cons
   return hipGetLastError();
 }
 
-hipError_t launch_set_merge(const uint64_t *keys, uint64_t n, uint64_t pool, const UniqArgs &u,
-                            hipStream_t s) {
+hipError_t launch_set_merge(const MergeSrc &m, uint64_t pool, const UniqArgs &u, hipStream_t s) {
+  const uint64_t n = m.world ? (uint64_t)m.world * m.cap : m.n;
   if (!n) return hipSuccess;
   unsigned g = (unsigned)((n + 255) / 256);
   if (g > 2048) g = 2048;
-  hipLaunchKernelGGL(k_set_merge, dim3(g), dim3(256), tbl_bytes(u), s, keys, n,
-                     make_fastmod(pool), u);
+  hipLaunchKernelGGL(k_set_merge, dim3(g), dim3(256), tbl_bytes(u), s, m, make_fastmod(pool), u);
+  return hipGetLastError();
+}
+
+hipError_t launch_pad_keys(const uint64_t *src, const unsigned long long *n_src, uint64_t cap,
+                           int wpk, uint64_t *dst, hipStream_t s) {
+  unsigned g = (unsigned)((cap * wpk + 255) / 256);
+  if (g > 1024) g = 1024;
+  if (!g) g = 1;
+  hipLaunchKernelGGL(k_pad_keys, dim3(g), dim3(256), 0, s, src, n_src, cap, wpk, dst);
   return hipGetLastError();
 }
 

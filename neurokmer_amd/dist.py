@@ -82,6 +82,42 @@ def allreduce_currents_(t, group=None, total_kmers=None) -> None:
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
 
 
+def _all_gather_into(out, inp, group=None):
+    """all_gather_into_tensor; with gloo the device tensors go through host memory."""
+    import torch.distributed as dist
+    if dist.get_backend(group) == "gloo" and out.is_cuda:
+        o = out.cpu()
+        dist.all_gather_into_tensor(o, inp.cpu(), group=group)
+        out.copy_(o)
+        return
+    dist.all_gather_into_tensor(out, inp, group=group)
+
+
+def union_top_kmers(ctr, group=None, cap: int = 4096) -> None:
+    """After finalize on every rank: the uniques column of the (identical) top
+    rows from the union of every shard's distinct top-N k-mers.  One fixed-size
+    all-gather of [n, keys...] segments (at most cap keys each) and no host
+    round trip before the merge; if some shard has more than cap keys (every
+    rank sees the same headers) all ranks fall back to the variable-length
+    exchange (gather_union)."""
+    import torch
+    world = torch.distributed.get_world_size(group)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    stream = torch.cuda.current_stream().cuda_stream
+    wpk = 2 if getattr(ctr, "kmer_width", 64) == 128 else 1
+    stride = 1 + wpk * cap
+    mine = torch.empty(stride, dtype=torch.int64, device=dev)
+    ctr.top_kmers_padded(mine.data_ptr(), cap, stream)
+    allb = torch.empty(world * stride, dtype=torch.int64, device=dev)
+    _all_gather_into(allb, mine, group=group)
+    if ctr.merge_top_kmers_padded(allb.data_ptr(), world, stride, cap, stream):
+        return
+    ptr, n = ctr.top_kmers_device()
+    keys = _dev_view(ptr, n * wpk, "<i8", dev)
+    allk = gather_union(keys, group)
+    ctr.merge_top_kmers(allk.data_ptr(), allk.numel() // wpk, stream)
+
+
 def gather_union(keys, group=None):
     """All-gather variable-length int64 key lists -> one concatenated tensor
     (the merge deduplicates).  Two collectives into single tensors and one
@@ -91,13 +127,13 @@ def gather_union(keys, group=None):
     world = dist.get_world_size(group)
     n = torch.tensor([keys.numel()], dtype=torch.int64, device=keys.device)
     sizes_t = torch.empty(world, dtype=torch.int64, device=keys.device)
-    dist.all_gather_into_tensor(sizes_t, n, group=group)
+    _all_gather_into(sizes_t, n, group=group)
     sizes = sizes_t.tolist()
     width = max(max(sizes), 1)
     pad = torch.full((width,), -1, dtype=torch.int64, device=keys.device)
     pad[:keys.numel()] = keys
     parts = torch.empty(world * width, dtype=torch.int64, device=keys.device)
-    dist.all_gather_into_tensor(parts, pad, group=group)
+    _all_gather_into(parts, pad, group=group)
     return torch.cat([parts[r * width:r * width + s] for r, s in enumerate(sizes)])
 
 

@@ -98,3 +98,54 @@ def test_two_ranks_exact_table_and_uniques():
         assert pres == [x is not None for x in exp]
         assert [c for c, p in zip(cnt, pres) if p] == [x for x in exp if x is not None]
     assert sum(r[2] for r in res) == ref.distinct_kmers()
+
+
+def _rank_union(rank, world, port, width, cap, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from neurokmer_amd import SpikingKmerCounter
+        from neurokmer_amd import dist as nkdist
+        bases, offs = _input()
+        k = 41 if width == 128 else K
+        lo, hi, so = nkdist.shard_records(offs, world, k)[rank]
+        b = bases[lo:hi]
+        d_b = torch.from_numpy(np.concatenate([b, np.zeros(16, np.uint8)])).cuda()
+        d_o = torch.from_numpy(so.astype(np.uint64).view(np.int64)).cuda()
+        torch.cuda.synchronize()
+        c = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, POOL, True, kmer_width=width)
+        c.accumulate_device(d_b.data_ptr(), d_o.data_ptr(), so.size - 1, b.size)
+        cur = torch.as_tensor(_CAI(c.device_currents_ptr(), POOL), device="cuda")
+        nkdist.allreduce_currents_(cur)
+        c.finalize(False)
+        nkdist.union_top_kmers(c, cap=cap)
+        q.put((rank, c.top_abundant_neurons(20)))
+        c.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("width,cap", [(64, 4096), (64, 3), (128, 4096), (128, 3)])
+def test_two_ranks_union_of_top_kmers(width, cap):
+    # cap 3: some shard holds more keys -> every rank takes the variable-length path
+    import torch.multiprocessing as mp
+    from oracle import cbind
+    bases, offs = _input()
+    k = 41 if width == 128 else K
+    ref = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, POOL, True, width=width)
+    ref.process_parallel_arrays(bases, offs)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_union, args=(r, 2, port, width, cap, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    top = ref.top_abundant_neurons(20)
+    for _, t in res:
+        assert t == top

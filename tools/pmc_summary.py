@@ -18,7 +18,7 @@ import os
 import sys
 from collections import defaultdict
 
-COUNT_KERNEL = "k_part<true>"  # K1a, canonical
+COUNT_KERNEL = "k_part<true"  # K1a, canonical (any bucket capacity)
 
 
 def main(src, dst):
