@@ -11,6 +11,8 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
 BENCH="python3 $ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline"
+# counters do not depend on the clock: no settle steps under --pmc
+BENCH_PMC="python3 $ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --settle 0"
 case $MODE in
   list)
     timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1
@@ -23,7 +25,7 @@ case $MODE in
     i=0
     for set in "$@"; do
       i=$((i+1))
-      timeout -k 10 600 rocprofv3 --pmc $set --output-format csv -d "$OUT/pmc$i" -o run -- $BENCH > "$OUT/pmc$i.log" 2>&1 || exit $?
+      timeout -k 10 240 rocprofv3 --pmc $set --output-format csv -d "$OUT/pmc$i" -o run -- $BENCH_PMC > "$OUT/pmc$i.log" 2>&1 || exit $?
     done
     ;;
 esac
