@@ -218,6 +218,12 @@ int nk_reset_async(nk_counter *c, void *stream);
  * (hipEvents on the stream the kernels ran on).  Returns the number of stages
  * written (<= cap); names are static strings. */
 int nk_last_timings(const nk_counter *c, const char **names, float *ms, int cap);
+/* Device time of the count kernel (K1: hash + partition/count) of each of the
+ * last min(cap, 256) accumulate/process calls, oldest first, milliseconds
+ * (hipEvents around the launch on its stream).  Lets a benchmark read every
+ * timed step's K1 duration after its timed loop.  Returns the number written.
+ * (No reference counterpart: measurement only.) */
+int nk_count_history(const nk_counter *c, float *ms, int cap);
 
 const char *nk_last_error(void);
 const char *nk_version(void);

@@ -34,6 +34,7 @@ EXPORTS = (
     "nk_energy_used", "nk_set_steps", "nk_get_steps", "nk_pool_size", "nk_k",
     "nk_use_canonical", "nk_copy_currents", "nk_copy_spike_counts", "nk_copy_voltages",
     "nk_copy_refractory", "nk_device_currents", "nk_reset", "nk_reset_async", "nk_last_timings",
+    "nk_count_history",
     "nk_top_kmers_padded", "nk_merge_top_kmers_padded",
     "nk_exact_owner", "nk_exact_partition", "nk_exact_adopt", "nk_device_kmer_per_neuron",
     "nk_last_error",
@@ -123,6 +124,7 @@ def load(share_torch: bool = True):
         "nk_reset": (C.c_int, [vp]),
         "nk_reset_async": (C.c_int, [vp, vp]),
         "nk_last_timings": (C.c_int, [vp, P(C.c_char_p), P(C.c_float), C.c_int]),
+        "nk_count_history": (C.c_int, [vp, P(C.c_float), C.c_int]),
         "nk_last_error": (C.c_char_p, []),
         "nk_version": (C.c_char_p, []),
     }

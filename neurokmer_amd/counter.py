@@ -241,3 +241,10 @@ class SpikingKmerCounter:
         ms = (C.c_float * 8)()
         n = self._L.nk_last_timings(self._h, names, ms, 8)
         return {names[i].decode(): float(ms[i]) for i in range(n)}
+
+    def count_history(self, n: int) -> list:
+        """K1 (count kernel) device time in ms of each of the last min(n, 256)
+        accumulate/process calls, oldest first (hipEvents around the launch)."""
+        buf = (C.c_float * max(n, 1))()
+        m = self._L.nk_count_history(self._h, buf, n)
+        return [float(buf[i]) for i in range(m)]

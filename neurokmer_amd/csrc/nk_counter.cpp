@@ -11,6 +11,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <chrono>
 #include <future>
 #include <string>
 #include <vector>
@@ -116,8 +117,11 @@ struct nk_counter {
   DevBuf<uint32_t> post_flags;  // [0] set too small [1] top bucket overflowed [2] top buckets
   // packed finalize results: ResultHdr | cand[m] | uniq[m]
   static constexpr size_t kResBytes = sizeof(ResultHdr) + kMaxTopN * (sizeof(TopCand) + 4);
+  // + a 64-B line after the results: k_gather's completion word (res_seq)
+  static constexpr size_t kResFlagOff = (kResBytes + 63) & ~(size_t)63;
   uint8_t *res_h = nullptr;   // pinned, mapped: written by k_gather
   uint8_t *res_hd = nullptr;  // its device-side address
+  uint64_t res_seq = 0;       // last completion word asked of k_gather
   // host copies of input (host-array entry points)
   DevBuf<uint8_t> in_bases;
   DevBuf<uint64_t> in_offs;
@@ -172,6 +176,12 @@ struct nk_counter {
   hipEvent_t ev[kStages + 1] = {};  // see collect_timings
   float stage_ms[kStages] = {};
   int n_stage = 0;
+  int timing_pending = 0;  // 0: stage_ms is current; 1/2: collect (without/with count) on demand
+  // ev[1]/ev[2] (around the count kernel) rotate through a ring, one pair per
+  // accumulate call, so every call's K1 time stays readable (nk_count_history)
+  static constexpr int kCountRing = 256;
+  hipEvent_t cnt_ev[kCountRing][2] = {};
+  uint64_t cnt_calls = 0;
 };
 
 // ev[i] for the stage timings; the inner stage boundaries only in full mode
@@ -319,7 +329,16 @@ nk_counter *nk_new(size_t k, float threshold, float leak, uint32_t refractory, d
   c->w128 = o.kmer_width == NK_KMER_128;
   c->device = o.device;
   bool ok = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) == hipSuccess;
-  for (int i = 0; ok && i <= kStages; ++i) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
+  // timing-only markers: no system-scope fence (a fenced marker between two
+  // kernels writes back L2 and idles the GPU ~2.5 us; tools/syncbench.hip)
+  for (int i = 0; ok && i <= kStages; ++i)
+    if (i != 1 && i != 2)
+      ok = hipEventCreateWithFlags(&c->ev[i], hipEventDisableSystemFence) == hipSuccess;
+  for (int i = 0; ok && i < nk_counter::kCountRing; ++i)
+    for (int j = 0; ok && j < 2; ++j)
+      ok = hipEventCreateWithFlags(&c->cnt_ev[i][j], hipEventDisableSystemFence) == hipSuccess;
+  c->ev[1] = c->cnt_ev[0][0];
+  c->ev[2] = c->cnt_ev[0][1];
   size_t P = pool_size ? pool_size : 1;
   ok = ok && !c->cur.ensure(P) && !c->sc.ensure(P) && !c->v.ensure(P) && !c->r.ensure(P) &&
        !c->hist.ensure(kHistBins * kHistCopies) && !c->stats.ensure(2) && !c->topst.ensure(1) &&
@@ -328,7 +347,7 @@ nk_counter *nk_new(size_t k, float threshold, float leak, uint32_t refractory, d
        !c->top_keys_n.ensure(1) && !c->radix_h.ensure(256) && !c->set_mask_d.ensure(1) &&
        !c->set_need_d.ensure(1) && !c->post_flags.ensure(4) && !c->set_keys.ensure((o.kmer_width == NK_KMER_128 ? 3 : 1) << 20) &&
        !c->hits.ensure(1 << 19) && !c->n_hits.ensure(1) &&
-       hipHostMalloc((void **)&c->res_h, nk_counter::kResBytes,
+       hipHostMalloc((void **)&c->res_h, nk_counter::kResFlagOff + 64,
                      hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
        hipHostGetDevicePointer((void **)&c->res_hd, c->res_h, 0) == hipSuccess;
   c->set_alloc = 1 << 20;
@@ -360,7 +379,10 @@ void nk_free(nk_counter *c) {
   c->set_need_d.release(); c->post_flags.release(); c->hits.release(); c->n_hits.release();
   if (c->res_h) (void)hipHostFree(c->res_h); c->in_bases.release(); c->in_offs.release();
   for (int i = 0; i <= kStages; ++i)
-    if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+    if (c->ev[i] && i != 1 && i != 2) (void)hipEventDestroy(c->ev[i]);
+  for (auto &pr : c->cnt_ev)
+    for (auto &e : pr)
+      if (e) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
 }
@@ -564,6 +586,11 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
     z.ptr[z.n] = c->stats.p; z.bytes[z.n++] = 16;
     c->lif_zeroed = true;
   }
+  {
+    const int slot = (int)(c->cnt_calls++ % nk_counter::kCountRing);
+    c->ev[1] = c->cnt_ev[slot][0];
+    c->ev[2] = c->cnt_ev[slot][1];
+  }
   HIPCHK(mark(c, 0, s));
   HIPCHK(launch_prep(in, cp.tile, c->tile_rec.p, z, s));
   c->cur_fresh = false;
@@ -741,7 +768,31 @@ static int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, bool post_don
 static int enqueue_readback(nk_counter *c, uint32_t m, bool uniq, hipStream_t s) {
   HIPCHK(launch_gather(c->topst.p, c->stats.p, uniq ? c->set_mask_d.p : nullptr,
                        uniq ? c->post_flags.p : nullptr, c->cand.p, uniq ? c->uniq.p : nullptr, m,
-                       c->res_hd, s));  // straight into pinned host memory: no copy
+                       c->res_hd, reinterpret_cast<uint64_t *>(c->res_hd + nk_counter::kResFlagOff),
+                       ++c->res_seq, s));  // straight into pinned host memory: no copy
+  return NK_OK;
+}
+
+// Wait for the k_gather of enqueue_readback: spin on its completion word in
+// mapped host memory (the results are complete once it shows res_seq; the
+// kernel does no memory access after it), which sees completion ~5 us sooner
+// than hipStreamSynchronize (tools/syncbench.hip).  Past kSpinUs the wait
+// falls back to hipStreamSynchronize, which also reports a failed launch.
+static int wait_readback(nk_counter *c, hipStream_t s) {
+  constexpr double kSpinUs = 20000.0;
+  const uint64_t *flag = reinterpret_cast<const uint64_t *>(c->res_h + nk_counter::kResFlagOff);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t i = 0;; ++i) {
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == c->res_seq) return NK_OK;
+    __builtin_ia32_pause();
+    if ((i & 1023) == 1023 &&
+        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() >
+            kSpinUs)
+      break;
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != c->res_seq)
+    return fail(NK_E_DEVICE, "result readback did not complete");
   return NK_OK;
 }
 
@@ -787,8 +838,8 @@ static int finish_top(nk_counter *c, uint64_t want, bool fused, bool uniq, bool 
   };
   if ((rc = uniques(fused))) return rc;
   if ((rc = enqueue_readback(c, (uint32_t)want, uniq, s))) return rc;
-  HIPCHK(mark(c, 6, s));
-  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(mark(c, 6, s));  // may still be pending on return: timings are collected on demand
+  if ((rc = wait_readback(c, s))) return rc;
   const ResultHdr *h = reinterpret_cast<const ResultHdr *>(c->res_h);
   const TopCand *hc = reinterpret_cast<const TopCand *>(c->res_h + sizeof(ResultHdr));
   const uint32_t *hu =
@@ -837,7 +888,17 @@ static int finish_top(nk_counter *c, uint64_t want, bool fused, bool uniq, bool 
   return NK_OK;
 }
 
+static void collect_timings_now(nk_counter *c, bool with_count);
+
+// The stage markers of the last call may still be pending when it returns
+// (the results are awaited on k_gather's completion word, not on the stream):
+// the timings are read when asked for.
 static void collect_timings(nk_counter *c, bool with_count) {
+  c->timing_pending = with_count ? 2 : 1;
+  c->n_stage = c->opts.stage_timing ? kStages : kStagesLight;
+}
+
+static void collect_timings_now(nk_counter *c, bool with_count) {
   // ev[0] start | ev[1] after index | ev[2] after K1 count (K1a) | ev[3] after
   // K1b/K1c | ev[4] after lif | ev[5] after topn | ev[6] after uniques |
   // ev[7] finalize start
@@ -1655,8 +1716,31 @@ int nk_copy_refractory(nk_counter *c, uint32_t *out, size_t n) {
   return copy_out(c, c->r, out, n);
 }
 
+int nk_count_history(const nk_counter *c, float *ms, int cap) {
+  if (!c || !ms || cap <= 0) return 0;
+  (void)hipSetDevice(c->device);
+  const uint64_t n = std::min<uint64_t>({(uint64_t)cap, c->cnt_calls, (uint64_t)nk_counter::kCountRing});
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t call = c->cnt_calls - n + i;
+    const auto &pr = c->cnt_ev[call % nk_counter::kCountRing];
+    float t = 0.0f;
+    if (hipEventSynchronize(pr[1]) != hipSuccess || hipEventElapsedTime(&t, pr[0], pr[1]) != hipSuccess)
+      t = -1.0f;
+    ms[i] = t;
+  }
+  return (int)n;
+}
+
 int nk_last_timings(const nk_counter *c, const char **names, float *ms, int cap) {
   if (!c) return 0;
+  if (c->timing_pending) {  // logically const: fills the cache of the last call's timings
+    nk_counter *m = const_cast<nk_counter *>(c);
+    (void)hipSetDevice(m->device);
+    const bool wc = m->timing_pending == 2;
+    m->timing_pending = 0;
+    if (hipEventSynchronize(m->ev[6]) == hipSuccess) collect_timings_now(m, wc);
+    else std::fill(m->stage_ms, m->stage_ms + kStages, 0.0f);
+  }
   int n = std::min(cap, c->n_stage);
   for (int i = 0; i < n; ++i) {
     if (names) names[i] = c->opts.stage_timing ? kStageNames[i] : kStageNamesLight[i];

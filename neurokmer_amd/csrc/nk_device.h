@@ -101,11 +101,12 @@ __device__ __forceinline__ uint64_t fastmod(uint64_t h, FastMod fm) {
   return r;
 }
 
-// Exact h % P for P < 2^30 in 32-bit arithmetic: r = h - q*P < 3P < 2^32, so
-// only the low word of q = mulhi64(h, magic) is needed (one mul_hi + two
-// v_mad_u64_u32 + one mul_lo), then r = h_lo - q_lo*P (mod 2^32) and two
-// branch-free corrections min(r, r - P).  Checked against % on 2.4e8 values
-// (tools/README).
+// Exact h % P for P < 2^30 in 32-bit arithmetic.  magic = floor((2^64-1)/P)
+// satisfies 2^64/P - 1 <= magic <= 2^64/P, so q = mulhi64(h, magic) lies in
+// (h/P - 1 - h/2^64, h/P], i.e. q = floor(h/P) - {0, 1}: r = h - q*P < 2P <
+// 2^31 and ONE branch-free correction min(r, r - P) is exact.  Only the low
+// word of q is needed (one mul_hi + two v_mad_u64_u32 + one mul_lo).  Model
+// and edge cases: tests/test_oracle.py::test_fastmod32_model.
 __device__ __forceinline__ uint32_t fastmod32(uint64_t h, FastMod fm) {
   const uint32_t h0 = (uint32_t)h, h1 = (uint32_t)(h >> 32);
   const uint32_t m0 = (uint32_t)fm.magic, m1 = (uint32_t)(fm.magic >> 32);
@@ -114,10 +115,8 @@ __device__ __forceinline__ uint32_t fastmod32(uint64_t h, FastMod fm) {
   uint64_t mid = (uint64_t)h1 * m0 + ahi;
   mid = (uint64_t)h0 * m1 + mid;
   const uint32_t qlo = h1 * m1 + (uint32_t)(mid >> 32);
-  uint32_t r = h0 - qlo * p;
-  r = min(r, r - p);
-  r = min(r, r - p);
-  return r;
+  const uint32_t r = h0 - qlo * p;
+  return min(r, r - p);
 }
 
 // ---- LIF -------------------------------------------------------------------

@@ -204,7 +204,7 @@ hipError_t launch_prep(const KmerInput &in, uint64_t tile_size, uint32_t *tile_r
 hipError_t launch_zero(const ZeroList &z, hipStream_t s);
 hipError_t launch_gather(const TopState *st, const uint64_t *stats, const uint64_t *mask,
                          const uint32_t *flags, const TopCand *cand, const uint32_t *uniq,
-                         uint32_t m, uint8_t *out, hipStream_t s);
+                         uint32_t m, uint8_t *out, uint64_t *done, uint64_t seq, hipStream_t s);
 hipError_t launch_set_compact(const unsigned long long *keys, uint64_t cap, const uint32_t *special,
                               uint32_t n_top, const TopCand *top, uint64_t pool,
                               uint64_t *out, unsigned long long *count, hipStream_t s);

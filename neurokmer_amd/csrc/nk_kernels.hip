@@ -2013,12 +2013,15 @@ hipError_t launch_zero(const ZeroList &z, hipStream_t s) {
   return hipGetLastError();
 }
 
-// Everything the host needs after a finalize, packed for ONE D2H copy:
-// [TopState | stats[2] | set mask | flags[4] | cand[m] | uniq[m]]
+// Everything the host needs after a finalize, written straight into mapped
+// host memory: [TopState | stats[2] | set mask | flags[4] | cand[m] | uniq[m]],
+// then the completion word `done = seq` the host spins on.  Every wave fences
+// its own stores at system scope before the barrier, so the word is published
+// after all of them; the kernel touches no memory after it.
 __global__ void k_gather(const TopState *__restrict__ st, const uint64_t *__restrict__ stats,
                          const uint64_t *__restrict__ mask, const uint32_t *__restrict__ flags,
                          const TopCand *__restrict__ cand, const uint32_t *__restrict__ uniq,
-                         uint32_t m, uint8_t *__restrict__ out) {
+                         uint32_t m, uint8_t *__restrict__ out, uint64_t *done, uint64_t seq) {
   ResultHdr *h = reinterpret_cast<ResultHdr *>(out);
   TopCand *c = reinterpret_cast<TopCand *>(out + sizeof(ResultHdr));
   uint32_t *u = reinterpret_cast<uint32_t *>(out + sizeof(ResultHdr) + (size_t)m * sizeof(TopCand));
@@ -2033,12 +2036,16 @@ __global__ void k_gather(const TopState *__restrict__ st, const uint64_t *__rest
     c[i] = cand[i];
     u[i] = uniq ? uniq[i] : 0;
   }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 hipError_t launch_gather(const TopState *st, const uint64_t *stats, const uint64_t *mask,
                          const uint32_t *flags, const TopCand *cand, const uint32_t *uniq,
-                         uint32_t m, uint8_t *out, hipStream_t s) {
-  hipLaunchKernelGGL(k_gather, dim3(1), dim3(1024), 0, s, st, stats, mask, flags, cand, uniq, m, out);
+                         uint32_t m, uint8_t *out, uint64_t *done, uint64_t seq, hipStream_t s) {
+  hipLaunchKernelGGL(k_gather, dim3(1), dim3(1024), 0, s, st, stats, mask, flags, cand, uniq, m, out,
+                     done, seq);
   return hipGetLastError();
 }
 

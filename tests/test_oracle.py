@@ -226,16 +226,18 @@ def fastmod32(h, p):
     mid = (h0 * m1 + mid) & (2**64 - 1)
     qlo = (h1 * m1 + (mid >> 32)) & 0xFFFFFFFF
     r = (h0 - qlo * p) & 0xFFFFFFFF
-    r = min(r, (r - p) & 0xFFFFFFFF)
-    r = min(r, (r - p) & 0xFFFFFFFF)
-    return r
+    return min(r, (r - p) & 0xFFFFFFFF)  # q = floor(h/P) - {0, 1}: one correction
 
 
 def test_fastmod32_model():
     rng = random.Random(5)
-    for p in (1, 2, 7, 64, 100_003, 2_000_000, 8_388_608, (1 << 30) - 1):
+    for p in (1, 2, 3, 7, 64, 100_003, 2_000_000, 8_388_608, 16_000_000, (1 << 30) - 1):
         vals = [0, 1, p - 1, p, 2**64 - 1, ((2**64 - 1) // p) * p, ((2**64 - 1) // p) * p - 1]
         vals += [rng.getrandbits(64) for _ in range(3000)]
+        # near multiples of P across the range, where q's error is largest
+        for _ in range(300):
+            m = rng.getrandbits(64) // p
+            vals += [m * p + d for d in (-1, 0, 1, p - 1) if 0 <= m * p + d < 2**64]
         for h in vals:
             assert fastmod32(h, p) == h % p, (h, p)
 

@@ -82,6 +82,8 @@ int main() {
   (void)hipMalloc(&clk, 8);
   run<0, 32768, 1024>("add random 32K bins, 1x1024 thr/CU", 1, out, clk);
   run<0, 16384, 512>("add random 16K bins, 2x512 thr/CU", 2, out, clk);
+  run<0, 16384, 1024>("add random 16K bins, 2x1024 thr/CU", 2, out, clk);
+  run<0, 32768, 512>("add random 32K bins, 1x512 thr/CU", 1, out, clk);
   run<1, 32768, 1024>("add conflict-free 32K bins", 1, out, clk);
   run<4, 32768, 1024>("read random 32K bins", 1, out, clk);
   run<2, 32768, 1024>("add_rtn random 32K bins", 1, out, clk);

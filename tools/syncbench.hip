@@ -68,23 +68,25 @@ int main() {
   *flag_h = 0;
   // wall_clock64 runs at 100 MHz on gfx9
   const uint64_t c20 = 2000;  // 20 us
-  hipEvent_t e[4];
+  hipEvent_t e[4], ef[4];
   for (auto &x : e) CK(hipEventCreate(&x));
+  for (auto &x : ef) CK(hipEventCreateWithFlags(&x, hipEventDisableSystemFence));
   // warm
   for (int i = 0; i < 20; ++i) hipLaunchKernelGGL(k_busy, dim3(1024), dim3(64), 0, s, c20, sink);
   CK(hipStreamSynchronize(s));
 
   const int R = 200;
-  // (a) 3 kernels back to back; markers between them vs ext events vs none
-  for (int mode = 0; mode < 3; ++mode) {
+  // (a) 3 kernels back to back; markers between them vs ext events vs none vs
+  // markers from events without the system-scope fence
+  for (int mode = 0; mode < 4; ++mode) {
     std::vector<float> v;
     for (int r = 0; r < R; ++r) {
       CK(hipEventRecord(e[0], s));
       hipLaunchKernelGGL(k_busy, dim3(1024), dim3(64), 0, s, c20, sink);
-      if (mode == 0) {
-        CK(hipEventRecord(e[2], s));
+      if (mode == 0 || mode == 3) {
+        CK(hipEventRecord(mode ? ef[2] : e[2], s));
         hipLaunchKernelGGL(k_busy, dim3(1024), dim3(64), 0, s, c20, sink);
-        CK(hipEventRecord(e[3], s));
+        CK(hipEventRecord(mode ? ef[3] : e[3], s));
       } else if (mode == 1) {
         hipExtLaunchKernelGGL(k_busy, dim3(1024), dim3(64), 0, s, e[2], e[3], 0, c20, sink);
       } else {
@@ -96,10 +98,12 @@ int main() {
       float ms = 0, mid = 0;
       CK(hipEventElapsedTime(&ms, e[0], e[1]));
       if (mode < 2) CK(hipEventElapsedTime(&mid, e[2], e[3]));
+      if (mode == 3) CK(hipEventElapsedTime(&mid, ef[2], ef[3]));
       v.push_back(ms * 1000.f);
       if (r == R - 1)
         printf("(a) mode %s: 3x20us kernels (last mid-kernel event span %.1f us)\n",
-               mode == 0 ? "markers" : mode == 1 ? "ext-events" : "none", mid * 1000.f);
+               mode == 0 ? "markers" : mode == 1 ? "ext-events" : mode == 2 ? "none" : "markers-nofence",
+               mid * 1000.f);
     }
     std::sort(v.begin(), v.end());
     printf("    median span %.1f us, p10 %.1f, p90 %.1f\n", v[R / 2], v[R / 10], v[R * 9 / 10]);
