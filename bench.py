@@ -100,6 +100,9 @@ def main() -> int:
     # test-only: rehearse the multi-rank path on a 1-GPU box (gloo, all ranks on cuda:0)
     ap.add_argument("--dist-backend", default="nccl")
     ap.add_argument("--same-device", action="store_true")
+    # rehearsal: run the multi-rank step (all-reduce, key all-gather, merge)
+    # in a 1-rank process group, to measure its overhead on a 1-GPU box
+    ap.add_argument("--force-dist", action="store_true")
     args = ap.parse_args()
     pool = args.pool
     k = args.k
@@ -109,7 +112,8 @@ def main() -> int:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.same_device:
         local = 0
-    if world > 1:
+    dist_on = world > 1 or args.force_dist
+    if dist_on:
         torch.cuda.set_device(local)
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -130,21 +134,26 @@ def main() -> int:
 
     ctr = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, True, device=local,
                              kmer_width=args.kmer_width)
-    cur_t = torch.as_tensor(_CAI(ctr.device_currents_ptr(), pool), device=dev)
+
+    # one non-default stream for the whole run: the library's kernels, its
+    # events and the collectives all go on it (a NULL stream handle would mean
+    # the library's own stream)
+    run_stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(run_stream)
+    s_handle = run_stream.cuda_stream
 
     def step():
-        s = torch.cuda.current_stream().cuda_stream
+        s = s_handle
         ctr.reset(s, blocking=False)
-        if world == 1:
+        if not dist_on:
             ctr.process_parallel_device(d_bases.data_ptr(), d_offs.data_ptr(), RECS, bases.size, s)
             return
         ctr.accumulate_device(d_bases.data_ptr(), d_offs.data_ptr(), RECS, bases.size, s)
-        # RCCL over xGMI: the u64 currents (int32 on the wire while every rank's
-        # k-mers together stay below 2^31)
-        nkdist.allreduce_currents_(cur_t, total_kmers=world * args.bases)
-        ctr.finalize(False, s)
-        # union of every shard's distinct top-N k-mers: one fixed-size all-gather
-        nkdist.union_top_kmers(ctr)
+        # RCCL over xGMI: the currents as u32 (every rank's k-mers together stay
+        # below 2^31), then LIF + top-N + this shard's top k-mers into a
+        # fixed-size all-gather segment, the union merged on the device: one
+        # host synchronisation per step
+        nkdist.finalize_step(ctr, total_kmers=world * args.bases)
 
     per = float("inf")  # fastest warmup step (the first one allocates)
     for _ in range(max(args.warmup, 1 if args.settle > 0 else 0)):
@@ -159,25 +168,27 @@ def main() -> int:
     settle = 0
     if args.settle > 0:
         settle = min(int(args.settle / max(per, 1e-4)) + 1, 5000)
-        if world > 1:
+        if dist_on:
             t = torch.tensor([settle], dtype=torch.int64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             settle = int(t.item())
         for _ in range(settle):
             step()
         torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
+    marks = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+        marks.append(time.perf_counter())  # host view: each step ends with its readback
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
@@ -218,6 +229,7 @@ def main() -> int:
                          "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(k1_ms, 4),
                          "launches_timed": len(c_ms)},
             "stage_ms": {k2: round(v, 4) for k2, v in timings.items()},
+            "step_ms_host": [round((b - a) * 1e3, 4) for a, b in zip([t0] + marks[:-1], marks)],
             "total_spikes": total_spikes,
         }
         if world == 1 and not args.no_cpu_baseline and k == K and args.kmer_width == 64:
@@ -248,7 +260,7 @@ def main() -> int:
             out["parity_on_cpu_sample"] = parity
         print(json.dumps(out), flush=True)
     ctr.close()
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
     return 0
 

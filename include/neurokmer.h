@@ -114,6 +114,34 @@ int nk_accumulate_device(nk_counter *c, const uint8_t *d_bases,
                          const uint64_t *d_rec_offsets, size_t n_recs,
                          size_t n_bases, void *stream);
 int nk_finalize(nk_counter *c, int streaming_semantics, void *stream);
+/* The same split-phase step with ONE host synchronisation (what
+ * neurokmer_amd/dist.py::finalize_step runs; the caller's collectives go on
+ * `stream` between the calls):
+ *   nk_accumulate_device
+ *   nk_wire32            — this shard's currents as u32 into d_wire[pool_size]
+ *                          (valid while all ranks' k-mers together < 2^31;
+ *                          else all-reduce nk_device_currents as u64 and pass
+ *                          d_wire = NULL below)
+ *   <caller: allreduce(d_wire, pool_size u32, sum)>
+ *   nk_finalize_export   — LIF from the reduced wire vector, top-N, this
+ *                          shard's distinct top k-mers into d_seg[1 + w*cap]
+ *                          ([n | flags << 56, keys...], w = 1, or 2 for 128-bit
+ *                          keys as (lo, hi)); enqueued, no wait
+ *   <caller: allgather(d_seg) -> d_buf[world * stride]>
+ *   nk_merge_export      — union of the segments -> uniques column, results
+ *                          read back (one wait); *redo = 1 when any rank could
+ *                          not export exactly (a full set, an overflowed top
+ *                          bucket, a top-N past the histogram, more than cap
+ *                          keys): every rank then sees the same *redo and
+ *                          calls nk_finalize_redo and the blocking exchange
+ *                          (nk_top_kmers_padded / nk_merge_top_kmers_padded).
+ * Not with opts.exact_counts (NK_E_UNSUPPORTED: use nk_finalize). */
+int nk_wire32(nk_counter *c, uint32_t *d_wire, void *stream);
+int nk_finalize_export(nk_counter *c, int streaming_semantics, const uint32_t *d_wire,
+                       uint64_t *d_seg, size_t cap, void *stream);
+int nk_merge_export(nk_counter *c, const uint64_t *d_buf, size_t world, size_t stride,
+                    size_t cap, int *redo, void *stream);
+int nk_finalize_redo(nk_counter *c, void *stream);
 /* After nk_finalize on a shard: the distinct k-mer keys of this shard that map
  * to the current top-N neurons (device buffer owned by the handle, valid until
  * the next call).  The caller gathers every shard's list and hands the union

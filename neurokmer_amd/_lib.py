@@ -34,7 +34,7 @@ EXPORTS = (
     "nk_energy_used", "nk_set_steps", "nk_get_steps", "nk_pool_size", "nk_k",
     "nk_use_canonical", "nk_copy_currents", "nk_copy_spike_counts", "nk_copy_voltages",
     "nk_copy_refractory", "nk_device_currents", "nk_reset", "nk_reset_async", "nk_last_timings",
-    "nk_count_history",
+    "nk_count_history", "nk_wire32", "nk_finalize_export", "nk_merge_export", "nk_finalize_redo",
     "nk_top_kmers_padded", "nk_merge_top_kmers_padded",
     "nk_exact_owner", "nk_exact_partition", "nk_exact_adopt", "nk_device_kmer_per_neuron",
     "nk_last_error",
@@ -125,6 +125,10 @@ def load(share_torch: bool = True):
         "nk_reset_async": (C.c_int, [vp, vp]),
         "nk_last_timings": (C.c_int, [vp, P(C.c_char_p), P(C.c_float), C.c_int]),
         "nk_count_history": (C.c_int, [vp, P(C.c_float), C.c_int]),
+        "nk_wire32": (C.c_int, [vp, vp, vp]),
+        "nk_finalize_export": (C.c_int, [vp, C.c_int, vp, vp, sz, vp]),
+        "nk_merge_export": (C.c_int, [vp, vp, sz, sz, sz, P(C.c_int), vp]),
+        "nk_finalize_redo": (C.c_int, [vp, vp]),
         "nk_last_error": (C.c_char_p, []),
         "nk_version": (C.c_char_p, []),
     }

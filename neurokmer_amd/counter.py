@@ -63,6 +63,7 @@ class SpikingKmerCounter:
         o.kmer_width = _lib.NK_KMER_128 if kmer_width == 128 else _lib.NK_KMER_COMPAT
         o.exact_counts = 1 if exact_counts else 0
         self.kmer_width = kmer_width
+        self.exact_counts = bool(exact_counts)
         self._h = None
         h = self._L.nk_new(k, threshold, leak, refractory, spike_cost, pool_size,
                            1 if use_canonical else 0, C.byref(o))
@@ -158,6 +159,25 @@ class SpikingKmerCounter:
         check(self._L.nk_merge_top_kmers_padded(self._h, d_buf, world, stride, cap,
                                                 C.byref(ok), stream or None))
         return bool(ok.value)
+
+    # --- multi-GPU step with one host synchronisation (dist.finalize_step) ---
+    def wire32(self, d_wire: int, stream: int = 0) -> None:
+        check(self._L.nk_wire32(self._h, d_wire, stream or None))
+
+    def finalize_export(self, d_wire: int, d_seg: int, cap: int, streaming: bool = False,
+                        stream: int = 0) -> None:
+        check(self._L.nk_finalize_export(self._h, 1 if streaming else 0, d_wire or None, d_seg,
+                                         cap, stream or None))
+
+    def merge_export(self, d_buf: int, world: int, stride: int, cap: int, stream: int = 0) -> bool:
+        """-> True when a redo is needed (the same answer on every rank)."""
+        redo = C.c_int(0)
+        check(self._L.nk_merge_export(self._h, d_buf, world, stride, cap, C.byref(redo),
+                                      stream or None))
+        return bool(redo.value)
+
+    def finalize_redo(self, stream: int = 0) -> None:
+        check(self._L.nk_finalize_redo(self._h, stream or None))
 
     def device_currents_ptr(self) -> int:
         return self._L.nk_device_currents(self._h) or 0

@@ -138,6 +138,20 @@ struct nk_counter {
   DevBuf<uint32_t> w_rec, w_over;
   DevBuf<unsigned long long> w_fill;
   uint32_t pend_slices = 0;  // K1b partials not yet folded into cur (fused into LIF)
+  bool cur_in_wire = false;  // nk_wire32 moved the currents into the caller's wire vector
+  // multi-GPU export (nk_finalize_export -> nk_merge_export -> [nk_finalize_redo])
+  DevBuf<unsigned long long> export_n;  // key counter of k_export_keys (kept zero between uses)
+  bool export_n_zeroed = false;
+  uint64_t *xport_dst = nullptr;  // set while nk_finalize_export enqueues its uniques pass
+  uint64_t xport_cap = 0;
+  // the union of the segments (nk_merge_export), apart from this shard's set
+  DevBuf<unsigned long long> mset_keys;
+  DevBuf<uint64_t> mset_mask_d;
+  DevBuf<uint32_t> muniq, mspecial;
+  uint64_t mset_alloc = 0;
+  bool export_pending = false, export_uniq = false, export_blocking = false, redo_ready = false;
+  uint32_t export_want = 0;
+  ResultHdr last_hdr{};
   bool lif_zeroed = false;   // hist/stats already zeroed by this call's prep kernel
   bool state_fresh = true;   // spikes/v/r are logically zero (lazy reset)
   bool cur_fresh = true;     // currents are logically zero (lazy reset)
@@ -176,6 +190,8 @@ struct nk_counter {
   hipEvent_t ev[kStages + 1] = {};  // see collect_timings
   float stage_ms[kStages] = {};
   int n_stage = 0;
+  hipStream_t last_s = nullptr;  // stream of the previous enqueue (pick_stream)
+  hipEvent_t order_ev = nullptr;
   int timing_pending = 0;  // 0: stage_ms is current; 1/2: collect (without/with count) on demand
   // ev[1]/ev[2] (around the count kernel) rotate through a ring, one pair per
   // accumulate call, so every call's K1 time stays readable (nk_count_history)
@@ -198,8 +214,16 @@ static uint64_t cost_fixed(double cost) {  // Rust `(cost * 1000.0) as u64`
   return (uint64_t)x;
 }
 
+// The stream an entry point enqueues on (NULL: the handle's own stream).  When
+// it differs from the previous call's, it first waits for that stream's work:
+// the calls of one handle stay ordered whatever streams the caller mixes.
 static hipStream_t pick_stream(nk_counter *c, void *s) {
-  return s ? (hipStream_t)s : c->own_stream;
+  hipStream_t t = s ? (hipStream_t)s : c->own_stream;
+  if (c->last_s && c->last_s != t && c->order_ev &&
+      hipEventRecord(c->order_ev, c->last_s) == hipSuccess)
+    (void)hipStreamWaitEvent(t, c->order_ev, 0);
+  c->last_s = t;
+  return t;
 }
 
 // Reset is lazy: the neuron state (spikes, v, r) and the currents are only
@@ -208,6 +232,9 @@ static hipStream_t pick_stream(nk_counter *c, void *s) {
 // kernel; the copy-out / pointer entry points materialise zeros on demand.
 static int zero_state_on(nk_counter *c, hipStream_t) {
   c->total_spikes = c->total_energy = 0;
+  c->pend_slices = 0;
+  c->cur_in_wire = false;
+  c->export_pending = c->redo_ready = false;
   c->top_valid = false;
   c->have_input = false;
   c->state_fresh = true;
@@ -237,10 +264,20 @@ static int materialize(nk_counter *c, bool currents, hipStream_t s) {
   return NK_OK;
 }
 
+// the K1b partials of an nk_accumulate_device not yet folded into the currents
+// (the LIF of nk_finalize folds them itself): for every other reader
+static int fold_pending(nk_counter *c, hipStream_t s) {
+  if (!c->pend_slices) return NK_OK;
+  HIPCHK(launch_partials_add(c->partials.p, c->pend_slices, c->pool, c->cur.p, s));
+  c->pend_slices = 0;
+  return NK_OK;
+}
+
 static int zero_state(nk_counter *c) {
-  int rc = zero_state_on(c, c->own_stream);
+  hipStream_t s = pick_stream(c, nullptr);
+  int rc = zero_state_on(c, s);
   if (rc) return rc;
-  HIPCHK(hipStreamSynchronize(c->own_stream));
+  HIPCHK(hipStreamSynchronize(s));
   c->total_spikes = c->total_energy = 0;
   c->top_valid = false;
   c->have_input = false;
@@ -253,9 +290,14 @@ static int copy_out(nk_counter *c, const DevBuf<T> &b, T *out, size_t n) {
   if (n != c->pool) return fail(NK_E_INVALID, "n (%zu) must equal pool_size (%zu)", n, c->pool);
   if (!n) return NK_OK;
   (void)hipSetDevice(c->device);
-  int rc = materialize(c, (const void *)&b == (const void *)&c->cur, c->own_stream);
+  const bool is_cur = (const void *)&b == (const void *)&c->cur;
+  if (is_cur && c->cur_in_wire)
+    return fail(NK_E_INVALID, "the currents are in the wire vector until nk_finalize_export");
+  hipStream_t s = pick_stream(c, nullptr);
+  int rc = materialize(c, is_cur, s);
   if (rc) return rc;
-  HIPCHK(hipStreamSynchronize(c->own_stream));
+  if (is_cur && (rc = fold_pending(c, s))) return rc;
+  HIPCHK(hipStreamSynchronize(s));
   HIPCHK(hipMemcpy(out, b.p, n * sizeof(T), hipMemcpyDeviceToHost));
   return NK_OK;
 }
@@ -328,7 +370,8 @@ nk_counter *nk_new(size_t k, float threshold, float leak, uint32_t refractory, d
   c->opts = o;
   c->w128 = o.kmer_width == NK_KMER_128;
   c->device = o.device;
-  bool ok = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) == hipSuccess;
+  bool ok = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) == hipSuccess &&
+            hipEventCreateWithFlags(&c->order_ev, hipEventDisableTiming) == hipSuccess;
   // timing-only markers: no system-scope fence (a fenced marker between two
   // kernels writes back L2 and idles the GPU ~2.5 us; tools/syncbench.hip)
   for (int i = 0; ok && i <= kStages; ++i)
@@ -363,6 +406,7 @@ nk_counter *nk_new(size_t k, float threshold, float leak, uint32_t refractory, d
 void nk_free(nk_counter *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
+  if (c->last_s) (void)hipStreamSynchronize(c->last_s);
   if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
   c->cur.release(); c->sc.release(); c->v.release(); c->r.release();
   c->p_off.release(); c->p_pos.release(); c->p_fill.release(); c->p_desc.release();
@@ -377,12 +421,15 @@ void nk_free(nk_counter *c) {
   c->cand.release(); c->top_cur.release(); c->set_keys.release(); c->top_keys.release();
   c->top_keys_n.release(); c->radix_h.release(); c->set_mask_d.release();
   c->set_need_d.release(); c->post_flags.release(); c->hits.release(); c->n_hits.release();
+  c->trunc_d.release(); c->export_n.release();
+  c->mset_keys.release(); c->mset_mask_d.release(); c->muniq.release(); c->mspecial.release();
   if (c->res_h) (void)hipHostFree(c->res_h); c->in_bases.release(); c->in_offs.release();
   for (int i = 0; i <= kStages; ++i)
     if (c->ev[i] && i != 1 && i != 2) (void)hipEventDestroy(c->ev[i]);
   for (auto &pr : c->cnt_ev)
     for (auto &e : pr)
       if (e) (void)hipEventDestroy(e);
+  if (c->order_ev) (void)hipEventDestroy(c->order_ev);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
 }
@@ -561,6 +608,9 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
     return fail(NK_E_INVALID, "pool_size 0 with k-mers present (the reference panics on % 0)");
   (void)hipSetDevice(c->device);
   hipStream_t s = pick_stream(c, stream);
+  c->pend_slices = 0;  // this call zeroes the currents: earlier partials are void
+  c->cur_in_wire = false;
+  c->export_pending = c->redo_ready = false;
   KmerInput in{};
   in.bases = d_bases;
   in.offsets = d_offs;
@@ -625,7 +675,9 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
 
 int nk_accumulate_device(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_offs,
                          size_t n_recs, size_t n_bases, void *stream) {
-  return accumulate(c, d_bases, d_offs, n_recs, n_bases, stream, false);
+  // the partials stay pending: nk_finalize's LIF (or nk_wire32) folds them,
+  // nk_device_currents / nk_copy_currents fold them first
+  return accumulate(c, d_bases, d_offs, n_recs, n_bases, stream, true);
 }
 
 // ---------------------------------------------------------------------------
@@ -663,8 +715,10 @@ static int refine_threshold(nk_counter *c, uint64_t want, uint64_t max_sc, TopSt
 
 // fuse_want > 0: the LIF kernel also selects the top rows and runs the
 // uniques post step (part: the partitioned count's records are used)
+// wire != nullptr: the currents are the (all-reduced) u32 wire vector of
+// nk_wire32; the LIF reads them from it and writes the u64 currents
 static int enqueue_lif(nk_counter *c, int streaming, uint32_t fuse_want, bool part,
-                       hipStream_t s) {
+                       hipStream_t s, const uint32_t *wire = nullptr) {
   LifParams lp;
   lp.steps = c->steps;
   lp.thr = c->thr;
@@ -705,8 +759,15 @@ static int enqueue_lif(nk_counter *c, int streaming, uint32_t fuse_want, bool pa
   c->lif_zeroed = false;
   // steps == 0: the kernel leaves every neuron as it is (streaming returns early,
   // src/spiking_hash.rs:549-551; in-memory runs zero iterations)
-  if ((rc = materialize(c, true, s))) return rc;  // finalize right after a reset
-  HIPCHK(launch_lif_apply(c->cur.p, c->partials.p, c->pend_slices, c->state_fresh ? 1 : 0, c->v.p,
+  if (wire) {
+    c->pend_slices = 0;
+    c->cur_fresh = false;
+    c->cur_in_wire = false;
+  } else if ((rc = materialize(c, true, s))) {  // finalize right after a reset
+    return rc;
+  }
+  HIPCHK(launch_lif_apply(c->cur.p, wire ? wire : c->partials.p, wire ? 1u : c->pend_slices,
+                          wire ? 1 : 0, c->state_fresh ? 1 : 0, c->v.p,
                           c->r.p, c->sc.p, c->pool, lp, c->lif_tbl.p, kLifTable, c->hist.p,
                           c->stats.p, tf, s));
   c->pend_slices = 0;
@@ -743,6 +804,11 @@ static int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, bool post_don
   u.set_mask = c->set_mask_d.p;
   u.uniq = c->uniq.p;
   u.special = c->special.p;
+  if (c->xport_dst) {  // nk_finalize_export: new keys also go to the segment
+    u.xdst = c->xport_dst;
+    u.xn = c->export_n.p;
+    u.xcap = c->xport_cap;
+  }
   if (part) {  // the scan kernel also empties the set
     const uint32_t slices = std::max<uint32_t>(1, 512 / m);
     HIPCHK(launch_part_uniques(c->last_in, (int)c->k, c->canonical, c->last_pa, u, c->tbuckets.p,
@@ -765,9 +831,12 @@ static int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, bool post_don
   return NK_OK;
 }
 
-static int enqueue_readback(nk_counter *c, uint32_t m, bool uniq, hipStream_t s) {
+// flag3: a device word copied into ResultHdr.flags[3] (the merge's reasons to redo)
+static int enqueue_readback(nk_counter *c, uint32_t m, bool uniq, hipStream_t s,
+                            const uint32_t *flag3 = nullptr, const uint32_t *uniq_src = nullptr) {
   HIPCHK(launch_gather(c->topst.p, c->stats.p, uniq ? c->set_mask_d.p : nullptr,
-                       uniq ? c->post_flags.p : nullptr, c->cand.p, uniq ? c->uniq.p : nullptr, m,
+                       uniq ? c->post_flags.p : nullptr, flag3, c->cand.p,
+                       uniq ? (uniq_src ? uniq_src : c->uniq.p) : nullptr, m,
                        c->res_hd, reinterpret_cast<uint64_t *>(c->res_hd + nk_counter::kResFlagOff),
                        ++c->res_seq, s));  // straight into pinned host memory: no copy
   return NK_OK;
@@ -803,16 +872,23 @@ static int wait_readback(nk_counter *c, hipStream_t s) {
 // (a process call with opts.exact_counts) instead of the uniques pass
 static int finish_top(nk_counter *c, uint64_t want, bool fused, bool uniq, bool use_kpn,
                       hipStream_t s);
+static int settle_top(nk_counter *c, uint64_t want, bool uniq, bool use_kpn, bool account,
+                      hipStream_t s);
 
-static int lif_top_uniques(nk_counter *c, int streaming, bool use_kpn, hipStream_t s) {
+static bool top_fused(const nk_counter *c, uint64_t want) {
+  return want && want <= kFuseMaxTopN && lif_blocks(c->pool) <= kFuseMaxBlocks &&
+         c->pool <= (1ull << 24);
+}
+
+static int lif_top_uniques(nk_counter *c, int streaming, bool use_kpn, hipStream_t s,
+                           const uint32_t *wire = nullptr) {
   int rc;
   c->top_keys_ready = false;
   const uint64_t want = std::min<uint64_t>(c->opts.top_n, c->pool);
   const bool uniq = want && c->have_input && c->last_in.n_tiles;
   // top-N selection (and the uniques post step) inside the LIF kernel
-  const bool fused = want && want <= kFuseMaxTopN && lif_blocks(c->pool) <= kFuseMaxBlocks &&
-                     c->pool <= (1ull << 24);
-  if ((rc = enqueue_lif(c, streaming, fused ? (uint32_t)want : 0u, uniq && c->part_used, s)))
+  const bool fused = top_fused(c, want);
+  if ((rc = enqueue_lif(c, streaming, fused ? (uint32_t)want : 0u, uniq && c->part_used, s, wire)))
     return rc;
   HIPCHK(mark(c, 4, s));
   return finish_top(c, want, fused, uniq, use_kpn, s);
@@ -840,12 +916,30 @@ static int finish_top(nk_counter *c, uint64_t want, bool fused, bool uniq, bool 
   if ((rc = enqueue_readback(c, (uint32_t)want, uniq, s))) return rc;
   HIPCHK(mark(c, 6, s));  // may still be pending on return: timings are collected on demand
   if ((rc = wait_readback(c, s))) return rc;
+  return settle_top(c, want, uniq, use_kpn, true, s);
+}
+
+// After the readback in c->res_h: energy (account), the rare corrections
+// (each with its own synchronisation) and c->top.
+static int settle_top(nk_counter *c, uint64_t want, bool uniq, bool use_kpn, bool account,
+                      hipStream_t s) {
+  int rc;
+  auto uniques = [&](bool post_done) -> int {
+    if (!uniq) return NK_OK;
+    if (use_kpn) {
+      HIPCHK(exact_top_uniques(c->cand.p, (uint32_t)want, c->kpn.p, c->uniq.p, s));
+      return NK_OK;
+    }
+    return enqueue_uniques(c, (uint32_t)want, false, post_done, s);
+  };
   const ResultHdr *h = reinterpret_cast<const ResultHdr *>(c->res_h);
   const TopCand *hc = reinterpret_cast<const TopCand *>(c->res_h + sizeof(ResultHdr));
   const uint32_t *hu =
       reinterpret_cast<const uint32_t *>(c->res_h + sizeof(ResultHdr) + want * sizeof(TopCand));
-  c->total_spikes += h->stats[0];
-  c->total_energy += h->stats[0] * cost_fixed(c->cost);
+  if (account) {
+    c->total_spikes += h->stats[0];
+    c->total_energy += h->stats[0] * cost_fixed(c->cost);
+  }
   if (want && h->st.refine) {  // spike counts >= 4095: exact radix refine, redo
     TopState st = h->st;
     if ((rc = refine_threshold(c, want, h->stats[1], st, s))) return rc;
@@ -988,7 +1082,7 @@ static int process_host(nk_counter *c, const uint8_t *bases, const uint64_t *off
     return NK_OK;
   }
   (void)hipSetDevice(c->device);
-  hipStream_t s = c->own_stream;
+  hipStream_t s = pick_stream(c, nullptr);
   if ((rc = c->in_bases.ensure(n_bases + 16))) return rc;
   if ((rc = c->in_offs.ensure(n_recs + 1))) return rc;
   if (n_bases) HIPCHK(hipMemcpyAsync(c->in_bases.p, bases, n_bases, hipMemcpyHostToDevice, s));
@@ -1022,7 +1116,7 @@ static int process_file(nk_counter *c, const char *path, int streaming) {
     if (rc) return fail(rc, "%s", err.c_str());
     return process_host(c, bases.data(), offs.data(), offs.size() - 1, streaming);
   }
-  hipStream_t s = c->own_stream;
+  hipStream_t s = pick_stream(c, nullptr);
   HIPCHK(mark(c, 0, s));
   HIPCHK(mark(c, 1, s));
   HIPCHK(mark(c, 2, s));
@@ -1043,7 +1137,7 @@ int nk_process_file_parallel(nk_counter *c, const char *path) {
 int nk_top_kmers(nk_counter *c, const uint64_t **d_keys, size_t *n_keys) {
   if (!c || !d_keys || !n_keys) return fail(NK_E_INVALID, "null argument");
   (void)hipSetDevice(c->device);
-  hipStream_t s = c->own_stream;
+  hipStream_t s = pick_stream(c, nullptr);
   const uint32_t m = (uint32_t)c->top.size();
   if (!m || !c->set_cap) {
     *d_keys = nullptr;
@@ -1071,40 +1165,16 @@ int nk_top_kmers(nk_counter *c, const uint64_t **d_keys, size_t *n_keys) {
 // uniques column of the top rows from a union of key lists (flat or the
 // fixed-stride all-gather form); *complete = 0 if a segment was truncated
 // (the top rows are then left as they were)
+static int enqueue_merge(nk_counter *c, const MergeSrc &src, uint64_t max_keys, uint32_t m,
+                         hipStream_t s, bool sep = false);
+
 static int merge_keys(nk_counter *c, const MergeSrc &src, uint64_t max_keys, int *complete,
                       hipStream_t s) {
   const uint32_t m = (uint32_t)c->top.size();
   if (complete) *complete = 1;
   if (!m) return NK_OK;
-  uint64_t cap = 64;
-  while (cap < 2 * max_keys + 2) cap <<= 1;
-  int rc;
-  if (cap > c->set_alloc) {
-    if ((rc = c->set_keys.ensure(c->w128 ? 3 * cap : cap))) return rc;
-    c->set_alloc = cap;
-  }
-  if ((rc = c->trunc_d.ensure(1))) return rc;
-  c->set_cap = cap;
-  HIPCHK(launch_set_word(c->set_mask_d.p, cap - 1, s));
-  HIPCHK(c->w128 ? launch_set_fill128(c->set_keys.p, c->set_mask_d.p, c->set_alloc, s)
-                 : launch_set_fill(c->set_keys.p, c->set_mask_d.p, c->set_alloc, s));
-  HIPCHK(hipMemsetAsync(c->uniq.p, 0, m * 4, s));
-  HIPCHK(hipMemsetAsync(c->special.p, 0, m * 4, s));
-  HIPCHK(hipMemsetAsync(c->trunc_d.p, 0, 4, s));
-  UniqArgs u{};
-  u.top = c->cand.p;
-  u.n_top = m;
-  u.tbl_size = (uint32_t)top_tbl_size(m);
-  u.set_keys = c->set_keys.p;
-  u.set_mask = c->set_mask_d.p;
-  u.uniq = c->uniq.p;
-  u.special = c->special.p;
-  MergeSrc ms = src;
-  ms.trunc = c->trunc_d.p;
-  if (c->w128)
-    HIPCHK(launch_set_merge128(ms, c->pool, u, s));
-  else
-    HIPCHK(launch_set_merge(ms, c->pool, u, s));
+  int rc = enqueue_merge(c, src, max_keys, m, s);
+  if (rc) return rc;
   uint32_t *hu = reinterpret_cast<uint32_t *>(c->res_h);
   HIPCHK(hipMemcpyAsync(hu, c->uniq.p, m * 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(hu + m, c->trunc_d.p, 4, hipMemcpyDeviceToHost, s));
@@ -1114,6 +1184,46 @@ static int merge_keys(nk_counter *c, const MergeSrc &src, uint64_t max_keys, int
     return NK_OK;
   }
   for (uint32_t i = 0; i < m; ++i) c->top[i].uniques = hu[i];
+  return NK_OK;
+}
+
+// the set emptied at the capacity max_keys needs, the uniques column zeroed,
+// the merge kernel enqueued (c->trunc_d: bit 0 a truncated segment, bits 1..3
+// the segment header flags).  sep: into the merge set (mset_*, muniq,
+// mspecial), leaving this shard's own set and uniques as they are (a redo
+// still exports them)
+static int enqueue_merge(nk_counter *c, const MergeSrc &src, uint64_t max_keys, uint32_t m,
+                         hipStream_t s, bool sep) {
+  uint64_t cap = 64;
+  while (cap < 2 * max_keys + 2) cap <<= 1;
+  int rc;
+  uint64_t &alloc = sep ? c->mset_alloc : c->set_alloc;
+  DevBuf<unsigned long long> &keys = sep ? c->mset_keys : c->set_keys;
+  if (cap > alloc) {
+    if ((rc = keys.ensure(c->w128 ? 3 * cap : cap))) return rc;
+    alloc = cap;
+  }
+  if ((rc = c->trunc_d.ensure(1)) || (rc = c->mset_mask_d.ensure(1)) ||
+      (rc = c->muniq.ensure(kMaxTopN)) || (rc = c->mspecial.ensure(kMaxTopN)))
+    return rc;
+  uint64_t *mask = sep ? c->mset_mask_d.p : c->set_mask_d.p;
+  uint32_t *uq = sep ? c->muniq.p : c->uniq.p, *sp = sep ? c->mspecial.p : c->special.p;
+  if (!sep) c->set_cap = cap;
+  HIPCHK(launch_merge_prep(keys.p, mask, cap, c->w128 ? 1 : 0, uq, sp, m, c->trunc_d.p, s));
+  UniqArgs u{};
+  u.top = c->cand.p;
+  u.n_top = m;
+  u.tbl_size = (uint32_t)top_tbl_size(m);
+  u.set_keys = keys.p;
+  u.set_mask = mask;
+  u.uniq = uq;
+  u.special = sp;
+  MergeSrc ms = src;
+  ms.trunc = c->trunc_d.p;
+  if (c->w128)
+    HIPCHK(launch_set_merge128(ms, c->pool, u, s));
+  else
+    HIPCHK(launch_set_merge(ms, c->pool, u, s));
   return NK_OK;
 }
 
@@ -1161,6 +1271,137 @@ int nk_merge_top_kmers_padded(nk_counter *c, const uint64_t *d_buf, size_t world
   src.stride = stride;
   src.cap = cap;
   return merge_keys(c, src, (uint64_t)world * cap, complete, pick_stream(c, stream));
+}
+
+// ---------------------------------------------------------------------------
+// Multi-GPU step with one host synchronisation (neurokmer_amd/dist.py::
+// finalize_step):  nk_accumulate_device -> nk_wire32 -> allreduce(wire, u32)
+// -> nk_finalize_export -> allgather(segments) -> nk_merge_export
+// [-> redo: nk_finalize_redo + the blocking key exchange]
+// ---------------------------------------------------------------------------
+int nk_wire32(nk_counter *c, uint32_t *d_wire, void *stream) {
+  if (!c || (!d_wire && c->pool)) return fail(NK_E_INVALID, "null argument");
+  if (c->cur_in_wire) return fail(NK_E_INVALID, "nk_wire32 twice without nk_finalize_export");
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  int rc = materialize(c, true, s);
+  if (rc) return rc;
+  // partitioned count with its partials pending: only overflowed buckets added into cur
+  const uint32_t *over = (c->pend_slices && c->part_used) ? c->p_over.p : nullptr;
+  HIPCHK(launch_wire32(c->cur.p, c->partials.p, c->pend_slices, over, c->pool, d_wire, s));
+  c->pend_slices = 0;
+  c->cur_in_wire = true;
+  return NK_OK;
+}
+
+int nk_finalize_export(nk_counter *c, int streaming, const uint32_t *d_wire, uint64_t *d_seg,
+                       size_t cap, void *stream) {
+  if (!c || !d_seg) return fail(NK_E_INVALID, "null argument");
+  if (c->cur_in_wire != (d_wire != nullptr))
+    return fail(NK_E_INVALID, d_wire ? "d_wire without nk_wire32" : "the currents are in the wire vector: pass it");
+  if (cap > (1ull << 40)) return fail(NK_E_INVALID, "cap too large");
+  const bool use_kpn = c->opts.exact_counts && c->exact_built && c->kpn_global;
+  if (use_kpn)
+    return fail(NK_E_UNSUPPORTED, "exact table: the uniques come from kmer_per_neuron (nk_finalize)");
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  HIPCHK(mark(c, 7, s));
+  c->top_keys_ready = false;
+  c->top_valid = false;
+  c->redo_ready = false;
+  const uint64_t want = std::min<uint64_t>(c->opts.top_n, c->pool);
+  const bool uniq = want && c->have_input && c->last_in.n_tiles;
+  int rc;
+  if ((rc = c->export_n.ensure(1))) return rc;
+  if (!c->export_n_zeroed) {
+    HIPCHK(hipMemsetAsync(c->export_n.p, 0, 8, s));
+    c->export_n_zeroed = true;
+  }
+  const bool fused = top_fused(c, want);
+  if (fused) {  // enqueue only: the host waits once, in nk_merge_export
+    if ((rc = enqueue_lif(c, streaming, (uint32_t)want, uniq && c->part_used, s, d_wire))) return rc;
+    HIPCHK(mark(c, 4, s));
+    HIPCHK(mark(c, 5, s));
+    c->xport_dst = d_seg;  // the pass appends each new key to the segment
+    c->xport_cap = cap;
+    rc = uniq ? enqueue_uniques(c, (uint32_t)want, false, true, s) : NK_OK;
+    c->xport_dst = nullptr;
+    if (rc) return rc;
+  } else if ((rc = lif_top_uniques(c, streaming, false, s, d_wire))) {  // blocking, corrected
+    return rc;
+  }
+  HIPCHK(launch_export(c->set_keys.p, c->set_mask_d.p, c->set_alloc, c->w128 ? 1 : 0, uniq,
+                       fused, c->special.p, (uint32_t)want, want ? c->topst.p : nullptr,
+                       c->post_flags.p, cap, d_seg, c->export_n.p, s));
+  c->export_pending = true;
+  c->export_blocking = !fused;
+  c->export_want = (uint32_t)want;
+  c->export_uniq = uniq;
+  return NK_OK;
+}
+
+int nk_merge_export(nk_counter *c, const uint64_t *d_buf, size_t world, size_t stride, size_t cap,
+                    int *redo, void *stream) {
+  if (!c || !d_buf || !redo) return fail(NK_E_INVALID, "null argument");
+  if (!c->export_pending) return fail(NK_E_INVALID, "nk_finalize_export first");
+  if (!world || world > (1u << 20) || stride < 1 + (c->w128 ? 2 : 1) * cap)
+    return fail(NK_E_INVALID, "bad all-gather layout (world %zu, stride %zu, cap %zu)", world,
+                stride, cap);
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  c->export_pending = false;
+  const uint32_t want = c->export_want;
+  int rc;
+  if ((rc = c->trunc_d.ensure(1))) return rc;
+  if (want) {
+    MergeSrc src{};
+    src.keys = d_buf;
+    src.world = (uint32_t)world;
+    src.stride = stride;
+    src.cap = cap;
+    if ((rc = enqueue_merge(c, src, (uint64_t)world * cap, want, s, true))) return rc;
+  }
+  if ((rc = enqueue_readback(c, want, want != 0, s, want ? c->trunc_d.p : nullptr,
+                             want ? c->muniq.p : nullptr)))
+    return rc;
+  HIPCHK(mark(c, 6, s));
+  if ((rc = wait_readback(c, s))) return rc;
+  const ResultHdr *h = reinterpret_cast<const ResultHdr *>(c->res_h);
+  const TopCand *hc = reinterpret_cast<const TopCand *>(c->res_h + sizeof(ResultHdr));
+  const uint32_t *hu =
+      reinterpret_cast<const uint32_t *>(c->res_h + sizeof(ResultHdr) + want * sizeof(TopCand));
+  if (!c->export_blocking) {  // the blocking export already counted its spikes
+    c->total_spikes += h->stats[0];
+    c->total_energy += h->stats[0] * cost_fixed(c->cost);
+  }
+  c->top.resize(want);
+  for (uint32_t i = 0; i < want; ++i) {
+    c->top[i].idx = hc[i].idx;
+    c->top[i].spikes = hc[i].sc;
+    c->top[i].uniques = hu[i];
+    c->top[i]._pad = 0;
+  }
+  c->set_cap = c->export_uniq ? h->mask + 1 : 0;  // this shard's set (the merge used its own)
+  *redo = (want && h->flags[3]) ? 1 : 0;
+  c->redo_ready = *redo != 0;
+  c->top_valid = !*redo;
+  collect_timings(c, c->have_input);
+  return NK_OK;
+}
+
+int nk_finalize_redo(nk_counter *c, void *stream) {
+  if (!c) return fail(NK_E_INVALID, "null counter");
+  if (!c->redo_ready) return fail(NK_E_INVALID, "no nk_merge_export asked for a redo");
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  c->redo_ready = false;
+  // c->res_h holds the merge readback: this rank's TopState and flags[0..2]
+  int rc = settle_top(c, c->export_want, c->export_uniq, false, false, s);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(s));
+  c->top_keys_ready = false;
+  c->top_valid = true;
+  return NK_OK;
 }
 
 long nk_top_abundant_neurons(nk_counter *c, size_t n, nk_top_row *out) {
@@ -1344,7 +1585,7 @@ static int ingest_file(nk_counter *c, const char *path, bool *fallback) {
   int rc = src.open(path, err);
   if (rc) return fail(rc, "%s", err.c_str());
   (void)hipSetDevice(c->device);
-  hipStream_t s = c->own_stream;
+  hipStream_t s = pick_stream(c, nullptr);
   // two pinned host buffers: [room for a FASTQ carry | chunk]; the reader
   // thread fills one while the device copies and parses the other
   size_t chunk = ingest_chunk_bytes();
@@ -1493,7 +1734,10 @@ int nk_process_sequence(nk_counter *c, const uint8_t *seq, size_t len) {
   if (c->pool == 0)
     return fail(NK_E_INVALID, "pool_size 0 with k-mers present (the reference panics on % 0)");
   (void)hipSetDevice(c->device);
-  hipStream_t s = c->own_stream;
+  hipStream_t s = pick_stream(c, nullptr);
+  if (c->cur_in_wire)
+    return fail(NK_E_INVALID, "the currents are in the wire vector until nk_finalize_export");
+  if ((rc = materialize(c, true, s)) || (rc = fold_pending(c, s))) return rc;
   if ((rc = c->in_bases.ensure(len + 16)) || (rc = c->in_offs.ensure(2)) ||
       (rc = c->x_n.ensure(2)) || (rc = c->kpn.ensure(c->pool)))
     return rc;
@@ -1553,7 +1797,7 @@ int nk_get_counts(nk_counter *c, const uint64_t *kmers, size_t n, uint32_t *out,
     return NK_OK;
   }
   (void)hipSetDevice(c->device);
-  hipStream_t s = c->own_stream;
+  hipStream_t s = pick_stream(c, nullptr);
   if ((rc = c->x_q.ensure(n)) || (rc = c->x_out.ensure(n)) || (rc = c->x_pres.ensure(n)))
     return rc;
   HIPCHK(hipMemcpyAsync(c->x_q.p, kmers, n * 8, hipMemcpyHostToDevice, s));
@@ -1580,7 +1824,7 @@ long nk_distinct_kmers(nk_counter *c) {
   int rc = need_exact(c);
   if (rc) return rc;
   (void)hipSetDevice(c->device);
-  HIPCHK(hipStreamSynchronize(c->own_stream));
+  HIPCHK(hipStreamSynchronize(pick_stream(c, nullptr)));
   unsigned long long n = 0, m[2] = {0, 0};
   if (c->exact_built) HIPCHK(hipMemcpy(&n, c->x_n.p + 1, 8, hipMemcpyDeviceToHost));
   if (!c->d_dirty) HIPCHK(hipMemcpy(m, c->d_meta.p, 16, hipMemcpyDeviceToHost));
@@ -1680,7 +1924,7 @@ int nk_copy_kmer_per_neuron(nk_counter *c, uint32_t *out, size_t n) {
     return NK_OK;
   }
   (void)hipSetDevice(c->device);
-  HIPCHK(hipStreamSynchronize(c->own_stream));
+  HIPCHK(hipStreamSynchronize(pick_stream(c, nullptr)));
   HIPCHK(hipMemcpy(out, c->kpn.p, n * 4, hipMemcpyDeviceToHost));
   return NK_OK;
 }
@@ -1698,10 +1942,14 @@ size_t nk_k(const nk_counter *c) { return c ? c->k : 0; }
 int nk_use_canonical(const nk_counter *c) { return c ? c->canonical : 0; }
 uint64_t *nk_device_currents(nk_counter *c) {
   if (!c) return nullptr;
-  if (c->cur_fresh) {  // lazily-reset currents: zero them before handing them out
+  if (c->cur_in_wire) {
+    fail(NK_E_INVALID, "the currents are in the wire vector until nk_finalize_export");
+    return nullptr;
+  }
+  if (c->cur_fresh || c->pend_slices) {  // lazily-reset currents / K1b partials pending
     (void)hipSetDevice(c->device);
-    if (materialize(c, true, c->own_stream) ||
-        hipStreamSynchronize(c->own_stream) != hipSuccess)
+    hipStream_t s = pick_stream(c, nullptr);
+    if (materialize(c, true, s) || fold_pending(c, s) || hipStreamSynchronize(s) != hipSuccess)
       return nullptr;
   }
   return c->cur.p;

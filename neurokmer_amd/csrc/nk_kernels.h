@@ -140,7 +140,7 @@ struct MergeSrc {
   uint32_t world;      // segments (0: flat)
   uint64_t stride;     // u64 words per segment
   uint64_t cap;        // keys stored per segment
-  uint32_t *trunc;     // set when a segment's n_r > cap
+  uint32_t *trunc;     // bit 0: a segment's n_r > cap; bits 1..3: the header flags of any segment
 };
 
 struct UniqArgs {
@@ -151,6 +151,12 @@ struct UniqArgs {
   const uint64_t *set_mask;      // device word: capacity - 1
   uint32_t *uniq;      // per top row: distinct keys
   uint32_t *special;   // per top row: key == ~0 seen
+  // multi-GPU export (nk_finalize_export): every key the set takes for the
+  // first time is also appended to xdst[1 + w*i] (w u64 words per key, i < xcap
+  // kept; *xn counts them all) -- the all-gather segment, without a set scan
+  uint64_t *xdst;
+  unsigned long long *xn;
+  uint64_t xcap;
 };
 
 hipError_t launch_tile_rec(const KmerInput &in, uint64_t tile_size, uint32_t *tile_rec,
@@ -164,6 +170,7 @@ hipError_t launch_lif_table(LifEntry *tbl, int n, LifParams lp, hipStream_t s);
 // first (the fused K1c of a single-device process call) and is written back.
 // fresh: v/r/sc are taken as 0 (lazy reset) and every neuron is written.
 hipError_t launch_lif_apply(uint64_t *currents, const uint32_t *partials, uint32_t slices,
+                            int cur_zero,
                             int fresh, float *v, uint32_t *r, uint64_t *sc, uint64_t pool, LifParams lp,
                             const LifEntry *tbl, int tbl_n, uint32_t *hist, uint64_t *stats,
                             const TopFuse &tf, hipStream_t s);
@@ -202,9 +209,20 @@ hipError_t launch_set_word(uint64_t *w, uint64_t v, hipStream_t s);
 hipError_t launch_prep(const KmerInput &in, uint64_t tile_size, uint32_t *tile_rec,
                        const ZeroList &z, hipStream_t s);
 hipError_t launch_zero(const ZeroList &z, hipStream_t s);
+hipError_t launch_merge_prep(unsigned long long *set_keys, uint64_t *mask, uint64_t cap, int w128,
+                             uint32_t *uniq, uint32_t *special, uint32_t m, uint32_t *trunc,
+                             hipStream_t s);
+hipError_t launch_wire32(const uint64_t *cur, const uint32_t *partials, uint32_t slices,
+                         const uint32_t *over, uint64_t pool, uint32_t *wire, hipStream_t s);
+hipError_t launch_export(const unsigned long long *set_keys, const uint64_t *set_mask,
+                         uint64_t set_alloc, int w128, bool uniq, bool appended,
+                         const uint32_t *special, uint32_t n_top, const TopState *st,
+                         const uint32_t *post_flags, uint64_t cap_out, uint64_t *dst,
+                         unsigned long long *count, hipStream_t s);
 hipError_t launch_gather(const TopState *st, const uint64_t *stats, const uint64_t *mask,
-                         const uint32_t *flags, const TopCand *cand, const uint32_t *uniq,
-                         uint32_t m, uint8_t *out, uint64_t *done, uint64_t seq, hipStream_t s);
+                         const uint32_t *flags, const uint32_t *flag3, const TopCand *cand,
+                         const uint32_t *uniq, uint32_t m, uint8_t *out, uint64_t *done,
+                         uint64_t seq, hipStream_t s);
 hipError_t launch_set_compact(const unsigned long long *keys, uint64_t cap, const uint32_t *special,
                               uint32_t n_top, const TopCand *top, uint64_t pool,
                               uint64_t *out, unsigned long long *count, hipStream_t s);

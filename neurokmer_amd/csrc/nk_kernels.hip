@@ -96,6 +96,10 @@ __device__ __forceinline__ void set_insert(const UniqArgs &u, uint32_t slot, uin
       unsigned long long prev = atomicCAS(&u.set_keys[h], kEmpty, (unsigned long long)key);
       if (prev == kEmpty) {
         atomicAdd(&u.uniq[slot], 1u);
+        if (u.xdst) {
+          const unsigned long long at = atomicAdd(u.xn, 1ull);
+          if (at < u.xcap) u.xdst[1 + at] = key;
+        }
         return;
       }
       if (prev == key) return;
@@ -248,6 +252,13 @@ __device__ __forceinline__ void set_insert128(const UniqArgs &u, uint32_t slot, 
         __hip_atomic_store(&S[3 * h + 2], (unsigned long long)w[2], __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
         atomicAdd(&u.uniq[slot], 1u);
+        if (u.xdst) {
+          const unsigned long long at = atomicAdd(u.xn, 1ull);
+          if (at < u.xcap) {
+            u.xdst[1 + 2 * at] = key.lo;
+            u.xdst[2 + 2 * at] = key.hi;
+          }
+        }
         return;
       }
       cur = prev;
@@ -359,8 +370,11 @@ __device__ __forceinline__ bool merge_src_key(const MergeSrc &m, uint64_t i, int
   }
   const uint64_t r = i / m.cap, j = i - r * m.cap;
   const uint64_t *seg = m.keys + r * m.stride;
-  const uint64_t nr = seg[0];
-  if (j == 0 && nr > m.cap) *m.trunc = 1u;
+  const uint64_t nr = seg[0] & ((1ull << 56) - 1);
+  if (j == 0) {
+    const uint32_t why = (nr > m.cap ? 1u : 0u) | (uint32_t)(seg[0] >> 56) << 1;
+    if (why) atomicOr(m.trunc, why);
+  }
   if (j >= nr) return false;
   *at = seg + 1 + (uint64_t)wpk * j;
   return true;
@@ -1123,6 +1137,7 @@ __device__ void defer_to_host(const TopFuse &tf) {
   tf.st->refine = 1u;
   for (int i = 0; i < 4; ++i) tf.post.flags[i] = 0;
   *tf.post.n_hits = 0;
+  if (tf.post.set_mask) *tf.post.set_mask = 0;  // the (idle) uniques pass clears one slot
 }
 
 // The final selection over the blocks' candidate lists C (one block of
@@ -1293,7 +1308,7 @@ __device__ void final_top(uint64_t pool, const uint64_t *currents, uint32_t nb,
 
 __global__ __launch_bounds__(kLifBlock) void k_lif_apply(uint64_t *__restrict__ currents,
                                                       const uint32_t *__restrict__ partials,
-                                                      uint32_t slices, int fresh,
+                                                      uint32_t slices, int cur_zero, int fresh,
                                                       float *__restrict__ V,
                                                       uint32_t *__restrict__ R,
                                                       uint64_t *__restrict__ SC, uint64_t pool,
@@ -1321,7 +1336,7 @@ __global__ __launch_bounds__(kLifBlock) void k_lif_apply(uint64_t *__restrict__ 
 #pragma unroll
   for (int j = 0; j < kLifPerThread; ++j) {
     const uint64_t i = idx_of(j);
-    cntv[j] = currents[i];
+    cntv[j] = cur_zero ? 0ull : currents[i];  // cur_zero: the partials (wire) hold it all
     scv[j] = fresh ? 0 : SC[i];
     vin[j] = fresh ? 0.0f : V[i];
     rin[j] = fresh ? 0u : R[i];
@@ -1649,6 +1664,129 @@ __global__ void k_pad_keys(const uint64_t *__restrict__ src, const unsigned long
 }
 
 // ---------------------------------------------------------------------------
+// Multi-GPU step with one host synchronisation (neurokmer_amd/dist.py::
+// finalize_step): the currents cross the wire as u32, the LIF reads them back
+// from the reduced wire vector, and this shard's distinct top k-mers go
+// straight into its all-gather segment [hdr, keys...] with hdr = n | flags << 56
+// (flags: 1 set too small, 2 top bucket overflowed, 4 top-N deferred to the
+// host refine), so every rank sees every rank's reasons to redo the slow way.
+// ---------------------------------------------------------------------------
+// over != nullptr (partitioned count): the zeroed currents only hold the
+// direct adds of overflowed buckets, so only those buckets are read
+__global__ void k_wire32(const uint64_t *__restrict__ cur, const uint32_t *__restrict__ partials,
+                         uint32_t slices, const uint32_t *__restrict__ over, uint64_t pool,
+                         uint32_t *__restrict__ wire) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < pool;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t x = (!over || over[i >> kBinBits]) ? cur[i] : 0ull;
+    for (uint32_t r = 0; r < slices; ++r) x += partials[(uint64_t)r * pool + i];
+    wire[i] = (uint32_t)x;
+  }
+}
+
+__global__ void k_export_keys(const unsigned long long *__restrict__ S,
+                              const uint64_t *__restrict__ set_mask, int w128, uint64_t cap_out,
+                              uint64_t *__restrict__ dst, unsigned long long *__restrict__ count) {
+  const uint64_t n = *set_mask + 1;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    if (w128) {
+      const unsigned long long w0 = S[3 * i];
+      if (!w0) continue;
+      const Key128 k = words_key128(w0, S[3 * i + 1], S[3 * i + 2]);
+      const unsigned long long at = atomicAdd(count, 1ull);
+      if (at < cap_out) {
+        dst[1 + 2 * at] = k.lo;
+        dst[2 + 2 * at] = k.hi;
+      }
+    } else {
+      const unsigned long long kk = S[i];
+      if (kk == kEmpty) continue;
+      const unsigned long long at = atomicAdd(count, 1ull);
+      if (at < cap_out) dst[1 + at] = kk;
+    }
+  }
+}
+
+__global__ void k_export_hdr(unsigned long long *__restrict__ count, const uint32_t *__restrict__ special,
+                             uint32_t n_top, const TopState *__restrict__ st,
+                             const uint32_t *__restrict__ post_flags, int w128, uint64_t cap_out,
+                             uint64_t *__restrict__ dst) {
+  uint64_t n = *count;
+  *count = 0;  // ready for the next export
+  uint64_t flags = (st && st->refine) ? 4u : 0u;
+  if (post_flags) flags |= (post_flags[0] ? 1u : 0u) | (post_flags[1] ? 2u : 0u);
+  if (!w128 && post_flags && !(st && st->refine)) {  // the kEmpty key lives outside the set
+    bool any = false;
+    for (uint32_t s = 0; s < n_top; ++s) any |= special[s] != 0;
+    if (any) {
+      if (n < cap_out) dst[1 + n] = kEmpty;
+      ++n;
+    }
+  }
+  dst[0] = n | (flags << 56);
+}
+
+// Everything a merge starts from, in one launch: the set emptied at capacity
+// cap (3 words per key for 128-bit keys), its mask word, the uniques column,
+// the kEmpty flags and the truncation word zeroed.
+__global__ void k_merge_prep(unsigned long long *__restrict__ S, uint64_t *__restrict__ mask,
+                             uint64_t cap, int w128, uint32_t *__restrict__ uniq,
+                             uint32_t *__restrict__ special, uint32_t m, uint32_t *__restrict__ trunc) {
+  const uint64_t n = w128 ? 3 * cap : cap;
+  const unsigned long long fill = w128 ? 0ull : kEmpty;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    S[i] = fill;
+  if (blockIdx.x == 0) {
+    for (uint32_t t = threadIdx.x; t < m; t += blockDim.x) {
+      uniq[t] = 0;
+      special[t] = 0;
+    }
+    if (threadIdx.x == 0) {
+      *mask = cap - 1;
+      *trunc = 0;
+    }
+  }
+}
+
+hipError_t launch_merge_prep(unsigned long long *set_keys, uint64_t *mask, uint64_t cap, int w128,
+                             uint32_t *uniq, uint32_t *special, uint32_t m, uint32_t *trunc,
+                             hipStream_t s) {
+  unsigned g = (unsigned)(((w128 ? 3 : 1) * cap + 255) / 256);
+  if (g > 2048) g = 2048;
+  if (!g) g = 1;
+  hipLaunchKernelGGL(k_merge_prep, dim3(g), dim3(256), 0, s, set_keys, mask, cap, w128, uniq, special,
+                     m, trunc);
+  return hipGetLastError();
+}
+
+hipError_t launch_wire32(const uint64_t *cur, const uint32_t *partials, uint32_t slices,
+                         const uint32_t *over, uint64_t pool, uint32_t *wire, hipStream_t s) {
+  if (!pool) return hipSuccess;
+  unsigned g = (unsigned)((pool + 255) / 256);
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(k_wire32, dim3(g), dim3(256), 0, s, cur, partials, slices, over, pool, wire);
+  return hipGetLastError();
+}
+
+hipError_t launch_export(const unsigned long long *set_keys, const uint64_t *set_mask,
+                         uint64_t set_alloc, int w128, bool uniq, bool appended,
+                         const uint32_t *special, uint32_t n_top, const TopState *st,
+                         const uint32_t *post_flags, uint64_t cap_out, uint64_t *dst,
+                         unsigned long long *count, hipStream_t s) {
+  if (uniq && !appended) {  // scan the set; grid for the largest capacity, blocks past *set_mask + 1 idle
+    unsigned g = (unsigned)((set_alloc + 255) / 256);
+    if (g > 1024) g = 1024;
+    hipLaunchKernelGGL(k_export_keys, dim3(g), dim3(256), 0, s, set_keys, set_mask, w128, cap_out,
+                       dst, count);
+  }
+  hipLaunchKernelGGL(k_export_hdr, dim3(1), dim3(1), 0, s, count, special, n_top, st,
+                     uniq ? post_flags : nullptr, w128, cap_out, dst);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
 uint64_t n_tiles_for(uint64_t n_bases, uint64_t tile) { return (n_bases + tile - 1) / tile; }
@@ -1709,14 +1847,14 @@ uint32_t lif_blocks(uint64_t pool) {
 }
 
 hipError_t launch_lif_apply(uint64_t *currents, const uint32_t *partials, uint32_t slices,
-                            int fresh, float *v, uint32_t *r, uint64_t *sc, uint64_t pool, LifParams lp,
+                            int cur_zero, int fresh, float *v, uint32_t *r, uint64_t *sc, uint64_t pool, LifParams lp,
                             const LifEntry *tbl, int tbl_n, uint32_t *hist, uint64_t *stats,
                             const TopFuse &tf, hipStream_t s) {
   if (!pool) return hipSuccess;
   const unsigned g = lif_blocks(pool);
   if (tf.want && (tf.want > kFuseMaxTopN || g > kFuseMaxBlocks || pool > (1ull << 24)))
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_lif_apply, dim3(g), dim3(kLifBlock), 0, s, currents, partials, slices, fresh,
+  hipLaunchKernelGGL(k_lif_apply, dim3(g), dim3(kLifBlock), 0, s, currents, partials, slices, cur_zero, fresh,
                      v, r, sc, pool, lp, tbl, tbl_n, hist, (unsigned long long *)stats, tf);
   if (tf.want)
     hipLaunchKernelGGL(k_top_final, dim3(1), dim3(kLifBlock), 0, s, pool, currents, g, tf);
@@ -2020,8 +2158,9 @@ hipError_t launch_zero(const ZeroList &z, hipStream_t s) {
 // after all of them; the kernel touches no memory after it.
 __global__ void k_gather(const TopState *__restrict__ st, const uint64_t *__restrict__ stats,
                          const uint64_t *__restrict__ mask, const uint32_t *__restrict__ flags,
-                         const TopCand *__restrict__ cand, const uint32_t *__restrict__ uniq,
-                         uint32_t m, uint8_t *__restrict__ out, uint64_t *done, uint64_t seq) {
+                         const uint32_t *__restrict__ flag3, const TopCand *__restrict__ cand,
+                         const uint32_t *__restrict__ uniq, uint32_t m, uint8_t *__restrict__ out,
+                         uint64_t *done, uint64_t seq) {
   ResultHdr *h = reinterpret_cast<ResultHdr *>(out);
   TopCand *c = reinterpret_cast<TopCand *>(out + sizeof(ResultHdr));
   uint32_t *u = reinterpret_cast<uint32_t *>(out + sizeof(ResultHdr) + (size_t)m * sizeof(TopCand));
@@ -2031,6 +2170,7 @@ __global__ void k_gather(const TopState *__restrict__ st, const uint64_t *__rest
     h->stats[1] = stats[1];
     h->mask = mask ? *mask : 0;
     for (int i = 0; i < 4; ++i) h->flags[i] = flags ? flags[i] : 0;
+    if (flag3) h->flags[3] = *flag3;
   }
   for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
     c[i] = cand[i];
@@ -2042,10 +2182,11 @@ __global__ void k_gather(const TopState *__restrict__ st, const uint64_t *__rest
 }
 
 hipError_t launch_gather(const TopState *st, const uint64_t *stats, const uint64_t *mask,
-                         const uint32_t *flags, const TopCand *cand, const uint32_t *uniq,
-                         uint32_t m, uint8_t *out, uint64_t *done, uint64_t seq, hipStream_t s) {
-  hipLaunchKernelGGL(k_gather, dim3(1), dim3(1024), 0, s, st, stats, mask, flags, cand, uniq, m, out,
-                     done, seq);
+                         const uint32_t *flags, const uint32_t *flag3, const TopCand *cand,
+                         const uint32_t *uniq, uint32_t m, uint8_t *out, uint64_t *done,
+                         uint64_t seq, hipStream_t s) {
+  hipLaunchKernelGGL(k_gather, dim3(1), dim3(1024), 0, s, st, stats, mask, flags, flag3, cand, uniq, m,
+                     out, done, seq);
   return hipGetLastError();
 }
 

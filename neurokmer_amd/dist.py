@@ -82,6 +82,82 @@ def allreduce_currents_(t, group=None, total_kmers=None) -> None:
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
 
 
+def finalize_step(ctr, group=None, total_kmers=None, cap: int = 4096,
+                  streaming: bool = False) -> None:
+    """After every rank's ctr.accumulate_device: the whole multi-GPU finish with
+    ONE host synchronisation (include/neurokmer.h, nk_finalize_export):
+
+      wire = this shard's currents as u32   (nk_wire32; u64 all-reduce when
+                                             total_kmers is unknown or >= 2^31)
+      all-reduce(wire)                      RCCL over xGMI
+      LIF + top-N + uniques of this shard, its distinct top k-mers into a
+      fixed-size segment                    (nk_finalize_export, enqueued)
+      all-gather(segments)
+      union -> uniques column, one readback (nk_merge_export)
+
+    If any rank could not export exactly (the segment headers carry the
+    reasons, so every rank decides alike) all ranks redo the slow way:
+    nk_finalize_redo + union_top_kmers.  With the exact k-mer table the
+    uniques come from kmer_per_neuron: plain finalize."""
+    import torch
+    import torch.distributed as dist
+    if torch.cuda.current_stream().cuda_stream == 0:
+        # the library reads a NULL stream as its own stream: run the step on a
+        # real torch stream so the collectives and our kernels share one order
+        _on_side_stream(ctr, lambda: finalize_step(ctr, group, total_kmers, cap, streaming))
+        return
+    if getattr(ctr, "exact_counts", False):  # (after exchange_exact_table)
+        cur = _dev_view(ctr.device_currents_ptr(), ctr.pool_size, "<i8",
+                        torch.device("cuda", torch.cuda.current_device()))
+        allreduce_currents_(cur, group=group, total_kmers=total_kmers)
+        ctr.finalize(streaming)
+        return
+    world = dist.get_world_size(group)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    stream = torch.cuda.current_stream().cuda_stream
+    bufs = ctr.__dict__.setdefault("_dist_bufs", {})
+    pool = ctr.pool_size
+    wire_ptr = 0
+    if total_kmers is not None and 0 <= total_kmers < (1 << 31):
+        wire = bufs.get("wire")
+        if wire is None or wire.numel() != max(pool, 1) or wire.device != dev:
+            wire = bufs["wire"] = torch.empty(max(pool, 1), dtype=torch.int32, device=dev)
+        ctr.wire32(wire.data_ptr(), stream)
+        if pool:
+            dist.all_reduce(wire[:pool], op=dist.ReduceOp.SUM, group=group)
+        wire_ptr = wire.data_ptr()
+    else:
+        cur = _dev_view(ctr.device_currents_ptr(), pool, "<i8", dev)
+        allreduce_currents_(cur, group=group)
+    wpk = 2 if getattr(ctr, "kmer_width", 64) == 128 else 1
+    stride = 1 + wpk * cap
+    key = ("seg", world, stride)
+    if key not in bufs:
+        bufs[key] = (torch.empty(stride, dtype=torch.int64, device=dev),
+                     torch.empty(world * stride, dtype=torch.int64, device=dev))
+    seg, allb = bufs[key]
+    ctr.finalize_export(wire_ptr, seg.data_ptr(), cap, streaming, stream)
+    _all_gather_into(allb, seg, group=group)
+    if ctr.merge_export(allb.data_ptr(), world, stride, cap, stream):
+        ctr.finalize_redo(stream)
+        union_top_kmers(ctr, group=group, cap=cap)
+
+
+def _on_side_stream(ctr, fn):
+    """Run fn with a cached non-default torch stream current (ordered after the
+    caller's stream, and the caller's after it)."""
+    import torch
+    bufs = ctr.__dict__.setdefault("_dist_bufs", {})
+    side = bufs.get("side")
+    if side is None:
+        side = bufs["side"] = torch.cuda.Stream()
+    cur = torch.cuda.current_stream()
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        fn()
+    cur.wait_stream(side)
+
+
 def _all_gather_into(out, inp, group=None):
     """all_gather_into_tensor; with gloo the device tensors go through host memory."""
     import torch.distributed as dist
@@ -101,6 +177,9 @@ def union_top_kmers(ctr, group=None, cap: int = 4096) -> None:
     rank sees the same headers) all ranks fall back to the variable-length
     exchange (gather_union)."""
     import torch
+    if torch.cuda.current_stream().cuda_stream == 0:
+        _on_side_stream(ctr, lambda: union_top_kmers(ctr, group, cap))
+        return
     world = torch.distributed.get_world_size(group)
     dev = torch.device("cuda", torch.cuda.current_device())
     stream = torch.cuda.current_stream().cuda_stream

@@ -149,3 +149,89 @@ def test_two_ranks_union_of_top_kmers(width, cap):
     top = ref.top_abundant_neurons(20)
     for _, t in res:
         assert t == top
+
+
+SKEW_POOL = 200_003  # 7 buckets of 32768 neurons: the poly-A bucket overflows its region
+
+
+def _skewed_input():
+    """_input plus a 300 kb poly-A record: one neuron takes ~300 k k-mers, more
+    than its bucket region holds (the partitioned count's direct-add overflow)."""
+    bases, offs = _input()
+    tail = np.full(300_000, ord("A"), np.uint8)
+    return (np.concatenate([bases, tail]),
+            np.concatenate([offs, [offs[-1] + tail.size]]).astype(np.uint64))
+
+
+def _rank_step(rank, world, port, width, cap, steps, wire, q, skew=False):
+    """dist.finalize_step (one host synchronisation per step), twice with a
+    reset in between, then once more on the kept state."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from neurokmer_amd import SpikingKmerCounter
+        from neurokmer_amd import dist as nkdist
+        bases, offs = _skewed_input() if skew else _input()
+        k = 41 if width == 128 else K
+        lo, hi, so = nkdist.shard_records(offs, world, k)[rank]
+        b = bases[lo:hi]
+        d_b = torch.from_numpy(np.concatenate([b, np.zeros(16, np.uint8)])).cuda()
+        d_o = torch.from_numpy(so.astype(np.uint64).view(np.int64)).cuda()
+        torch.cuda.synchronize()
+        pool = SKEW_POOL if skew else POOL
+        c = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, True, kmer_width=width)
+        c.set_steps(steps)
+        out = []
+        for it in range(3):
+            if it == 1:
+                c.reset()
+            c.accumulate_device(d_b.data_ptr(), d_o.data_ptr(), so.size - 1, b.size)
+            nkdist.finalize_step(c, total_kmers=int(offs[-1]) if wire else None, cap=cap)
+            out.append((c.top_abundant_neurons(20), c.energy.total_spikes()))
+        q.put((rank, out, c.currents().tolist(), c.spike_counts().tolist()))
+        c.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("width,cap,steps,wire,skew", [
+    (64, 4096, 1000, True, False),    # the fast path: u32 wire, exact export, one wait
+    (64, 4096, 1000, False, False),   # u64 all-reduce of the currents
+    (64, 3, 1000, True, False),       # truncated segments: every rank redoes, variable-length union
+    (64, 4096, 20000, True, False),   # spike counts past the histogram: host refine on every rank
+    (64, 4096, 1000, True, True),     # an overflowed bucket region (direct adds into the currents)
+    (128, 4096, 1000, True, False),
+    (128, 2, 1000, True, False),
+])
+def test_two_ranks_finalize_step(width, cap, steps, wire, skew):
+    import torch.multiprocessing as mp
+    from oracle import cbind
+    bases, offs = _skewed_input() if skew else _input()
+    k = 41 if width == 128 else K
+    pool = SKEW_POOL if skew else POOL
+    ref = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, True, width=width)
+    ref.set_steps(steps)
+    exp = []
+    for it in range(3):
+        if it == 1:
+            ref = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, True, width=width)
+            ref.set_steps(steps)
+        ref.process_parallel_arrays(bases, offs)
+        exp.append((ref.top_abundant_neurons(20), ref.total_spikes))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_step, args=(r, 2, port, width, cap, steps, wire, q, skew))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, out, cur, sc in res:
+        assert out == exp
+        assert cur == ref.currents().tolist()
+        assert sc == ref.spike_counts().tolist()
