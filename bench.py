@@ -50,15 +50,21 @@ def n_kmers(offsets: np.ndarray, k: int) -> int:
     return int(np.clip(lens - k + 1, 0, None).sum())
 
 
-def load_pmc_traffic():
-    """HBM bytes per K1 launch from the committed rocprofv3 PMC summary, if any."""
+# VALU issue cycles per instruction of K1a's mix: the per-k-mer loop body's
+# 142 instructions cost 470 issue clocks at the measured gfx950 rates (VOP1/2
+# e32 2.45 clk, v_bitop3 2.37, VOP3 4.2; tools/isabench.hip)
+K1A_ISSUE_CLK_PER_INSTR = 3.31
+
+
+def load_pmc():
+    """The committed rocprofv3 PMC summary of K1 (profiles/pmc_count_kernel.json):
+    HBM bytes per launch, VALU instructions and busy cycles per launch."""
     path = os.path.join(ROOT, "profiles", "pmc_count_kernel.json")
     try:
         with open(path) as f:
-            d = json.load(f)
-        return d.get("hbm_bytes_per_launch"), d.get("source")
+            return json.load(f)
     except Exception:
-        return None, None
+        return {}
 
 
 def cpu_baseline(bases: np.ndarray, offsets: np.ndarray, per_record: int = 2_000_000,
@@ -209,7 +215,20 @@ def main() -> int:
         k1_ms = float(np.mean(c_ms)) if c_ms else timings.get("count", float("nan"))
         alg_bytes = bases.size + 8 * nk
         achieved = alg_bytes / (k1_ms * 1e-3)
-        traffic, traffic_src = load_pmc_traffic()
+        pmc = load_pmc()
+        traffic, traffic_src = pmc.get("hbm_bytes_per_launch"), pmc.get("source")
+        valu = None
+        if pmc.get("valu_instr_per_launch") and pmc.get("sclk_ghz") and pmc.get("pmc_launch_ns"):
+            # K1a is VALU-issue bound: issue cycles its instructions need per SIMD
+            # (1024 SIMDs) vs the cycles the launch took (PMC GRBM_GUI_ACTIVE)
+            busy = pmc["sclk_ghz"] * pmc["pmc_launch_ns"]  # cycles per launch
+            need = pmc["valu_instr_per_launch"] / 1024.0 * K1A_ISSUE_CLK_PER_INSTR
+            valu = {"instr_per_launch": pmc["valu_instr_per_launch"],
+                    "issue_clk_per_instr": K1A_ISSUE_CLK_PER_INSTR,
+                    "busy_cycles_per_launch": round(busy),
+                    "issue_frac": round(need / busy, 4),
+                    "sclk_ghz_live": round(busy / (k1_ms * 1e6), 3),
+                    "source": traffic_src}
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "Mk-mers/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "settle_steps": settle,
@@ -227,9 +246,10 @@ def main() -> int:
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(k1_ms, 4),
-                         "launches_timed": len(c_ms)},
+                         "launches_timed": len(c_ms), "valu": valu},
             "stage_ms": {k2: round(v, 4) for k2, v in timings.items()},
             "step_ms_host": [round((b - a) * 1e3, 4) for a, b in zip([t0] + marks[:-1], marks)],
+            "k1_ms_steps": [round(x, 4) for x in count_ms],
             "total_spikes": total_spikes,
         }
         if world == 1 and not args.no_cpu_baseline and k == K and args.kmer_width == 64:
