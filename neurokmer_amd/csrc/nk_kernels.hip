@@ -446,7 +446,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
   const uint64_t T0 = tile * (uint64_t)kPartTile;
   const uint32_t B = pa.n_buckets;
   for (uint32_t b = tid; b <= B; b += kPartBlock) s_cnt[b] = 0;
-  stage_tile<kPartTile, kPartBlock, !CANON>(L, in, tile, k);  // syncs
+  stage_tile<kPartTile, kPartBlock, !CANON, !CANON>(L, in, tile, k);  // syncs (INV: pack_kmer only)
 
   // phase 1: this lane's 16 consecutive positions q0..q0+15.  The first
   // window is extracted from the bit streams, the next 15 are rolled in from

@@ -30,22 +30,35 @@ struct Conv4 {
   uint32_t inv;   // 4 invalid-byte bits, first base in bit 0
 };
 
-__device__ __forceinline__ Conv4 conv4(uint32_t x) {
-  uint32_t t = x | 0x20202020u;
-  uint32_t valid = eq_bytes(t, 0x61616161u) | eq_bytes(t, 0x63636363u) |
-                   eq_bytes(t, 0x67676767u) | eq_bytes(t, 0x74747474u);
-  uint32_t vm = valid >> 7;  // 0x01 per valid byte
-  uint32_t vm3 = vm * 3u;
-  uint32_t code = ((x >> 1) ^ (x >> 2)) & 0x03030303u & vm3;
-  uint32_t comp = (code ^ 0x03030303u) & vm3;
-  Conv4 o;
-  o.fnib = ((code << 6) & 0xC0u) | ((code >> 4) & 0x30u) | ((code >> 14) & 0x0Cu) |
-           ((code >> 24) & 0x03u);
-  o.rnib = (comp & 0x03u) | ((comp >> 6) & 0x0Cu) | ((comp >> 12) & 0x30u) |
-           ((comp >> 18) & 0xC0u);
-  uint32_t m = ~vm & 0x01010101u;
-  o.inv = (m & 1u) | ((m >> 7) & 2u) | ((m >> 14) & 4u) | ((m >> 21) & 8u);
+// Four bytes -> codes, in ~14 VALU ops: code = ((x>>1) ^ (x>>2)) & 3 per byte
+// (A/a 0, C/c 1, G/g 2, T/t 3); a byte is valid iff (byte | 0x20) equals the
+// lowercase letter of its own code, looked up with one v_perm_b32; the 2-bit
+// fields are gathered into byte 3 of a product by one multiply each (the
+// multipliers place field i at 30-2i / 24+2i / 28+i with no overlapping or
+// carrying partial products).  Equal to the byte-compare form on all 2^32
+// words (tools/conv4_check.cpp).
+struct Conv4P {
+  uint32_t pf;  // forward codes in bits 31:24, first base in 31:30
+  uint32_t pr;  // complement codes in bits 31:24, first base in 25:24
+  uint32_t pi;  // invalid-byte bits in bits 31:28, first base in 28
+};
+
+__device__ __forceinline__ Conv4P conv4p(uint32_t x, bool want_inv = true) {
+  const uint32_t code = ((x >> 1) ^ (x >> 2)) & 0x03030303u;
+  const uint32_t expect = __builtin_amdgcn_perm(0u, 0x74676361u, code);  // "acgt"[code]
+  const uint32_t z = (x | 0x20202020u) ^ expect;
+  const uint32_t valid = ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u;
+  const uint32_t vm3 = (valid >> 6) | (valid >> 7);  // 0x03 per valid byte
+  Conv4P o;
+  o.pf = (code & vm3) * 0x40100401u;
+  o.pr = (~code & vm3) * 0x01041040u;
+  o.pi = want_inv ? ((~valid >> 7) & 0x01010101u) * 0x10204080u : 0u;
   return o;
+}
+
+__device__ __forceinline__ Conv4 conv4(uint32_t x) {
+  const Conv4P p = conv4p(x);
+  return Conv4{p.pf >> 24, p.pr >> 24, p.pi >> 28};
 }
 
 __device__ __forceinline__ bool valid_byte(uint8_t b) {
@@ -69,8 +82,9 @@ struct TileLds {
   uint4 RAWB[RAW ? kChunks : 1];
 };
 
-// Loads the tile, builds F/R/INV/WIN.  Ends with a __syncthreads().
-template <int TILE, int BLOCK, bool RAW>
+// Loads the tile, builds F/R/INV/WIN (INV only when WANT_INV: the canonical
+// partitioned count never reads it).  Ends with a __syncthreads().
+template <int TILE, int BLOCK, bool RAW, bool WANT_INV = true>
 __device__ __forceinline__ void stage_tile(TileLds<TILE, RAW> &L, const KmerInput &in,
                                            uint64_t tile, int k) {
   constexpr int kChunks = TileLds<TILE, RAW>::kChunks;
@@ -100,14 +114,20 @@ __device__ __forceinline__ void stage_tile(TileLds<TILE, RAW> &L, const KmerInpu
         if (g + j < n_bases) w[j >> 2] |= (uint32_t)in.bases[g + j] << (8 * (j & 3));
       v = make_uint4(w[0], w[1], w[2], w[3]);
     }
-    Conv4 a = conv4(v.x), b = conv4(v.y), cc = conv4(v.z), d = conv4(v.w);
-    L.F[c] = (a.fnib << 24) | (b.fnib << 16) | (cc.fnib << 8) | d.fnib;
-    L.R[c] = a.rnib | (b.rnib << 8) | (cc.rnib << 16) | (d.rnib << 24);
-    L.INV[c] = (uint16_t)(a.inv | (b.inv << 4) | (cc.inv << 8) | (d.inv << 12));
+    const Conv4P a = conv4p(v.x, WANT_INV), b = conv4p(v.y, WANT_INV),
+                 cc = conv4p(v.z, WANT_INV), d = conv4p(v.w, WANT_INV);
+    // byte 3 of each product, MSB-first (F) / LSB-first (R): two v_perm + or
+    L.F[c] = __builtin_amdgcn_perm(a.pf, b.pf, 0x07030C0Cu) |
+             __builtin_amdgcn_perm(cc.pf, d.pf, 0x0C0C0703u);
+    L.R[c] = __builtin_amdgcn_perm(b.pr, a.pr, 0x0C0C0703u) |
+             __builtin_amdgcn_perm(d.pr, cc.pr, 0x07030C0Cu);
+    if (WANT_INV)
+      L.INV[c] = (uint16_t)((a.pi >> 28) | ((b.pi >> 28) << 4) | ((cc.pi >> 28) << 8) |
+                            ((d.pi >> 28) << 12));
     if (RAW) L.RAWB[c] = v;
   }
   if (tid < 2) { L.F[kChunks + tid] = 0; L.R[kChunks + tid] = 0; }
-  if (tid < 4) L.INV[kChunks + tid] = 0;
+  if (WANT_INV && tid < 4) L.INV[kChunks + tid] = 0;
   for (int i = tid; i < TILE / 32; i += BLOCK) L.WIN[i] = 0;
   __syncthreads();
   // windows crossing a record end (or running past the input) are not k-mers
