@@ -12,6 +12,9 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libneurokmer.so")
+# A/B experiments only (tools/ab_build.sh): another build of the same library
+if os.environ.get("NK_AB_LIB"):
+    LIB_PATH = os.path.abspath(os.environ["NK_AB_LIB"])
 CLI_PATH = os.path.join(_HERE, "bin", "neurokmer")
 
 NK_OK = 0

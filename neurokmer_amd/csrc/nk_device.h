@@ -17,6 +17,9 @@ namespace nk {
 // (v_lshl_add_u64), carry adds and multiplies at ~4.2.  So a 64-bit add is one
 // v_lshl_add_u64, a rotate is two v_alignbit on the 32-bit halves (a rotate by
 // 32 is a free register swap), and xors stay 32-bit VOP2: 70 clk per SipRound.
+// (Building the swapped v0/v2 pairs with one v_pk_mov_b32 instead of two
+// v_mov_b32 is 4 % faster in isolation, tools/sipbench.hip V3, but made the
+// count kernel 6 % slower in an A/B on one box, tools/ab_run.sh: not used.)
 __device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) {
   const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
   const uint32_t nlo = __builtin_amdgcn_alignbit(lo, hi, 32 - r);

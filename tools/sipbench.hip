@@ -81,10 +81,43 @@ __device__ __forceinline__ uint64_t sip13_sw(uint64_t m) {
   return v0 ^ v1 ^ swap32(v2) ^ v3;
 }
 
+// V3: the 32-bit swap as ONE v_pk_mov_b32 (op_sel picks the halves) instead
+// of two v_mov_b32 into an aligned pair
+__device__ __forceinline__ uint64_t swap32_pk(uint64_t x) {
+  uint64_t r;
+  asm("v_pk_mov_b32 %0, %1, %1 op_sel:[1,0]" : "=v"(r) : "v"(x));
+  return r;
+}
+#define NK_SIPROUND_PK                                                \
+  do {                                                               \
+    v0 += v1; v1 = rotl64(v1, 13); v1 ^= v0; v0 = swap32_pk(v0);     \
+    v2 += v3; v3 = rotl64(v3, 16); v3 ^= v2;                         \
+    v0 += v3; v3 = rotl64(v3, 21); v3 ^= v0;                         \
+    v2 += v1; v1 = rotl64(v1, 17); v1 ^= v2; v2 = swap32_pk(v2);     \
+  } while (0)
+__device__ __forceinline__ uint64_t sip13_pk(uint64_t m) {
+  uint64_t v0 = 0x736f6d6570736575ULL;
+  uint64_t v1 = 0x646f72616e646f6dULL;
+  uint64_t v2 = 0x6c7967656e657261ULL;
+  uint64_t v3 = 0x7465646279746573ULL ^ m;
+  NK_SIPROUND;  // round 1: v0 is a constant here, the compiler folds it
+  v0 ^= m;
+  const uint64_t b = 8ULL << 56;
+  v3 ^= b;
+  NK_SIPROUND_PK;
+  v0 ^= b;
+  v2 ^= 0xffULL;
+  NK_SIPROUND_PK;
+  NK_SIPROUND_PK;
+  NK_SIPROUND;  // last round: the swaps feed only the final xor
+  return v0 ^ v1 ^ v2 ^ v3;
+}
+
 template <int V>
 __device__ __forceinline__ uint32_t hmod(uint64_t key, FastMod fm) {
   if (V == 0) return fastmod32(sip13_u64(key), fm);
   if (V == 1) return fastmod32(sip13_sw<1>(key), fm);
+  if (V == 3) return fastmod32(sip13_pk(key), fm);
   return fastmod32(sip13_sw<2>(key), fm);
 }
 
@@ -107,7 +140,7 @@ __global__ void kcheck(uint64_t n, FastMod fm, uint32_t *bad) {
   const uint64_t key = tid * 0xD1B54A32D192ED03ULL ^ (tid >> 7);
   if (hmod<V>(key, fm) != hmod<0>(key, fm)) atomicAdd(bad, 1u);
   // raw hash too
-  uint64_t h = V == 0 ? sip13_u64(key) : V == 1 ? sip13_sw<1>(key) : sip13_sw<2>(key);
+  uint64_t h = V == 0 ? sip13_u64(key) : V == 1 ? sip13_sw<1>(key) : V == 3 ? sip13_pk(key) : sip13_sw<2>(key);
   if (h != sip13_u64(key)) atomicAdd(bad, 1u);
 }
 
@@ -122,20 +155,21 @@ int main(int argc, char **argv) {
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
-  const char *names[] = {"V0 shipped (lshl_add + moves)", "V1 swapped adds, asm carry", "V2 swapped adds, C carry"};
+  const char *names[] = {"V0 shipped (lshl_add + moves)", "V1 swapped adds, asm carry", "V2 swapped adds, C carry",
+                         "V3 swaps as v_pk_mov_b32"};
   // check that SipHash-1-3(0) matches the recorded KAT on the host side too
-  for (int v = 0; v < 3; ++v) {
+  for (int v = 0; v < 4; ++v) {
     hipMemset(bad, 0, 4);
     const uint64_t nchk = 1 << 24;
 #define CHK(V) hipLaunchKernelGGL(kcheck<V>, dim3(nchk / 256), dim3(256), 0, 0, nchk, fm, bad)
-    if (v == 0) CHK(0); else if (v == 1) CHK(1); else CHK(2);
+    if (v == 0) CHK(0); else if (v == 1) CHK(1); else if (v == 2) CHK(2); else CHK(3);
     uint32_t hb = 0;
     hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost);
     float best = 1e9;
     for (int rep = 0; rep < 7; ++rep) {
       hipEventRecord(a);
 #define RUN(V) hipLaunchKernelGGL(kbench<V>, dim3(blocks), dim3(threads), 0, 0, n_per, fm, out)
-      if (v == 0) RUN(0); else if (v == 1) RUN(1); else RUN(2);
+      if (v == 0) RUN(0); else if (v == 1) RUN(1); else if (v == 2) RUN(2); else RUN(3);
       hipEventRecord(b);
       hipEventSynchronize(b);
       float ms;
