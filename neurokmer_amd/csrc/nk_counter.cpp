@@ -110,6 +110,10 @@ struct nk_counter {
   DevBuf<uint32_t> radix_h;
   uint64_t set_cap = 0;     // capacity used by the last uniques pass
   uint64_t set_alloc = 0;   // allocated capacity of set_keys (keys)
+  // set_keys[i] == kEmpty for every i >= set_dirty; set_clean: for every i (the
+  // count's prep kernel empties [0, set_dirty) for the partitioned path's scan)
+  uint64_t set_dirty = 0, dirty_before = 0;
+  bool set_clean = false;
   bool w128 = false;        // --kmer-width=128: u128 keys, 3 set words per key
   size_t n_top_keys = 0;
   DevBuf<uint64_t> set_mask_d, set_need_d;
@@ -389,11 +393,12 @@ nk_counter *nk_new(size_t k, float threshold, float leak, uint32_t refractory, d
        !c->uniq.ensure(kMaxTopN) && !c->special.ensure(kMaxTopN) &&
        !c->top_keys_n.ensure(1) && !c->radix_h.ensure(256) && !c->set_mask_d.ensure(1) &&
        !c->set_need_d.ensure(1) && !c->post_flags.ensure(4) && !c->set_keys.ensure((o.kmer_width == NK_KMER_128 ? 3 : 1) << 20) &&
-       !c->hits.ensure(1 << 19) && !c->n_hits.ensure(1) &&
+       !c->n_hits.ensure(1) &&
        hipHostMalloc((void **)&c->res_h, nk_counter::kResFlagOff + 64,
                      hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
        hipHostGetDevicePointer((void **)&c->res_hd, c->res_h, 0) == hipSuccess;
   c->set_alloc = 1 << 20;
+  c->set_dirty = c->set_alloc;  // uninitialised memory
   if (!ok || zero_state(c) != NK_OK) {
     std::string e = g_err.empty() ? "device allocation failed" : g_err;
     nk_free(c);
@@ -631,6 +636,14 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
   const bool counted = cp.path != CountPath::Atomic && in.n_tiles > 0;
   c->part_used = counted && cp.path == CountPath::Part;
   c->gen_km = (cp.path == CountPath::Gen || cp.path == CountPath::Wide) ? cp.km : -1;
+  if (cp.path == CountPath::Part && c->set_dirty && !c->w128 && z.n < kZeroMax) {
+    // the uniques set, empty for this input's scan (k_uniq_scan inserts as it goes)
+    z.ptr[z.n] = c->set_keys.p; z.bytes[z.n] = c->set_dirty * 8; z.fill[z.n++] = 0xFF;
+    c->set_dirty = 0;
+    c->set_clean = true;
+  } else if (cp.path == CountPath::Part && !c->set_dirty) {
+    c->set_clean = true;
+  }
   if (defer_partials) {  // the LIF of this process call accumulates into these
     z.ptr[z.n] = c->hist.p;  z.bytes[z.n++] = kHistBins * kHistCopies * 4;
     z.ptr[z.n] = c->stats.p; z.bytes[z.n++] = 16;
@@ -793,9 +806,13 @@ static int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, bool post_don
   if (!post_done) HIPCHK(launch_top_post(c->cand.p, c->top_cur.p, m, c->set_alloc, part ? c->p_over.p : nullptr,
                          part ? 1 : 0, c->set_mask_d.p, c->tbuckets.p, c->post_flags.p, c->uniq.p,
                          c->special.p, c->n_hits.p, s));
-  if (!part)
+  // the set must be empty up to the pass's mask: after the count's prep it is
+  c->dirty_before = c->set_clean ? 0 : c->set_alloc;
+  if (!part || !c->set_clean)
     HIPCHK(c->w128 ? launch_set_fill128(c->set_keys.p, c->set_mask_d.p, c->set_alloc, s)
                    : launch_set_fill(c->set_keys.p, c->set_mask_d.p, c->set_alloc, s));
+  c->set_clean = false;
+  c->set_dirty = c->set_alloc;  // until a readback tells the mask the pass used
   UniqArgs u{};
   u.top = c->cand.p;
   u.n_top = m;
@@ -809,11 +826,10 @@ static int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, bool post_don
     u.xn = c->export_n.p;
     u.xcap = c->xport_cap;
   }
-  if (part) {  // the scan kernel also empties the set
+  if (part) {
     const uint32_t slices = std::max<uint32_t>(1, 512 / m);
     HIPCHK(launch_part_uniques(c->last_in, (int)c->k, c->canonical, c->last_pa, u, c->tbuckets.p,
-                               c->post_flags.p + 2, m, slices, c->hits.p, c->n_hits.p, c->hits.n,
-                               s));
+                               c->post_flags.p + 2, m, slices, s));
   } else {
     KmerInput in = c->last_in;
     const uint64_t tile = c->gen_km >= 0 ? kPartTile : kTile;
@@ -960,8 +976,9 @@ static int settle_top(nk_counter *c, uint64_t want, bool uniq, bool use_kpn, boo
       for (uint64_t x : tc) sum += x;
       while (cap < 2 * sum + 2) cap <<= 1;
       if ((rc = c->set_keys.ensure(c->w128 ? 3 * cap : cap))) return rc;
-      if ((rc = c->hits.ensure(cap / 2))) return rc;
       c->set_alloc = cap;
+      c->set_dirty = cap;
+      c->set_clean = false;
     }
     if (h->flags[0] || h->flags[1]) {
       if ((rc = enqueue_uniques(c, (uint32_t)want, h->flags[1] != 0, false, s))) return rc;
@@ -969,6 +986,7 @@ static int settle_top(nk_counter *c, uint64_t want, bool uniq, bool use_kpn, boo
       HIPCHK(hipStreamSynchronize(s));
     }
     c->set_cap = h->mask + 1;
+    c->set_dirty = std::max(c->dirty_before, c->set_cap);  // the last pass wrote below its mask
   } else {
     c->set_cap = 0;
   }
@@ -1203,6 +1221,10 @@ static int enqueue_merge(nk_counter *c, const MergeSrc &src, uint64_t max_keys, 
     if ((rc = keys.ensure(c->w128 ? 3 * cap : cap))) return rc;
     alloc = cap;
   }
+  if (!sep) {  // the merge fills the shard's own set below cap
+    c->set_clean = false;
+    c->set_dirty = std::max(c->set_dirty, cap);
+  }
   if ((rc = c->trunc_d.ensure(1)) || (rc = c->mset_mask_d.ensure(1)) ||
       (rc = c->muniq.ensure(kMaxTopN)) || (rc = c->mspecial.ensure(kMaxTopN)))
     return rc;
@@ -1382,6 +1404,7 @@ int nk_merge_export(nk_counter *c, const uint64_t *d_buf, size_t world, size_t s
     c->top[i]._pad = 0;
   }
   c->set_cap = c->export_uniq ? h->mask + 1 : 0;  // this shard's set (the merge used its own)
+  if (c->export_uniq) c->set_dirty = std::max(c->dirty_before, c->set_cap);
   *redo = (want && h->flags[3]) ? 1 : 0;
   c->redo_ready = *redo != 0;
   c->top_valid = !*redo;

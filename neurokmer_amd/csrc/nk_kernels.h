@@ -76,9 +76,10 @@ struct TopFuse {
 };
 
 constexpr int kZeroMax = 8;
-struct ZeroList {
+struct ZeroList {  // (filled with fill[b] bytes: 0, or 0xFF for the uniques set's kEmpty)
   void *ptr[kZeroMax];
   uint64_t bytes[kZeroMax];
+  uint8_t fill[kZeroMax];
   int n;
 };
 
@@ -247,8 +248,7 @@ hipError_t launch_partials_add(const uint32_t *partials, uint32_t slices, uint64
 // (also empties the uniques hash set u.set_keys[0 .. *u.set_mask])
 hipError_t launch_part_uniques(const KmerInput &in, int k, int canonical, const PartArgs &pa,
                                const UniqArgs &u, const uint32_t *tbuckets, const uint32_t *n_tb,
-                               uint32_t max_tb, uint32_t slices, unsigned long long *hits,
-                               unsigned long long *n_hits, uint64_t hit_cap, hipStream_t s);
+                               uint32_t max_tb, uint32_t slices, hipStream_t s);
 
 uint64_t top_tbl_size(uint32_t n_top);
 uint64_t n_tiles_for(uint64_t n_bases, uint64_t tile);

@@ -742,16 +742,16 @@ __device__ uint64_t wave_search_le(const uint2 *d, uint64_t n, uint64_t x) {
   return lo;
 }
 
-// Uniques from the kept records, in two flat kernels:
-//   U1 k_uniq_scan: stream the records of the buckets holding top-N neurons
-//      (16-B loads), test each bin offset against an LDS bitmap of the
-//      bucket's top bins, collect hits {bucket, top row, record index} in LDS
-//      and publish them with one global reservation per workgroup;
-//      At the end each workgroup resolves its hits to base positions
-//      (record -> segment through an LDS table of the slice's segments);
-//   U2 k_uniq_hits: one lane per hit: recompute the key from the bases,
-//      per-workgroup dedup in LDS, insert into the global hash set.
-// Hits never serialise inside a wave and no lane waits on another's latency.
+// Uniques from the kept records, in ONE flat kernel, k_uniq_scan: stream the
+// records of the buckets holding top-N neurons (16-B loads), test each bin
+// offset against an LDS bitmap of the bucket's top bins, collect hits {top
+// row, record index} in LDS; then each workgroup resolves its hits to base
+// positions (record -> segment through an LDS table of the slice's segments),
+// recomputes each hit's key from the bases, deduplicates in LDS and inserts
+// into the global hash set.  The set is emptied beforehand (by the prep kernel
+// of the count, or by k_set_fill), never by this kernel's own blocks, so no
+// block can insert into a slot another block has yet to clear.  Hits never
+// serialise inside a wave and no lane waits on another's latency.
 constexpr int kScanBuf = 4096;
 
 // A scan hit {bucket | top row | record index} as k_uniq_hits takes it:
@@ -779,32 +779,23 @@ __device__ unsigned long long resolve_hit(const PartArgs &pa, uint32_t b, uint64
   return hit_at(pa, b, a, e);
 }
 
-__global__ __launch_bounds__(kHistBlock) void k_uniq_scan(PartArgs pa, UniqArgs u,
+template <bool CANON>
+__global__ __launch_bounds__(kHistBlock) void k_uniq_scan(KmerInput in, int k, PartArgs pa,
+                                                          UniqArgs u,
                                                           const uint32_t *__restrict__ tbuckets,
                                                           const uint32_t *__restrict__ n_tb,
-                                                          uint32_t slices,
-                                                          unsigned long long *__restrict__ hits,
-                                                          unsigned long long *__restrict__ n_hits,
-                                                          uint64_t hit_cap,
-                                                          unsigned long long *__restrict__ set_keys,
-                                                          const uint64_t *__restrict__ set_mask) {
+                                                          uint32_t slices) {
   __shared__ uint32_t bits[65536 / 32];  // covers the pad sentinel bin (never set)
   __shared__ uint32_t t_off[kMaxTopN];
   __shared__ uint32_t t_slot[kMaxTopN];
   __shared__ unsigned long long buf[kScanBuf];
+  __shared__ unsigned long long seen[kSeen];
   __shared__ uint32_t t_n, s_nh;
-  __shared__ unsigned long long s_base;
   __shared__ uint64_t s_seg[2];
-  {  // every block first empties its share of the uniques hash set (k_uniq_hits fills it)
-    const uint64_t cap = *set_mask + 1;
-    const uint64_t nthr = (uint64_t)gridDim.x * gridDim.y * kHistBlock;
-    for (uint64_t i = ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * kHistBlock + threadIdx.x;
-         i < cap; i += nthr)
-      set_keys[i] = kEmpty;
-  }
   if (blockIdx.y >= *n_tb) return;
   const uint32_t b = tbuckets[blockIdx.y], r = blockIdx.x;
   for (int i = threadIdx.x; i < 65536 / 32; i += kHistBlock) bits[i] = 0;
+  seen_init(seen);
   if (threadIdx.x == 0) { t_n = 0; s_nh = 0; }
   __syncthreads();
   for (uint32_t s = threadIdx.x; s < u.n_top; s += kHistBlock) {
@@ -825,6 +816,13 @@ __global__ __launch_bounds__(kHistBlock) void k_uniq_scan(PartArgs pa, UniqArgs 
   if (n_seg > pa.max_segs) n_seg = pa.max_segs;
   const uint32_t tn = t_n;
   const uint16_t *src = pa.off + (uint64_t)b * pa.cap;
+  // a hit's key into the set: recomputed from the bases at its position
+  auto insert_hit = [&](unsigned long long h) {
+    const uint32_t slot = (uint32_t)(h >> 48);
+    const uint64_t p = h & ((1ull << 48) - 1);
+    const uint64_t key = vec_window_key<CANON>(in.bases, in.n_bases, p, k);
+    if (key == kEmpty || !seen_before(seen, key)) set_insert(u, slot, key);
+  };
   // one hit record: bucket | top row | record index (< 2^38)
   auto push = [&](uint64_t i, uint32_t off) {
     uint32_t slot = 0;
@@ -833,12 +831,8 @@ __global__ __launch_bounds__(kHistBlock) void k_uniq_scan(PartArgs pa, UniqArgs 
     const unsigned long long e = ((unsigned long long)b << 48) |
                                  ((unsigned long long)slot << 38) | i;
     const uint32_t at = atomicAdd(&s_nh, 1u);
-    if (at < kScanBuf) {
-      buf[at] = e;
-    } else {  // LDS list full (very hit-dense slice): resolve and publish this one directly
-      const unsigned long long g = atomicAdd(n_hits, 1ull);
-      if (g < hit_cap) hits[g] = resolve_hit(pa, b, 0, n_seg, e);
-    }
+    if (at < kScanBuf) buf[at] = e;
+    else insert_hit(resolve_hit(pa, b, 0, n_seg, e));  // LDS list full (very hit-dense slice)
   };
   // 8 records per 16-B load, eight loads in flight per lane (the slice is a
   // few dozen loads per lane: latency, not bandwidth, bounds a shallow loop);
@@ -894,11 +888,8 @@ __global__ __launch_bounds__(kHistBlock) void k_uniq_scan(PartArgs pa, UniqArgs 
   const bool staged = ns <= (uint64_t)(65536 / 32);
   if (staged)
     for (uint32_t j = threadIdx.x; j < ns; j += kHistBlock) tab[j] = d[s0 + j].y;
-  if (threadIdx.x == 0) s_base = atomicAdd(n_hits, (unsigned long long)nh);
   __syncthreads();
-  const unsigned long long gb = s_base;
   for (uint32_t h = threadIdx.x; h < nh; h += kHistBlock) {
-    if (gb + h >= hit_cap) break;
     const unsigned long long e = buf[h];
     unsigned long long out;
     if (staged) {
@@ -913,27 +904,7 @@ __global__ __launch_bounds__(kHistBlock) void k_uniq_scan(PartArgs pa, UniqArgs 
     } else {
       out = resolve_hit(pa, b, s0, s0 + ns, e);
     }
-    hits[gb + h] = out;
-  }
-}
-
-template <bool CANON>
-__global__ __launch_bounds__(256) void k_uniq_hits(KmerInput in, int k, PartArgs pa, UniqArgs u,
-                                                   const unsigned long long *__restrict__ hits,
-                                                   const unsigned long long *__restrict__ n_hits,
-                                                   uint64_t hit_cap) {
-  __shared__ unsigned long long seen[kSeen];
-  seen_init(seen);
-  __syncthreads();
-  uint64_t nh = *n_hits;
-  if (nh > hit_cap) nh = hit_cap;
-  for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < nh;
-       h += (uint64_t)gridDim.x * blockDim.x) {
-    const unsigned long long e = hits[h];
-    const uint32_t slot = (uint32_t)(e >> 48);
-    const uint64_t p = e & ((1ull << 48) - 1);
-    const uint64_t key = vec_window_key<CANON>(in.bases, in.n_bases, p, k);
-    if (key == kEmpty || !seen_before(seen, key)) set_insert(u, slot, key);
+    insert_hit(out);
   }
 }
 
@@ -2043,20 +2014,17 @@ hipError_t launch_partials_add(const uint32_t *partials, uint32_t slices, uint64
   return hipGetLastError();
 }
 
+// the set must be empty (kEmpty) up to *u.set_mask: the caller clears it
 hipError_t launch_part_uniques(const KmerInput &in, int k, int canonical, const PartArgs &pa,
                                const UniqArgs &u, const uint32_t *tbuckets, const uint32_t *n_tb,
-                               uint32_t max_tb, uint32_t slices, unsigned long long *hits,
-                               unsigned long long *n_hits, uint64_t hit_cap, hipStream_t s) {
+                               uint32_t max_tb, uint32_t slices, hipStream_t s) {
   if (!max_tb) return hipSuccess;
-  hipLaunchKernelGGL(k_uniq_scan, dim3(slices, max_tb), dim3(kHistBlock), 0, s, pa, u, tbuckets,
-                     n_tb, slices, hits, n_hits, hit_cap, u.set_keys, u.set_mask);
-  const unsigned g = 1024;
   if (canonical)
-    hipLaunchKernelGGL(k_uniq_hits<true>, dim3(g), dim3(256), 0, s, in, k, pa, u, hits, n_hits,
-                       hit_cap);
+    hipLaunchKernelGGL(k_uniq_scan<true>, dim3(slices, max_tb), dim3(kHistBlock), 0, s, in, k, pa,
+                       u, tbuckets, n_tb, slices);
   else
-    hipLaunchKernelGGL(k_uniq_hits<false>, dim3(g), dim3(256), 0, s, in, k, pa, u, hits, n_hits,
-                       hit_cap);
+    hipLaunchKernelGGL(k_uniq_scan<false>, dim3(slices, max_tb), dim3(kHistBlock), 0, s, in, k, pa,
+                       u, tbuckets, n_tb, slices);
   return hipGetLastError();
 }
 
@@ -2093,9 +2061,10 @@ __global__ void k_zero(ZeroList z) {
   for (int b = 0; b < z.n; ++b) {
     uint8_t *p = (uint8_t *)z.ptr[b];
     const uint64_t n = z.bytes[b];
+    const uint32_t f = 0x01010101u * z.fill[b];
     const uint64_t n16 = ((uintptr_t)p & 15) ? 0 : n / 16;
-    for (uint64_t i = tid; i < n16; i += stride) reinterpret_cast<uint4 *>(p)[i] = make_uint4(0, 0, 0, 0);
-    for (uint64_t i = n16 * 16 + tid; i < n; i += stride) p[i] = 0;
+    for (uint64_t i = tid; i < n16; i += stride) reinterpret_cast<uint4 *>(p)[i] = make_uint4(f, f, f, f);
+    for (uint64_t i = n16 * 16 + tid; i < n; i += stride) p[i] = (uint8_t)f;
   }
 }
 
@@ -2121,9 +2090,10 @@ __global__ void k_prep(const uint64_t *__restrict__ offsets, uint64_t n_recs, ui
   for (int b = 0; b < z.n; ++b) {
     uint8_t *p = (uint8_t *)z.ptr[b];
     const uint64_t n = z.bytes[b];
+    const uint32_t f = 0x01010101u * z.fill[b];
     const uint64_t n16 = ((uintptr_t)p & 15) ? 0 : n / 16;
-    for (uint64_t i = tid; i < n16; i += stride) reinterpret_cast<uint4 *>(p)[i] = make_uint4(0, 0, 0, 0);
-    for (uint64_t i = n16 * 16 + tid; i < n; i += stride) p[i] = 0;
+    for (uint64_t i = tid; i < n16; i += stride) reinterpret_cast<uint4 *>(p)[i] = make_uint4(f, f, f, f);
+    for (uint64_t i = n16 * 16 + tid; i < n; i += stride) p[i] = (uint8_t)f;
   }
 }
 

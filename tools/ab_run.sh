@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 for round in 1 2; do
   for tag in A "$@"; do
     if [ "$tag" = A ]; then lib=""; else lib=tools/bin/ab/$tag/libneurokmer.so; fi
-    NK_AB_LIB=$lib timeout -k 10 200 python bench.py --steps 20 --warmup 2 --no-cpu-baseline \
+    NK_AB_LIB=$lib timeout -k 10 90 python bench.py --steps 20 --warmup 2 --no-cpu-baseline \
       > gpurun_out/ab_${tag}_$round.log 2>&1 || exit $?
     python3 -c "import json,sys; d=json.loads(open('gpurun_out/ab_${tag}_$round.log').read().strip().splitlines()[-1]); print('$tag', $round, d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'], d['stage_ms'])"
   done
