@@ -779,8 +779,11 @@ static int enqueue_lif(nk_counter *c, int streaming, uint32_t fuse_want, bool pa
   } else if ((rc = materialize(c, true, s))) {  // finalize right after a reset
     return rc;
   }
+  // partitioned count with its partials pending: the prep zeroed the currents and
+  // only overflowed buckets added into them, so only those buckets are read
+  const uint32_t *over = (!wire && c->pend_slices && c->part_used) ? c->p_over.p : nullptr;
   HIPCHK(launch_lif_apply(c->cur.p, wire ? wire : c->partials.p, wire ? 1u : c->pend_slices,
-                          wire ? 1 : 0, c->state_fresh ? 1 : 0, c->v.p,
+                          wire ? 1 : 0, over, c->state_fresh ? 1 : 0, c->v.p,
                           c->r.p, c->sc.p, c->pool, lp, c->lif_tbl.p, kLifTable, c->hist.p,
                           c->stats.p, tf, s));
   c->pend_slices = 0;

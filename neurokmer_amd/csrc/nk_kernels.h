@@ -171,7 +171,7 @@ hipError_t launch_lif_table(LifEntry *tbl, int n, LifParams lp, hipStream_t s);
 // first (the fused K1c of a single-device process call) and is written back.
 // fresh: v/r/sc are taken as 0 (lazy reset) and every neuron is written.
 hipError_t launch_lif_apply(uint64_t *currents, const uint32_t *partials, uint32_t slices,
-                            int cur_zero,
+                            int cur_zero, const uint32_t *over,
                             int fresh, float *v, uint32_t *r, uint64_t *sc, uint64_t pool, LifParams lp,
                             const LifEntry *tbl, int tbl_n, uint32_t *hist, uint64_t *stats,
                             const TopFuse &tf, hipStream_t s);

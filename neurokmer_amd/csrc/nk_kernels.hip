@@ -1279,7 +1279,8 @@ __device__ void final_top(uint64_t pool, const uint64_t *currents, uint32_t nb,
 
 __global__ __launch_bounds__(kLifBlock) void k_lif_apply(uint64_t *__restrict__ currents,
                                                       const uint32_t *__restrict__ partials,
-                                                      uint32_t slices, int cur_zero, int fresh,
+                                                      uint32_t slices, int cur_zero,
+                                                      const uint32_t *__restrict__ over, int fresh,
                                                       float *__restrict__ V,
                                                       uint32_t *__restrict__ R,
                                                       uint64_t *__restrict__ SC, uint64_t pool,
@@ -1307,7 +1308,9 @@ __global__ __launch_bounds__(kLifBlock) void k_lif_apply(uint64_t *__restrict__ 
 #pragma unroll
   for (int j = 0; j < kLifPerThread; ++j) {
     const uint64_t i = idx_of(j);
-    cntv[j] = cur_zero ? 0ull : currents[i];  // cur_zero: the partials (wire) hold it all
+    // cur_zero: the partials (wire) hold it all; over: the count zeroed the
+    // currents and only overflowed buckets added into them
+    cntv[j] = (cur_zero || (over && !over[i >> kBinBits])) ? 0ull : currents[i];
     scv[j] = fresh ? 0 : SC[i];
     vin[j] = fresh ? 0.0f : V[i];
     rin[j] = fresh ? 0u : R[i];
@@ -1818,14 +1821,14 @@ uint32_t lif_blocks(uint64_t pool) {
 }
 
 hipError_t launch_lif_apply(uint64_t *currents, const uint32_t *partials, uint32_t slices,
-                            int cur_zero, int fresh, float *v, uint32_t *r, uint64_t *sc, uint64_t pool, LifParams lp,
+                            int cur_zero, const uint32_t *over, int fresh, float *v, uint32_t *r, uint64_t *sc, uint64_t pool, LifParams lp,
                             const LifEntry *tbl, int tbl_n, uint32_t *hist, uint64_t *stats,
                             const TopFuse &tf, hipStream_t s) {
   if (!pool) return hipSuccess;
   const unsigned g = lif_blocks(pool);
   if (tf.want && (tf.want > kFuseMaxTopN || g > kFuseMaxBlocks || pool > (1ull << 24)))
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_lif_apply, dim3(g), dim3(kLifBlock), 0, s, currents, partials, slices, cur_zero, fresh,
+  hipLaunchKernelGGL(k_lif_apply, dim3(g), dim3(kLifBlock), 0, s, currents, partials, slices, cur_zero, over, fresh,
                      v, r, sc, pool, lp, tbl, tbl_n, hist, (unsigned long long *)stats, tf);
   if (tf.want)
     hipLaunchKernelGGL(k_top_final, dim3(1), dim3(kLifBlock), 0, s, pool, currents, g, tf);
