@@ -830,7 +830,10 @@ static int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, bool post_don
     u.xcap = c->xport_cap;
   }
   if (part) {
-    const uint32_t slices = std::max<uint32_t>(1, 512 / m);
+#ifndef NK_U1_SLICE_BUDGET
+#define NK_U1_SLICE_BUDGET 1024  // scan workgroups per launch (A/B: 1024 with 4 loads in flight best)
+#endif
+    const uint32_t slices = std::max<uint32_t>(1, NK_U1_SLICE_BUDGET / m);
     HIPCHK(launch_part_uniques(c->last_in, (int)c->k, c->canonical, c->last_pa, u, c->tbuckets.p,
                                c->post_flags.p + 2, m, slices, s));
   } else {

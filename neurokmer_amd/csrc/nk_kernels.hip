@@ -837,7 +837,10 @@ __global__ __launch_bounds__(kHistBlock) void k_uniq_scan(KmerInput in, int k, P
   // 8 records per 16-B load, eight loads in flight per lane (the slice is a
   // few dozen loads per lane: latency, not bandwidth, bounds a shallow loop);
   // no barrier in the loop
-  constexpr int kU = 8;
+#ifndef NK_U1_KU
+#define NK_U1_KU 4
+#endif
+  constexpr int kU = NK_U1_KU;  // 16-B loads in flight per lane
   const uint64_t lo8 = lo & ~7ull;
   const uint64_t step = 8ull * kHistBlock;
   for (uint64_t c0 = lo8 + 8ull * threadIdx.x; c0 < hi; c0 += kU * step) {

@@ -9,6 +9,6 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$ROOT/tools/bin/ab/$TAG
 mkdir -p "$OUT/obj"
 make -s -j8 -C "$ROOT/neurokmer_amd/csrc" OBJDIR="$OUT/obj" LIBDIR="$OUT" \
-  HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result -I$ROOT/include -munsafe-fp-atomics $EXTRA" \
+  CXXFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result -I$ROOT/include $EXTRA" \
   "$OUT/libneurokmer.so"
 echo "$OUT/libneurokmer.so"
