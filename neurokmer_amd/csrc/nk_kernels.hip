@@ -989,7 +989,10 @@ __device__ void top_post_block(const TopCand *top, const uint64_t *top_cur, uint
   }
 }
 
-constexpr int kLifPerThread = 8;
+#ifndef NK_LIF_PER_THREAD
+#define NK_LIF_PER_THREAD 8
+#endif
+constexpr int kLifPerThread = NK_LIF_PER_THREAD;
 
 constexpr int kLifBlock = 1024;
 constexpr int kLifWaves = kLifBlock / 64;
