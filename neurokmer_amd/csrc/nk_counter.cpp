@@ -519,7 +519,7 @@ static int plan_count(nk_counter *c, uint64_t est_bases, uint64_t slack, uint64_
   const uint64_t P = c->pool;
   if (!P) return NK_OK;
   const int k = (int)c->k;
-  const uint64_t B = (P + kBinsPerBucket - 1) >> kBinBits;
+  uint64_t B = (P + kBinsPerBucket - 1) >> kBinBits;
   cp.km = c->w128 ? 2 : (k > 32 ? 1 : 0);
   const bool keys_ok = cp.km == 0 || k <= 64;
   const bool wide_ok = keys_ok && P <= (1ull << 31);
@@ -529,6 +529,19 @@ static int plan_count(nk_counter *c, uint64_t est_bases, uint64_t slack, uint64_
   else if (keys_ok && B <= (uint64_t)kMaxBuckets) cp.path = CountPath::Gen;
   else if (wide_ok) cp.path = CountPath::Wide;
   if (cp.path == CountPath::Atomic) return NK_OK;
+#ifndef NK_PART_MIN_BITS
+#define NK_PART_MIN_BITS 15  // A/B: 13 (245 buckets at P = 2 M) costs K1a +20 us and the histogram +20 us
+#endif
+  int pbits = kBinBits;
+  if (cp.path == CountPath::Part) {
+    // bucket width: the narrowest from NK_PART_MIN_BITS that fits K1a's 256
+    // bucket counters.  Narrower buckets would need no histogram slices and a
+    // shorter uniques scan, but measured slower overall (more K1a segments and
+    // reservations, hotter LDS histogram bins): the default keeps 32768 bins
+    pbits = NK_PART_MIN_BITS;
+    while (pbits < kBinBits && ((P + (1ull << pbits) - 1) >> pbits) > 256) ++pbits;
+    B = (P + (1ull << pbits) - 1) >> pbits;
+  }
   cp.tile = kPartTile;
   const uint64_t est = std::max<uint64_t>(est_bases, 1);
   int rc;
@@ -564,6 +577,7 @@ static int plan_count(nk_counter *c, uint64_t est_bases, uint64_t slack, uint64_
   pa.fill = c->p_fill.p;
   pa.overflow = c->p_over.p;
   pa.currents = (unsigned long long *)c->cur.p;
+  pa.bin_bits = (uint32_t)pbits;
   if (cp.path == CountPath::Part) {
     if ((rc = c->p_pos.ensure(B * cap)) || (rc = c->p_desc.ensure(B * max_segs))) return rc;
     pa.pos = c->p_pos.p;
@@ -767,7 +781,8 @@ static int enqueue_lif(nk_counter *c, int streaming, uint32_t fuse_want, bool pa
     tf.cand = c->cand.p;
     tf.top_cur = c->top_cur.p;
     tf.post = PostArgs{c->set_alloc, part ? c->p_over.p : nullptr, part ? 1 : 0, c->set_mask_d.p,
-                       c->tbuckets.p, c->post_flags.p, c->uniq.p, c->special.p, c->n_hits.p};
+                       c->tbuckets.p, c->post_flags.p, c->uniq.p, c->special.p, c->n_hits.p,
+                       c->last_pa.bin_bits};
   }
   c->lif_zeroed = false;
   // steps == 0: the kernel leaves every neuron as it is (streaming returns early,
@@ -783,7 +798,7 @@ static int enqueue_lif(nk_counter *c, int streaming, uint32_t fuse_want, bool pa
   // only overflowed buckets added into them, so only those buckets are read
   const uint32_t *over = (!wire && c->pend_slices && c->part_used) ? c->p_over.p : nullptr;
   HIPCHK(launch_lif_apply(c->cur.p, wire ? wire : c->partials.p, wire ? 1u : c->pend_slices,
-                          wire ? 1 : 0, over, c->state_fresh ? 1 : 0, c->v.p,
+                          wire ? 1 : 0, over, (int)c->last_pa.bin_bits, c->state_fresh ? 1 : 0, c->v.p,
                           c->r.p, c->sc.p, c->pool, lp, c->lif_tbl.p, kLifTable, c->hist.p,
                           c->stats.p, tf, s));
   c->pend_slices = 0;
@@ -808,7 +823,7 @@ static int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, bool post_don
   if ((rc = c->tbuckets.ensure(m))) return rc;
   if (!post_done) HIPCHK(launch_top_post(c->cand.p, c->top_cur.p, m, c->set_alloc, part ? c->p_over.p : nullptr,
                          part ? 1 : 0, c->set_mask_d.p, c->tbuckets.p, c->post_flags.p, c->uniq.p,
-                         c->special.p, c->n_hits.p, s));
+                         c->special.p, c->n_hits.p, c->last_pa.bin_bits, s));
   // the set must be empty up to the pass's mask: after the count's prep it is
   c->dirty_before = c->set_clean ? 0 : c->set_alloc;
   if (!part || !c->set_clean)
@@ -1316,7 +1331,8 @@ int nk_wire32(nk_counter *c, uint32_t *d_wire, void *stream) {
   if (rc) return rc;
   // partitioned count with its partials pending: only overflowed buckets added into cur
   const uint32_t *over = (c->pend_slices && c->part_used) ? c->p_over.p : nullptr;
-  HIPCHK(launch_wire32(c->cur.p, c->partials.p, c->pend_slices, over, c->pool, d_wire, s));
+  HIPCHK(launch_wire32(c->cur.p, c->partials.p, c->pend_slices, over, (int)c->last_pa.bin_bits,
+                       c->pool, d_wire, s));
   c->pend_slices = 0;
   c->cur_in_wire = true;
   return NK_OK;

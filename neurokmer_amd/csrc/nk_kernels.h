@@ -57,6 +57,7 @@ struct PostArgs {
   uint32_t *uniq;
   uint32_t *special;
   unsigned long long *n_hits;
+  uint32_t bin_bits = kBinBits;  // of the partitioned count's buckets
 };
 
 // Top-N selection fused into the LIF kernel (want <= kFuseMaxTopN): every LIF
@@ -115,6 +116,7 @@ struct PartArgs {
   uint64_t max_segs;
   uint32_t *overflow;             // [bucket] region overflowed (records counted directly)
   unsigned long long *currents;   // overflow target
+  uint32_t bin_bits = kBinBits;   // bucket = neuron >> bin_bits (13..15 on the partitioned path)
 };
 
 // Generic partition (nk_wide.hip): any key mode; narrow (u16 offsets into
@@ -171,7 +173,7 @@ hipError_t launch_lif_table(LifEntry *tbl, int n, LifParams lp, hipStream_t s);
 // first (the fused K1c of a single-device process call) and is written back.
 // fresh: v/r/sc are taken as 0 (lazy reset) and every neuron is written.
 hipError_t launch_lif_apply(uint64_t *currents, const uint32_t *partials, uint32_t slices,
-                            int cur_zero, const uint32_t *over,
+                            int cur_zero, const uint32_t *over, int over_bits,
                             int fresh, float *v, uint32_t *r, uint64_t *sc, uint64_t pool, LifParams lp,
                             const LifEntry *tbl, int tbl_n, uint32_t *hist, uint64_t *stats,
                             const TopFuse &tf, hipStream_t s);
@@ -192,7 +194,7 @@ hipError_t launch_top_post(const TopCand *top, const uint64_t *top_cur, uint32_t
                            uint64_t set_alloc, const uint32_t *overflow, int part,
                            uint64_t *set_mask, uint32_t *tbuckets, uint32_t *flags,
                            uint32_t *uniq, uint32_t *special, unsigned long long *n_hits,
-                           hipStream_t s);
+                           uint32_t bin_bits, hipStream_t s);
 // --kmer-width=128 (k <= 64): the count, the top rows' uniques (set of 3
 // words per slot, u.set_keys), and the set helpers; keys outside the set are
 // (lo, hi) pairs of u64.
@@ -214,7 +216,8 @@ hipError_t launch_merge_prep(unsigned long long *set_keys, uint64_t *mask, uint6
                              uint32_t *uniq, uint32_t *special, uint32_t m, uint32_t *trunc,
                              hipStream_t s);
 hipError_t launch_wire32(const uint64_t *cur, const uint32_t *partials, uint32_t slices,
-                         const uint32_t *over, uint64_t pool, uint32_t *wire, hipStream_t s);
+                         const uint32_t *over, int over_bits, uint64_t pool, uint32_t *wire,
+                         hipStream_t s);
 hipError_t launch_export(const unsigned long long *set_keys, const uint64_t *set_mask,
                          uint64_t set_alloc, int w128, bool uniq, bool appended,
                          const uint32_t *special, uint32_t n_top, const TopState *st,

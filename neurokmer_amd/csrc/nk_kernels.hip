@@ -488,6 +488,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
   }
   const uint32_t kmask = (k >= 32) ? 0xFFFFFFFFu : ((1u << k) - 1u);
   const int topsh = twok - 2;
+  const uint32_t bbits = pa.bin_bits, bmask = (1u << bbits) - 1u;
   uint32_t E[kPartPerThread];  // bucket << 16 | rank
   uint32_t O[kPartPerThread];  // bin offset within the bucket
 #pragma unroll
@@ -514,10 +515,10 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
       }
     }
     const uint32_t idx = fastmod32(sip13_u64(key), fm);
-    const uint32_t b = ((ok >> j) & 1u) ? (idx >> kBinBits) : B;
+    const uint32_t b = ((ok >> j) & 1u) ? (idx >> bbits) : B;
     const uint32_t rank = atomicAdd(&s_cnt[b], 1u);
     E[j] = (b << 16) | rank;
-    O[j] = idx & (kBinsPerBucket - 1);
+    O[j] = idx & bmask;
   }
   __syncthreads();
   // exclusive scan of the padded bucket counts (one wave) + HBM reservation
@@ -603,7 +604,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
       const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
       for (int i = 0; i < 8; ++i)
         if ((w[i] & 0xFFFFu) != kPadOff)
-          atomicAdd(&pa.currents[((uint64_t)b << kBinBits) | (w[i] & 0xFFFFu)], 1ULL);
+          atomicAdd(&pa.currents[((uint64_t)b << pa.bin_bits) | (w[i] & 0xFFFFu)], 1ULL);
     }
   }
 }
@@ -611,13 +612,15 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
 // partials == nullptr: add the histogram into pa.currents instead (u64; plain
 // read-modify-write of the bins this workgroup owns when slices == 1, atomics
 // otherwise; bins that stayed zero are not touched)
+template <int BB>  // 2^BB bins per bucket (pa.bin_bits)
 __global__ __launch_bounds__(kHistBlock) void k_bucket_hist(PartArgs pa, uint64_t pool,
                                                             uint32_t slices,
                                                             uint32_t *__restrict__ partials) {
-  __shared__ uint32_t h[kBinsPerBucket + 1];  // + a spill bin for pad records
+  constexpr uint32_t kBins = 1u << BB;
+  __shared__ uint32_t h[kBins + 1];  // + a spill bin for pad records
   const uint32_t b = blockIdx.x, r = blockIdx.y;  // buckets on x: up to 65536 of them
-  for (int i = threadIdx.x; i <= kBinsPerBucket; i += kHistBlock) h[i] = 0;
-  auto bin = [](uint32_t off) { return off < (uint32_t)kBinsPerBucket ? off : (uint32_t)kBinsPerBucket; };
+  for (int i = threadIdx.x; i <= (int)kBins; i += kHistBlock) h[i] = 0;
+  auto bin = [](uint32_t off) { return off < kBins ? off : kBins; };
   __syncthreads();
   uint64_t n = pa.fill[b] & ((1ull << 40) - 1);
   if (n > pa.cap) n = pa.cap;
@@ -660,8 +663,8 @@ __global__ __launch_bounds__(kHistBlock) void k_bucket_hist(PartArgs pa, uint64_
   for (; j < hi8; j += step) hist8(*reinterpret_cast<const uint4 *>(src + j));
   for (uint64_t j = hi8 + threadIdx.x; j < hi; j += kHistBlock) atomicAdd(&h[bin(src[j])], 1u);
   __syncthreads();
-  const uint64_t nb0 = (uint64_t)b << kBinBits;
-  const uint64_t nbins = pool - nb0 < (uint64_t)kBinsPerBucket ? pool - nb0 : kBinsPerBucket;
+  const uint64_t nb0 = (uint64_t)b << BB;
+  const uint64_t nbins = pool - nb0 < (uint64_t)kBins ? pool - nb0 : kBins;
   if (!partials) {
     unsigned long long *cur = pa.currents + nb0;
     for (uint32_t t = threadIdx.x; t < nbins; t += kHistBlock) {
@@ -800,8 +803,8 @@ __global__ __launch_bounds__(kHistBlock) void k_uniq_scan(KmerInput in, int k, P
   __syncthreads();
   for (uint32_t s = threadIdx.x; s < u.n_top; s += kHistBlock) {
     const uint64_t idx = u.top[s].idx;
-    if ((idx >> kBinBits) == b) {
-      const uint32_t off = (uint32_t)(idx & (kBinsPerBucket - 1));
+    if ((idx >> pa.bin_bits) == b) {
+      const uint32_t off = (uint32_t)(idx & ((1u << pa.bin_bits) - 1u));
       const uint32_t t = atomicAdd(&t_n, 1u);
       t_off[t] = off;
       t_slot[t] = s;
@@ -962,7 +965,7 @@ __device__ void top_post_block(const TopCand *top, const uint64_t *top_cur, uint
   __shared__ uint32_t s_bk[kMaxTopN];
   if (threadIdx.x == 0) { s_sum = 0; s_nb = 0; s_over = 0; *pa.n_hits = 0; }
   for (uint32_t i = threadIdx.x; i < m; i += blockDim.x)
-    s_bk[i] = (uint32_t)(top[i].idx >> kBinBits);
+    s_bk[i] = (uint32_t)(top[i].idx >> pa.bin_bits);
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
     pa.uniq[i] = 0;
@@ -1247,7 +1250,7 @@ __device__ void final_top(uint64_t pool, const uint64_t *currents, uint32_t nb,
   const uint64_t idx = key_idx(key), sc = key_sc(key);
   const uint64_t cur = row ? currents[idx] : 0ull;
   const PostArgs &pa = tf.post;
-  const uint32_t bk = (uint32_t)(idx >> kBinBits);
+  const uint32_t bk = (uint32_t)(idx >> pa.bin_bits);
   const uint32_t over = (row && pa.part) ? pa.overflow[bk] : 0u;
   if (row) {
     tf.cand[lane].idx = idx;
@@ -1286,7 +1289,8 @@ __device__ void final_top(uint64_t pool, const uint64_t *currents, uint32_t nb,
 __global__ __launch_bounds__(kLifBlock) void k_lif_apply(uint64_t *__restrict__ currents,
                                                       const uint32_t *__restrict__ partials,
                                                       uint32_t slices, int cur_zero,
-                                                      const uint32_t *__restrict__ over, int fresh,
+                                                      const uint32_t *__restrict__ over,
+                                                      int over_bits, int fresh,
                                                       float *__restrict__ V,
                                                       uint32_t *__restrict__ R,
                                                       uint64_t *__restrict__ SC, uint64_t pool,
@@ -1316,7 +1320,7 @@ __global__ __launch_bounds__(kLifBlock) void k_lif_apply(uint64_t *__restrict__ 
     const uint64_t i = idx_of(j);
     // cur_zero: the partials (wire) hold it all; over: the count zeroed the
     // currents and only overflowed buckets added into them
-    cntv[j] = (cur_zero || (over && !over[i >> kBinBits])) ? 0ull : currents[i];
+    cntv[j] = (cur_zero || (over && !over[i >> over_bits])) ? 0ull : currents[i];
     scv[j] = fresh ? 0 : SC[i];
     vin[j] = fresh ? 0.0f : V[i];
     rin[j] = fresh ? 0u : R[i];
@@ -1654,11 +1658,11 @@ __global__ void k_pad_keys(const uint64_t *__restrict__ src, const unsigned long
 // over != nullptr (partitioned count): the zeroed currents only hold the
 // direct adds of overflowed buckets, so only those buckets are read
 __global__ void k_wire32(const uint64_t *__restrict__ cur, const uint32_t *__restrict__ partials,
-                         uint32_t slices, const uint32_t *__restrict__ over, uint64_t pool,
-                         uint32_t *__restrict__ wire) {
+                         uint32_t slices, const uint32_t *__restrict__ over, int over_bits,
+                         uint64_t pool, uint32_t *__restrict__ wire) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < pool;
        i += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t x = (!over || over[i >> kBinBits]) ? cur[i] : 0ull;
+    uint64_t x = (!over || over[i >> over_bits]) ? cur[i] : 0ull;
     for (uint32_t r = 0; r < slices; ++r) x += partials[(uint64_t)r * pool + i];
     wire[i] = (uint32_t)x;
   }
@@ -1742,11 +1746,13 @@ hipError_t launch_merge_prep(unsigned long long *set_keys, uint64_t *mask, uint6
 }
 
 hipError_t launch_wire32(const uint64_t *cur, const uint32_t *partials, uint32_t slices,
-                         const uint32_t *over, uint64_t pool, uint32_t *wire, hipStream_t s) {
+                         const uint32_t *over, int over_bits, uint64_t pool, uint32_t *wire,
+                         hipStream_t s) {
   if (!pool) return hipSuccess;
   unsigned g = (unsigned)((pool + 255) / 256);
   if (g > 8192) g = 8192;
-  hipLaunchKernelGGL(k_wire32, dim3(g), dim3(256), 0, s, cur, partials, slices, over, pool, wire);
+  hipLaunchKernelGGL(k_wire32, dim3(g), dim3(256), 0, s, cur, partials, slices, over, over_bits, pool,
+                     wire);
   return hipGetLastError();
 }
 
@@ -1827,14 +1833,14 @@ uint32_t lif_blocks(uint64_t pool) {
 }
 
 hipError_t launch_lif_apply(uint64_t *currents, const uint32_t *partials, uint32_t slices,
-                            int cur_zero, const uint32_t *over, int fresh, float *v, uint32_t *r, uint64_t *sc, uint64_t pool, LifParams lp,
+                            int cur_zero, const uint32_t *over, int over_bits, int fresh, float *v, uint32_t *r, uint64_t *sc, uint64_t pool, LifParams lp,
                             const LifEntry *tbl, int tbl_n, uint32_t *hist, uint64_t *stats,
                             const TopFuse &tf, hipStream_t s) {
   if (!pool) return hipSuccess;
   const unsigned g = lif_blocks(pool);
   if (tf.want && (tf.want > kFuseMaxTopN || g > kFuseMaxBlocks || pool > (1ull << 24)))
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_lif_apply, dim3(g), dim3(kLifBlock), 0, s, currents, partials, slices, cur_zero, over, fresh,
+  hipLaunchKernelGGL(k_lif_apply, dim3(g), dim3(kLifBlock), 0, s, currents, partials, slices, cur_zero, over, over_bits, fresh,
                      v, r, sc, pool, lp, tbl, tbl_n, hist, (unsigned long long *)stats, tf);
   if (tf.want)
     hipLaunchKernelGGL(k_top_final, dim3(1), dim3(kLifBlock), 0, s, pool, currents, g, tf);
@@ -2008,8 +2014,13 @@ hipError_t launch_part(const KmerInput &in, int k, int canonical, uint64_t pool,
 hipError_t launch_bucket_hist(const PartArgs &pa, uint64_t pool, uint32_t slices,
                               uint32_t *partials, hipStream_t s) {
   if (!pa.n_buckets) return hipSuccess;
-  hipLaunchKernelGGL(k_bucket_hist, dim3(pa.n_buckets, slices), dim3(kHistBlock), 0, s, pa, pool,
-                     slices, partials);
+  const dim3 g(pa.n_buckets, slices);
+  switch (pa.bin_bits) {
+    case 13: hipLaunchKernelGGL(k_bucket_hist<13>, g, dim3(kHistBlock), 0, s, pa, pool, slices, partials); break;
+    case 14: hipLaunchKernelGGL(k_bucket_hist<14>, g, dim3(kHistBlock), 0, s, pa, pool, slices, partials); break;
+    case 15: hipLaunchKernelGGL(k_bucket_hist<15>, g, dim3(kHistBlock), 0, s, pa, pool, slices, partials); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
@@ -2051,8 +2062,8 @@ hipError_t launch_top_post(const TopCand *top, const uint64_t *top_cur, uint32_t
                            uint64_t set_alloc, const uint32_t *overflow, int part,
                            uint64_t *set_mask, uint32_t *tbuckets, uint32_t *flags,
                            uint32_t *uniq, uint32_t *special, unsigned long long *n_hits,
-                           hipStream_t s) {
-  PostArgs pa{set_alloc, overflow, part, set_mask, tbuckets, flags, uniq, special, n_hits};
+                           uint32_t bin_bits, hipStream_t s) {
+  PostArgs pa{set_alloc, overflow, part, set_mask, tbuckets, flags, uniq, special, n_hits, bin_bits};
   hipLaunchKernelGGL(k_top_post, dim3(1), dim3(1024), 0, s, top, top_cur, m, pa);
   return hipGetLastError();
 }
