@@ -612,7 +612,10 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
 // partials == nullptr: add the histogram into pa.currents instead (u64; plain
 // read-modify-write of the bins this workgroup owns when slices == 1, atomics
 // otherwise; bins that stayed zero are not touched)
-template <int BB>  // 2^BB bins per bucket (pa.bin_bits)
+#ifndef NK_HIST_KU
+#define NK_HIST_KU 4
+#endif
+template <int BB, int KU = NK_HIST_KU>  // 2^BB bins per bucket (pa.bin_bits)
 __global__ __launch_bounds__(kHistBlock) void k_bucket_hist(PartArgs pa, uint64_t pool,
                                                             uint32_t slices,
                                                             uint32_t *__restrict__ partials) {
@@ -632,35 +635,41 @@ __global__ __launch_bounds__(kHistBlock) void k_bucket_hist(PartArgs pa, uint64_
     if (threadIdx.x == 0) atomicAdd(&h[bin(src[i])], 1u);
   const uint64_t hi8 = i + ((hi - i) & ~7ull);
   const uint64_t step = 8ull * kHistBlock;
-  uint64_t j = i + 8ull * threadIdx.x;
-  // four 16-B loads per lane per round, software-pipelined: the next round's
-  // loads are in flight while this round's 32 LDS atomics issue
+  // NK_HIST_KU 16-B loads per lane per round, software-pipelined: the next
+  // round's loads are in flight while this round's 8*KU LDS atomics issue.
+  // Loads past hi8 are clamped to a valid address (static wait counts) and
+  // their records skipped, so there is no serial tail of single loads.
   auto hist8 = [&](const uint4 &v) {
     atomicAdd(&h[bin(v.x & 0xFFFFu)], 1u); atomicAdd(&h[bin(v.x >> 16)], 1u);
     atomicAdd(&h[bin(v.y & 0xFFFFu)], 1u); atomicAdd(&h[bin(v.y >> 16)], 1u);
     atomicAdd(&h[bin(v.z & 0xFFFFu)], 1u); atomicAdd(&h[bin(v.z >> 16)], 1u);
     atomicAdd(&h[bin(v.w & 0xFFFFu)], 1u); atomicAdd(&h[bin(v.w >> 16)], 1u);
   };
-  if (j + 3 * step < hi8) {
-    uint4 cur[4];
+  uint64_t j = i + 8ull * threadIdx.x;
+  if (j < hi8) {
+    auto load_round = [&](uint64_t jb, uint4 *v) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) cur[t] = *reinterpret_cast<const uint4 *>(src + j + t * step);
+      for (int t = 0; t < KU; ++t) {
+        const uint64_t jt = jb + (uint64_t)t * step;
+        v[t] = *reinterpret_cast<const uint4 *>(src + (jt < hi8 ? jt : i));
+      }
+    };
+    uint4 cur[KU];
+    load_round(j, cur);
     for (;;) {
-      const uint64_t jn = j + 4 * step;
-      const bool more = jn + 3 * step < hi8;
-      uint4 nxt[4];  // unconditional (clamped) loads keep the wait counts static
-      const uint64_t jl = more ? jn : j;
+      const uint64_t jn = j + (uint64_t)KU * step;
+      const bool more = jn < hi8;
+      uint4 nxt[KU];
+      load_round(more ? jn : j, nxt);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) nxt[t] = *reinterpret_cast<const uint4 *>(src + jl + t * step);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) hist8(cur[t]);
-      j = jn;
+      for (int t = 0; t < KU; ++t)
+        if (j + (uint64_t)t * step < hi8) hist8(cur[t]);
       if (!more) break;
+      j = jn;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) cur[t] = nxt[t];
+      for (int t = 0; t < KU; ++t) cur[t] = nxt[t];
     }
   }
-  for (; j < hi8; j += step) hist8(*reinterpret_cast<const uint4 *>(src + j));
   for (uint64_t j = hi8 + threadIdx.x; j < hi; j += kHistBlock) atomicAdd(&h[bin(src[j])], 1u);
   __syncthreads();
   const uint64_t nb0 = (uint64_t)b << BB;

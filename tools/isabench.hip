@@ -16,9 +16,16 @@
   asm volatile(ASM : "+v"(a4) : "v"(b0), "v"(c0)); asm volatile(ASM : "+v"(a5) : "v"(b0), "v"(c0)); \
   asm volatile(ASM : "+v"(a6) : "v"(b0), "v"(c0)); asm volatile(ASM : "+v"(a7) : "v"(b0), "v"(c0));
 
+#define CHAIN8S(ASM)                                                                      \
+  asm volatile(ASM : "+v"(a0) : "s"(s0)); asm volatile(ASM : "+v"(a1) : "s"(s0));         \
+  asm volatile(ASM : "+v"(a2) : "s"(s0)); asm volatile(ASM : "+v"(a3) : "s"(s0));         \
+  asm volatile(ASM : "+v"(a4) : "s"(s0)); asm volatile(ASM : "+v"(a5) : "s"(s0));         \
+  asm volatile(ASM : "+v"(a6) : "s"(s0)); asm volatile(ASM : "+v"(a7) : "s"(s0));
+
 template <int OP>
 __global__ __launch_bounds__(256) void kop(uint32_t *out, uint64_t *clk) {
   uint32_t b0 = threadIdx.x * 7 + 1, c0 = threadIdx.x ^ 0x55;
+  uint32_t s0 = __builtin_amdgcn_readfirstlane(b0 ^ 0x74656462u);
   uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5,
            a6 = a0 + 6, a7 = a0 + 7;
   uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
@@ -50,6 +57,15 @@ __global__ __launch_bounds__(256) void kop(uint32_t *out, uint64_t *clk) {
 #define SWP(A, B) asm volatile("v_swap_b32 %0, %1" : "+v"(A), "+v"(B));
       SWP(a0, a1) SWP(a2, a3) SWP(a4, a5) SWP(a6, a7) SWP(a1, a2) SWP(a3, a4) SWP(a5, a6) SWP(a7, a0)
     }
+    if (OP == 25) { CHAIN8("v_xor_b32_e32 %0, 0x74656462, %0") }
+    if (OP == 26) { CHAIN8S("v_xor_b32_e32 %0, %1, %0") }
+    if (OP == 27) { CHAIN8("v_lshlrev_b32_e32 %0, 13, %0") }
+    if (OP == 28) { CHAIN8("v_cndmask_b32_e32 %0, %0, %1, vcc") }
+    if (OP == 29) { CHAIN8("v_and_b32_e32 %0, 0x3fffffff, %0") }
+    if (OP == 30) { CHAIN8("v_min_u32_e32 %0, %0, %1") }
+    if (OP == 31) { CHAIN8("v_sub_u32_e32 %0, %0, %1") }
+    if (OP == 32) { CHAIN8("v_lshlrev_b32_e64 %0, 13, %0") }
+    if (OP == 33) { CHAIN8("v_xor_b32_e64 %0, %0, %1") }
     if (OP == 24) {  // 64-bit add as a VOP2 carry pair through VCC
 #define ADC(L, H) asm volatile("v_add_co_u32_e32 %0, vcc, %0, %2\n\tv_addc_co_u32_e32 %1, vcc, %1, %3, vcc" : "+v"(L), "+v"(H) : "v"(b0), "v"(c0) : "vcc");
       ADC(a0, a1) ADC(a2, a3) ADC(a4, a5) ADC(a6, a7)
@@ -146,6 +162,15 @@ int main() {
   run("v_mov_b32_e32", kop<22>, out, clk);
   run("v_swap_b32 (8/iter)", kop<23>, out, clk);
   run("add_co+addc_co e32 (4 pairs)", kop<24>, out, clk);
+  run("v_xor_b32_e32 literal", kop<25>, out, clk);
+  run("v_xor_b32_e32 sgpr", kop<26>, out, clk);
+  run("v_lshlrev_b32_e32", kop<27>, out, clk);
+  run("v_cndmask_b32_e32 vcc", kop<28>, out, clk);
+  run("v_and_b32_e32 literal", kop<29>, out, clk);
+  run("v_min_u32_e32", kop<30>, out, clk);
+  run("v_sub_u32_e32", kop<31>, out, clk);
+  run("v_lshlrev_b32_e64", kop<32>, out, clk);
+  run("v_xor_b32_e64", kop<33>, out, clk);
   run("v_lshl_add_u64", kop64<0>, out, clk);
   run("v_pk_mov_b32 swap", kop64<3>, out, clk);
   run("v_mov_b64_e32", kop64<4>, out, clk);
