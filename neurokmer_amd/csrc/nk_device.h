@@ -19,7 +19,10 @@ namespace nk {
 // 32 is a free register swap), and xors stay 32-bit VOP2: 70 clk per SipRound.
 // (Building the swapped v0/v2 pairs with one v_pk_mov_b32 instead of two
 // v_mov_b32 is 4 % faster in isolation, tools/sipbench.hip V3, but made the
-// count kernel 6 % slower in an A/B on one box, tools/ab_run.sh: not used.)
+// count kernel 6 % slower in an A/B on one box, tools/ab_run.sh: not used.
+// Likewise adding a swapped operand as v_mad_u64_u32(w.hi, 1, x) plus a 32-bit
+// add on the high word, in inline asm, removes 12 of the 21 v_mov_b32 per
+// k-mer but made K1a 7 % slower in an A/B: not used.)
 __device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) {
   const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
   const uint32_t nlo = __builtin_amdgcn_alignbit(lo, hi, 32 - r);

@@ -43,8 +43,8 @@ def main(src, dst):
         return 1
     m = means[name]
     if "FETCH_SIZE" not in m or "WRITE_SIZE" not in m:
-        print("FETCH_SIZE / WRITE_SIZE missing:", sorted(m))
-        return 1
+        print("no FETCH_SIZE / WRITE_SIZE in this pass (per-kernel means only):", sorted(m))
+        return 0
     fetch = m["FETCH_SIZE"] * 1024.0
     write = m["WRITE_SIZE"] * 1024.0
     valu = {}
