@@ -122,15 +122,16 @@ __device__ __forceinline__ int probe_top(const uint64_t *tbl_idx, const uint32_t
 __device__ void build_top_tbl(const UniqArgs &u, uint64_t *tbl_idx, uint32_t *tbl_slot) {
   for (uint32_t i = threadIdx.x; i < u.tbl_size; i += blockDim.x) tbl_idx[i] = kEmpty;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t mask = u.tbl_size - 1;
-    for (uint32_t s = 0; s < u.n_top; ++s) {
-      uint64_t idx = u.top[s].idx;
-      uint32_t h = (uint32_t)idx & mask;
-      while (tbl_idx[h] != kEmpty) h = (h + 1) & mask;
-      tbl_idx[h] = idx;
-      tbl_slot[h] = s;
-    }
+  // parallel insertion (the top rows are distinct neurons): one global load
+  // per thread instead of n_top dependent loads on one thread
+  const uint32_t mask = u.tbl_size - 1;
+  for (uint32_t s = threadIdx.x; s < u.n_top; s += blockDim.x) {
+    const uint64_t idx = u.top[s].idx;
+    uint32_t h = (uint32_t)idx & mask;
+    while (atomicCAS(reinterpret_cast<unsigned long long *>(&tbl_idx[h]), (unsigned long long)kEmpty,
+                     (unsigned long long)idx) != (unsigned long long)kEmpty)
+      h = (h + 1) & mask;
+    tbl_slot[h] = s;
   }
   __syncthreads();
 }

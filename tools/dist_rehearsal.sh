@@ -12,5 +12,6 @@ timeout -k 10 300 python bench.py --steps 20 --warmup 2 --no-cpu-baseline > gpur
 tail -1 gpurun_out/reh_plain.log | cut -c1-400
 timeout -k 10 300 python bench.py --steps 20 --warmup 2 --no-cpu-baseline --force-dist > gpurun_out/reh_dist.log 2>&1 || exit $?
 tail -1 gpurun_out/reh_dist.log | cut -c1-400
+mkdir -p $ROOT/gpurun_out/prof_reh
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/gpurun_out/prof_reh/trace -o run -- python3 $ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --force-dist > $ROOT/gpurun_out/prof_reh/trace.log 2>&1
