@@ -55,7 +55,9 @@ typedef struct nk_opts {
   uint32_t stage_timing; /* 0 (default): HIP events around the count kernel only
                             (nk_last_timings: index, count, post, total);
                             1: an event between every stage (each costs ~6 us
-                            of GPU idle time on MI355X) */
+                            of GPU idle time on MI355X);
+                            2: events at both ends of a call only (no event
+                            between two kernels; no count-kernel time) */
   uint32_t exact_counts; /* 1: also build the exact k-mer count table on the
                             device (the reference's `counts` DashMap and the full
                             `kmer_per_neuron`, src/spiking_hash.rs:27,157-172):
@@ -234,7 +236,10 @@ int nk_copy_currents(nk_counter *c, uint64_t *out, size_t n);
 int nk_copy_spike_counts(nk_counter *c, uint64_t *out, size_t n);
 int nk_copy_voltages(nk_counter *c, float *out, size_t n);
 int nk_copy_refractory(nk_counter *c, uint32_t *out, size_t n);
-/* Device pointer of the u64 currents vector (pool_size entries). */
+/* Device pointer of the u64 currents vector (pool_size entries).  Pending
+ * partial sums are folded first.  The vector is complete on the stream of the
+ * last call that passed one; after a call on the handle's own stream (NULL)
+ * this waits for that stream, so any stream may read it.  NULL on error. */
 uint64_t *nk_device_currents(nk_counter *c);
 /* Resets neurons, currents and energy to the state nk_new() left them in. */
 int nk_reset(nk_counter *c);
@@ -252,6 +257,16 @@ int nk_last_timings(const nk_counter *c, const char **names, float *ms, int cap)
  * timed step's K1 duration after its timed loop.  Returns the number written.
  * (No reference counterpart: measurement only.) */
 int nk_count_history(const nk_counter *c, float *ms, int cap);
+/* Sets nk_opts.stage_timing (0, 1 or 2) for later calls on this handle, e.g. 2
+ * for timed benchmark steps and 0 for a separate count-kernel measurement.
+ * (No reference counterpart: measurement only.) */
+int nk_set_stage_timing(nk_counter *c, uint32_t level);
+/* Diagnostic: the best of `reps` device times (ms) of a kernel that computes
+ * SipHash-1-3 (key 0) of n_keys u64 keys generated in registers plus the exact
+ * `% pool` (nk_device.h: sip13_u64 + fastmod32, the count kernel's per-k-mer
+ * hash work with no memory traffic).  Measures the VALU floor of the count
+ * kernel live on the device.  (No reference counterpart.) */
+int nk_diag_hash_ms(int device, uint64_t n_keys, uint64_t pool, int reps, float *ms);
 
 const char *nk_last_error(void);
 const char *nk_version(void);

@@ -262,9 +262,22 @@ class SpikingKmerCounter:
         n = self._L.nk_last_timings(self._h, names, ms, 8)
         return {names[i].decode(): float(ms[i]) for i in range(n)}
 
+    def set_stage_timing(self, level: int) -> None:
+        """0: events around the count kernel (default); 1: every stage; 2: only
+        at both ends of a call (no event between kernels, no K1 time)."""
+        _lib.check(self._L.nk_set_stage_timing(self._h, level))
+
     def count_history(self, n: int) -> list:
         """K1 (count kernel) device time in ms of each of the last min(n, 256)
         accumulate/process calls, oldest first (hipEvents around the launch)."""
         buf = (C.c_float * max(n, 1))()
         m = self._L.nk_count_history(self._h, buf, n)
         return [float(buf[i]) for i in range(m)]
+
+
+def diag_hash_ms(n_keys: int, pool: int, device: int = 0, reps: int = 5) -> float:
+    """Best device time (ms) of SipHash-1-3 + exact % pool over n_keys keys
+    generated in registers: the count kernel's hash floor (nk_diag_hash_ms)."""
+    ms = C.c_float(0.0)
+    _lib.check(_lib.load().nk_diag_hash_ms(device, n_keys, pool, reps, C.byref(ms)))
+    return float(ms.value)

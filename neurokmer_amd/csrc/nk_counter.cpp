@@ -205,8 +205,12 @@ struct nk_counter {
 };
 
 // ev[i] for the stage timings; the inner stage boundaries only in full mode
+// (stage_timing 0: also around the count kernel; 1: every stage; 2: the ends
+// of a call only, so no event sits between two kernels)
+static bool full_timing(const nk_counter *c) { return c->opts.stage_timing == 1; }
+static bool count_timing(const nk_counter *c) { return c->opts.stage_timing != 2; }
 static hipError_t mark(nk_counter *c, int i, hipStream_t s) {
-  if (c->opts.stage_timing || i == 0 || i == 1 || i == 2 || i == 6 || i == 7)
+  if (full_timing(c) || i == 0 || i == 6 || i == 7 || (count_timing(c) && (i == 1 || i == 2)))
     return hipEventRecord(c->ev[i], s);
   return hipSuccess;
 }
@@ -510,6 +514,13 @@ static int wide_bits_forced() {
   return e ? atoi(e) : 0;
 }
 
+// tests: NK_FORCE_ATOMIC=1 forces the direct-atomic count kernels (k_kmers,
+// k_kmers_compat, k_kmers128), which otherwise run only past the partitions
+static bool atomic_forced() {
+  const char *e = getenv("NK_FORCE_ATOMIC");
+  return e && atoi(e) != 0;
+}
+
 // Sizes the buffers for a batch of about est_bases bases (slack: extra
 // records per bucket region; max_segs: Part's descriptors per bucket) and
 // lists the arrays to zero before the first batch.
@@ -524,6 +535,7 @@ static int plan_count(nk_counter *c, uint64_t est_bases, uint64_t slack, uint64_
   const bool keys_ok = cp.km == 0 || k <= 64;
   const bool wide_ok = keys_ok && P <= (1ull << 31);
   const int forced = wide_bits_forced();
+  if (atomic_forced()) return NK_OK;  // tests: the direct-atomic kernels at any size
   if (forced > 0 && wide_ok) cp.path = CountPath::Wide;
   else if (cp.km == 0 && B <= (uint64_t)kMaxBuckets) cp.path = CountPath::Part;
   else if (keys_ok && B <= (uint64_t)kMaxBuckets) cp.path = CountPath::Gen;
@@ -663,7 +675,7 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
     z.ptr[z.n] = c->stats.p; z.bytes[z.n++] = 16;
     c->lif_zeroed = true;
   }
-  {
+  if (count_timing(c)) {  // level 2 records no count-kernel events
     const int slot = (int)(c->cnt_calls++ % nk_counter::kCountRing);
     c->ev[1] = c->cnt_ev[slot][0];
     c->ev[2] = c->cnt_ev[slot][1];
@@ -1028,7 +1040,7 @@ static void collect_timings_now(nk_counter *c, bool with_count);
 // the timings are read when asked for.
 static void collect_timings(nk_counter *c, bool with_count) {
   c->timing_pending = with_count ? 2 : 1;
-  c->n_stage = c->opts.stage_timing ? kStages : kStagesLight;
+  c->n_stage = full_timing(c) ? kStages : kStagesLight;
 }
 
 static void collect_timings_now(nk_counter *c, bool with_count) {
@@ -1039,10 +1051,11 @@ static void collect_timings_now(nk_counter *c, bool with_count) {
     float ms = 0;
     return hipEventElapsedTime(&ms, a, b) == hipSuccess ? ms : 0.0f;
   };
-  if (!c->opts.stage_timing) {
-    c->stage_ms[0] = with_count ? el(c->ev[0], c->ev[1]) : 0.0f;
-    c->stage_ms[1] = with_count ? el(c->ev[1], c->ev[2]) : 0.0f;
-    c->stage_ms[2] = el(with_count ? c->ev[2] : c->ev[7], c->ev[6]);
+  if (!full_timing(c)) {
+    const bool wc = with_count && count_timing(c);  // no count markers at level 2
+    c->stage_ms[0] = wc ? el(c->ev[0], c->ev[1]) : (with_count ? -1.0f : 0.0f);
+    c->stage_ms[1] = wc ? el(c->ev[1], c->ev[2]) : (with_count ? -1.0f : 0.0f);
+    c->stage_ms[2] = with_count && !wc ? -1.0f : el(with_count ? c->ev[2] : c->ev[7], c->ev[6]);
     c->stage_ms[3] = el(with_count ? c->ev[0] : c->ev[7], c->ev[6]);
     c->n_stage = kStagesLight;
     return;
@@ -1996,6 +2009,14 @@ uint64_t *nk_device_currents(nk_counter *c) {
     hipStream_t s = pick_stream(c, nullptr);
     if (materialize(c, true, s) || fold_pending(c, s) || hipStreamSynchronize(s) != hipSuccess)
       return nullptr;
+  } else if (c->last_s && c->last_s == c->own_stream) {
+    // the last call ran on the handle's private stream, which the caller
+    // cannot order against: wait for it (a caller stream stays the caller's)
+    (void)hipSetDevice(c->device);
+    if (hipStreamSynchronize(c->own_stream) != hipSuccess) {
+      fail(NK_E_DEVICE, "hipStreamSynchronize failed");
+      return nullptr;
+    }
   }
   return c->cur.p;
 }
@@ -2007,6 +2028,44 @@ int nk_copy_spike_counts(nk_counter *c, uint64_t *out, size_t n) {
 int nk_copy_voltages(nk_counter *c, float *out, size_t n) { return copy_out(c, c->v, out, n); }
 int nk_copy_refractory(nk_counter *c, uint32_t *out, size_t n) {
   return copy_out(c, c->r, out, n);
+}
+
+int nk_diag_hash_ms(int device, uint64_t n_keys, uint64_t pool, int reps, float *ms) {
+  if (!ms || !n_keys || !pool || pool >= (1ull << 30) || reps < 1)
+    return fail(NK_E_INVALID, "nk_diag_hash_ms: n_keys, pool in [1, 2^30), reps >= 1, ms");
+  if (hipSetDevice(device) != hipSuccess) return fail(NK_E_NO_DEVICE, "hipSetDevice failed");
+  uint32_t *out = nullptr;
+  hipStream_t s = nullptr;
+  hipEvent_t a = nullptr, b = nullptr;
+  int rc = NK_OK;
+  float best = 1e30f;
+  if (hipMalloc(&out, diag_hash_out_words(n_keys) * 4) != hipSuccess) return fail(NK_E_OOM, "hipMalloc");
+  if (hipStreamCreate(&s) != hipSuccess || hipEventCreate(&a) != hipSuccess ||
+      hipEventCreate(&b) != hipSuccess) {
+    rc = fail(NK_E_DEVICE, "stream/event creation failed");
+  }
+  for (int i = 0; rc == NK_OK && i < reps + 1; ++i) {  // + 1 untimed warm-up
+    float t = 0.0f;
+    if (hipEventRecord(a, s) != hipSuccess || launch_diag_hash(n_keys, pool, out, s) != hipSuccess ||
+        hipEventRecord(b, s) != hipSuccess || hipEventSynchronize(b) != hipSuccess ||
+        hipEventElapsedTime(&t, a, b) != hipSuccess)
+      rc = fail(NK_E_DEVICE, "diag hash kernel failed");
+    else if (i > 0 && t < best)
+      best = t;
+  }
+  if (a) (void)hipEventDestroy(a);
+  if (b) (void)hipEventDestroy(b);
+  if (s) (void)hipStreamDestroy(s);
+  (void)hipFree(out);
+  if (rc == NK_OK) *ms = best;
+  return rc;
+}
+
+int nk_set_stage_timing(nk_counter *c, uint32_t level) {
+  if (!c) return fail(NK_E_INVALID, "null counter");
+  if (level > 2) return fail(NK_E_INVALID, "stage timing level must be 0, 1 or 2");
+  c->opts.stage_timing = level;
+  return NK_OK;
 }
 
 int nk_count_history(const nk_counter *c, float *ms, int cap) {
@@ -2036,7 +2095,7 @@ int nk_last_timings(const nk_counter *c, const char **names, float *ms, int cap)
   }
   int n = std::min(cap, c->n_stage);
   for (int i = 0; i < n; ++i) {
-    if (names) names[i] = c->opts.stage_timing ? kStageNames[i] : kStageNamesLight[i];
+    if (names) names[i] = full_timing(c) ? kStageNames[i] : kStageNamesLight[i];
     if (ms) ms[i] = c->stage_ms[i];
   }
   return n;

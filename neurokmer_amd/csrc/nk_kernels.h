@@ -169,6 +169,9 @@ hipError_t launch_count(const KmerInput &in, int k, int canonical, uint64_t pool
 hipError_t launch_uniques(const KmerInput &in, int k, int canonical, uint64_t pool,
                           const UniqArgs &u, hipStream_t s);
 hipError_t launch_lif_table(LifEntry *tbl, int n, LifParams lp, hipStream_t s);
+// diagnostic: SipHash-1-3 + % pool of n_keys register-generated keys
+hipError_t launch_diag_hash(uint64_t n_keys, uint64_t pool, uint32_t *out, hipStream_t s);
+uint64_t diag_hash_out_words(uint64_t n_keys);
 // partials/slices: when slices > 0, currents[i] += sum of the K1b partials
 // first (the fused K1c of a single-device process call) and is written back.
 // fresh: v/r/sc are taken as 0 (lazy reset) and every neuron is written.

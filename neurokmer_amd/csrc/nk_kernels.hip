@@ -428,6 +428,17 @@ struct PartShape {
   using GMap = typename std::conditional<(MAXB > 256), uint16_t, uint8_t>::type;
 };
 
+#if defined(NK_ABL_STAMPS)  // ablation build: per-workgroup phase timestamps
+__device__ unsigned long long g_stamps[1 << 18];
+#define NK_STAMP(I)                                                              \
+  do {                                                                           \
+    if (threadIdx.x == 0 && blockIdx.x < (1u << 14))                             \
+      g_stamps[blockIdx.x * 16 + (I)] = (I) == 0 || (I) == 7                     \
+          ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();    \
+  } while (0)
+#else
+#define NK_STAMP(I) do {} while (0)
+#endif
 template <bool CANON, int MAXB>
 __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMod fm, PartArgs pa) {
   using S = PartShape<MAXB>;
@@ -446,8 +457,15 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
   const uint64_t tile = in.tile_base + blockIdx.x;
   const uint64_t T0 = tile * (uint64_t)kPartTile;
   const uint32_t B = pa.n_buckets;
+  NK_STAMP(0);
+  NK_STAMP(8);
   for (uint32_t b = tid; b <= B; b += kPartBlock) s_cnt[b] = 0;
   stage_tile<kPartTile, kPartBlock, !CANON, !CANON>(L, in, tile, k);  // syncs (INV: pack_kmer only)
+  NK_STAMP(2);
+#if defined(NK_ABL_STAGEONLY)  // ablation: staging only
+  if (L.F[tid] == 0x12345678u && tid == 1000000) pa.overflow[0] = 1u;
+  return;
+#endif
 
   // phase 1: this lane's 16 consecutive positions q0..q0+15.  The first
   // window is extracted from the bit streams, the next 15 are rolled in from
@@ -524,13 +542,28 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
         key = pk;
       }
     }
+#if defined(NK_ABL_NOHASH)  // ablation builds only (tools/ablate_k1a.sh): hash -> identity
+    const uint32_t idx = fastmod32(key, fm);
+#else
     const uint32_t idx = fastmod32(sip13_u64(key), fm);
+#endif
     const uint32_t b = ((ok >> j) & 1u) ? (idx >> bbits) : B;
+#if defined(NK_ABL_NORANK)  // ablation: no LDS rank atomic (records collide; timing only)
+    const uint32_t rank = (uint32_t)j;
+    if (tid == 0 && j == 0) atomicAdd(&s_cnt[b], 1u);
+#else
     const uint32_t rank = atomicAdd(&s_cnt[b], 1u);
+#endif
     E[j] = (b << 16) | rank;
     O[j] = idx & bmask;
   }
   __syncthreads();
+  NK_STAMP(3);
+#if defined(NK_ABL_NOSORT)  // ablation: stop after the hash + rank phase
+  if (tid == 0) pa.overflow[0] = s_cnt[0] == 0x7FFFFFFFu;
+  if (E[0] == 0xFFFFFFFFu || O[kPartPerThread - 1] == 0xFFFFFFFFu) pa.overflow[1] = 1u;
+  return;
+#endif
   // exclusive scan of the padded bucket counts (one wave) + HBM reservation
   // (one atomic per non-empty bucket: entries in the low 40 bits, segments
   // above).  Reservations are multiples of 8 records, so every segment starts
@@ -569,6 +602,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
     s_fit[b] = fit;
   }
   __syncthreads();
+  NK_STAMP(4);
   // phase 2: counting-sort the records in LDS (positions that start no k-mer
   // land in the dummy bucket's region after the last group and are dropped);
   // one thread per bucket writes its pad records and its group map entries
@@ -586,6 +620,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
     for (uint32_t g = st >> 3; g < (st + cp) >> 3; ++g) s_gmap[g] = (typename S::GMap)b;
   }
   __syncthreads();
+  NK_STAMP(5);
   // phase 3: each thread moves 8-record groups -> one 16-B store into the
   // offset array and one into the position array
   const uint32_t n_groups = s_start[B] >> 3;
@@ -597,6 +632,10 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
     const uint32_t j8 = g * 8 - s_start[b];
     const uint4 w0 = *reinterpret_cast<const uint4 *>(&s_sorted[g * 8]);
     const uint4 w1 = *reinterpret_cast<const uint4 *>(&s_sorted[g * 8 + 4]);
+#if defined(NK_ABL_NOWRITE)  // ablation: LDS sort kept, no HBM record stores
+    if (w0.x == 0x12345678u && w1.w == 0x9ABCDEF0u) pa.overflow[b] = 1u;
+    continue;
+#endif
     if (j8 < s_fit[b]) {
       const uint64_t dst = (uint64_t)b * pa.cap + s_base[b] + j8;
       // v_perm: bytes {lo16(a), lo16(b)} and {hi16(a), hi16(b)}
@@ -620,6 +659,18 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
           atomicAdd(&pa.currents[((uint64_t)b << pa.bin_bits) | (w[i] & 0xFFFFu)], 1ULL);
     }
   }
+#if defined(NK_ABL_STAMPS)
+  __syncthreads();
+  NK_STAMP(6);
+  if (threadIdx.x == 0 && blockIdx.x < (1u << 14)) {
+    unsigned hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g_stamps[blockIdx.x * 16 + 1] = ((unsigned long long)xcc << 32) | hw;
+  }
+  NK_STAMP(7);
+#endif
 }
 
 // partials == nullptr: add the histogram into pa.currents instead (u64; plain
@@ -2206,3 +2257,44 @@ hipError_t launch_gather(const TopState *st, const uint64_t *stats, const uint64
 }
 
 }  // namespace nk
+
+namespace nk {
+// ---------------------------------------------------------------------------
+// Diagnostic: the count kernel's per-k-mer hash work alone (SipHash-1-3 +
+// exact % pool, nk_device.h), keys generated in registers, no memory traffic
+// but one store per thread.  nk_diag_hash_ms times it: the VALU floor of K1a.
+// ---------------------------------------------------------------------------
+constexpr int kDiagPer = 64;
+__global__ __launch_bounds__(256) void k_diag_hash(FastMod fm, uint64_t n_keys,
+                                                   uint32_t *__restrict__ out) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t key = (t * 0x9E3779B97F4A7C15ull) ^ 0x4E4B4D52ull;
+  uint32_t acc = 0;
+  const uint64_t first = t * kDiagPer;
+#pragma unroll 16
+  for (int i = 0; i < kDiagPer; ++i) {
+    if (first + (uint64_t)i < n_keys) acc ^= fastmod32(sip13_u64(key), fm);
+    key += 0xD1B54A32D192ED03ull;
+  }
+  out[t] = acc;
+}
+
+hipError_t launch_diag_hash(uint64_t n_keys, uint64_t pool, uint32_t *out, hipStream_t s) {
+  const uint64_t threads = (n_keys + kDiagPer - 1) / kDiagPer;
+  const uint64_t blocks = (threads + 255) / 256;
+  hipLaunchKernelGGL(k_diag_hash, dim3((uint32_t)blocks), dim3(256), 0, s, make_fastmod(pool),
+                     n_keys, out);
+  return hipGetLastError();
+}
+
+uint64_t diag_hash_out_words(uint64_t n_keys) {
+  return ((n_keys + kDiagPer - 1) / kDiagPer + 255) / 256 * 256;
+}
+}  // namespace nk
+
+#if defined(NK_ABL_STAMPS)
+extern "C" int nk_diag_stamps(unsigned long long *out, size_t n) {
+  if (n > (1u << 18)) n = 1u << 18;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(nk::g_stamps), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -106,15 +106,16 @@ def finalize_step(ctr, group=None, total_kmers=None, cap: int = 4096,
         # real torch stream so the collectives and our kernels share one order
         _on_side_stream(ctr, lambda: finalize_step(ctr, group, total_kmers, cap, streaming))
         return
+    stream = torch.cuda.current_stream().cuda_stream
     if getattr(ctr, "exact_counts", False):  # (after exchange_exact_table)
-        cur = _dev_view(ctr.device_currents_ptr(), ctr.pool_size, "<i8",
-                        torch.device("cuda", torch.cuda.current_device()))
+        cur = _currents_view(ctr, torch.device("cuda", torch.cuda.current_device()))
         allreduce_currents_(cur, group=group, total_kmers=total_kmers)
-        ctr.finalize(streaming)
+        # the LIF must run after the all-reduce on the SAME stream: the
+        # library's own stream would not wait for torch's collective
+        ctr.finalize(streaming, stream)
         return
     world = dist.get_world_size(group)
     dev = torch.device("cuda", torch.cuda.current_device())
-    stream = torch.cuda.current_stream().cuda_stream
     bufs = ctr.__dict__.setdefault("_dist_bufs", {})
     pool = ctr.pool_size
     wire_ptr = 0
@@ -127,7 +128,7 @@ def finalize_step(ctr, group=None, total_kmers=None, cap: int = 4096,
             dist.all_reduce(wire[:pool], op=dist.ReduceOp.SUM, group=group)
         wire_ptr = wire.data_ptr()
     else:
-        cur = _dev_view(ctr.device_currents_ptr(), pool, "<i8", dev)
+        cur = _currents_view(ctr, dev)
         allreduce_currents_(cur, group=group)
     wpk = 2 if getattr(ctr, "kmer_width", 64) == 128 else 1
     stride = 1 + wpk * cap
@@ -222,6 +223,17 @@ class _CAI:
     def __init__(self, ptr: int, n: int, typestr: str):
         self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr,
                                          "data": (ptr, False), "version": 3}
+
+
+def _currents_view(ctr, dev):
+    """The counter's device currents as an int64 tensor view.  A null pointer
+    with a non-empty pool means the library could not materialise them (fold or
+    sync error): raise with its error instead of all-reducing nothing."""
+    ptr = ctr.device_currents_ptr()
+    if not ptr and ctr.pool_size:
+        from ._lib import NeuroKmerError, last_error
+        raise NeuroKmerError(-7, "device currents unavailable: " + last_error())
+    return _dev_view(ptr, ctr.pool_size, "<i8", dev)
 
 
 def _dev_view(ptr: int, n: int, typestr: str, dev):

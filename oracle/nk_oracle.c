@@ -555,15 +555,42 @@ static int accumulate(nko_counter *c, const uint8_t *bases, const uint64_t *offs
   return 0;
 }
 
+/* Test-speed memo for the LIF loop (oracle only): a neuron that enters the
+ * 1000-step loop in the fresh state (v = +0.0, r = 0) ends in a state that
+ * depends on its count alone, so the reference loop runs ONCE per distinct
+ * count among fresh neurons and the result is reused for the others
+ * (pool = 16 M streaming / 256 M in-memory parity cases).  Neurons in any
+ * other state always run the loop. */
+#define LIF_MEMO_BITS 16
+typedef struct { uint64_t count; uint64_t spikes; float v; uint32_t r; int used; } lif_memo_t;
+static void lif_neuron(nko_counter *c, lif_memo_t *memo, size_t i, int skip_zero) {
+  uint32_t vb;
+  memcpy(&vb, &c->v[i], 4);
+  if (memo && vb == 0 && c->r[i] == 0) {
+    uint64_t cnt = c->currents[i];
+    lif_memo_t *m = &memo[(cnt * 0x9E3779B97F4A7C15ULL) >> (64 - LIF_MEMO_BITS)];
+    if (!(m->used && m->count == cnt)) {
+      float v = 0.0f; uint32_t r = 0; uint64_t sp = 0;
+      nko_lif(cnt, c->steps, c->thr, c->leak, c->refr, skip_zero, &v, &r, &sp);
+      m->count = cnt; m->spikes = sp; m->v = v; m->r = r; m->used = 1;
+    }
+    c->v[i] = m->v; c->r[i] = m->r; c->sc[i] += m->spikes;
+    return;
+  }
+  nko_lif(c->currents[i], c->steps, c->thr, c->leak, c->refr, skip_zero, &c->v[i], &c->r[i], &c->sc[i]);
+}
+
 int nko_process_parallel(nko_counter *c, const uint8_t *bases, const uint64_t *offsets,
                          size_t n_recs, int n_threads) {
   if (accumulate(c, bases, offsets, n_recs, n_threads)) return -1;
   /* Spike simulation, serial (:186-200) */
+  lif_memo_t *memo = (lif_memo_t *)calloc((size_t)1 << LIF_MEMO_BITS, sizeof(lif_memo_t));
   for (size_t i = 0; i < c->pool; ++i) {
     uint64_t before = c->sc[i];
-    nko_lif(c->currents[i], c->steps, c->thr, c->leak, c->refr, 1, &c->v[i], &c->r[i], &c->sc[i]);
+    lif_neuron(c, memo, i, 1);
     add_spikes(c, c->sc[i] - before);
   }
+  free(memo);
   return 0;
 }
 
@@ -574,11 +601,13 @@ int nko_process_streaming(nko_counter *c, const uint8_t *bases, const uint64_t *
    * steps == 0 returns before touching anything (:549-551). */
   if (c->steps == 0) return 0;
   uint64_t total = 0;
+  lif_memo_t *memo = (lif_memo_t *)calloc((size_t)1 << LIF_MEMO_BITS, sizeof(lif_memo_t));
   for (size_t i = 0; i < c->pool; ++i) {
     uint64_t before = c->sc[i];
-    nko_lif(c->currents[i], c->steps, c->thr, c->leak, c->refr, 0, &c->v[i], &c->r[i], &c->sc[i]);
+    lif_neuron(c, memo, i, 0);
     total += c->sc[i] - before;
   }
+  free(memo);
   add_spikes(c, total);
   return 0;
 }
@@ -646,6 +675,25 @@ static int top_cmp(const void *a, const void *b) {
 size_t nko_top_abundant(const nko_counter *c, size_t n, uint64_t *idx, uint64_t *spikes,
                         uint32_t *uniques) {
   size_t P = c->pool;
+  if (n <= 4096 && P > 8 * n) {
+    /* same order as the sort below, by selection: scan in index order and keep
+     * the best m rows sorted (sc desc, idx asc); a later index never beats an
+     * equal count, so only strictly larger counts enter (test speed at 256 M) */
+    size_t m = n, have = 0;
+    top_t *b = (top_t *)malloc((m ? m : 1) * sizeof(top_t));
+    for (size_t i = 0; i < P; ++i) {
+      uint64_t sc = c->sc[i];
+      if (have == m && (m == 0 || sc <= b[m - 1].sc)) continue;
+      size_t j = have < m ? have++ : m - 1;
+      while (j > 0 && b[j - 1].sc < sc) { b[j] = b[j - 1]; --j; }
+      b[j].idx = i; b[j].sc = sc;
+    }
+    for (size_t i = 0; i < have; ++i) {
+      idx[i] = b[i].idx; spikes[i] = b[i].sc; uniques[i] = c->kpn[b[i].idx];
+    }
+    free(b);
+    return have;
+  }
   top_t *t = (top_t *)malloc((P ? P : 1) * sizeof(top_t));
   for (size_t i = 0; i < P; ++i) { t[i].idx = i; t[i].sc = c->sc[i]; }
   qsort(t, P, sizeof(top_t), top_cmp); /* (sc desc, idx asc) == stable sort */

@@ -235,3 +235,78 @@ def test_two_ranks_finalize_step(width, cap, steps, wire, skew):
         assert out == exp
         assert cur == ref.currents().tolist()
         assert sc == ref.spike_counts().tolist()
+
+
+# ---- config 4 shape: k=31, pool 2M, byte-range shards that split records -----
+C4_K, C4_POOL = 31, 2_000_000
+
+
+def _config4_input():
+    """3 long records (2.4 Mbases), planted repeats: 2 ranks cut the middle
+    record, so one window range is counted across a k-1 base halo."""
+    from neurokmer_amd import synth
+    return synth.make_records(2_400_000, 3, seed=404, repeats_per_mb=300, motif_len=150,
+                              n_rate=0.001)
+
+
+def _rank_config4(rank, world, port, exact, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from neurokmer_amd import SpikingKmerCounter
+        from neurokmer_amd import dist as nkdist
+        bases, offs = _config4_input()
+        lo, hi, so = nkdist.shard_records(offs, world, C4_K)[rank]
+        b = bases[lo:hi]
+        d_b = torch.from_numpy(np.concatenate([b, np.zeros(16, np.uint8)])).cuda()
+        d_o = torch.from_numpy(so.astype(np.uint64).view(np.int64)).cuda()
+        torch.cuda.synchronize()
+        c = SpikingKmerCounter(C4_K, 1.0, 0.95, 2, 1.0, C4_POOL, True, exact_counts=exact)
+        c.accumulate_device(d_b.data_ptr(), d_o.data_ptr(), so.size - 1, b.size)
+        if exact:
+            nkdist.exchange_exact_table(c)
+        # no manual synchronisation: finalize_step orders the LIF after the
+        # all-reduce on the caller's stream (exact branch included)
+        nkdist.finalize_step(c, total_kmers=int(offs[-1]))
+        q.put((rank, (lo, hi, so.tolist()), c.currents().tolist(), c.spike_counts().tolist(),
+               c.top_abundant_neurons(20), c.energy.total_spikes(),
+               c.kmer_per_neuron().tolist() if exact else None))
+        c.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("exact", [False, True])
+def test_two_ranks_config4_split_records(exact):
+    import torch.multiprocessing as mp
+    from oracle import cbind
+    from neurokmer_amd import dist as nkdist
+    bases, offs = _config4_input()
+    shards = nkdist.shard_records(offs, 2, C4_K)
+    # the cut falls inside record 1: both shards hold part of it (+ halo)
+    assert shards[0][1] > shards[1][0] and len(shards[0][2]) == 3 and len(shards[1][2]) == 3
+    ref = cbind.OracleCounter(C4_K, 1.0, 0.95, 2, 1.0, C4_POOL, True)
+    ref.process_parallel_arrays(bases, offs, 3)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_config4, args=(r, 2, port, exact, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    cur = ref.currents().tolist()
+    sc = ref.spike_counts().tolist()
+    top = ref.top_abundant_neurons(20)
+    assert ref.total_spikes > 0
+    for _, _, c, s, t, tot, kpn in res:
+        assert c == cur
+        assert s == sc
+        assert t == top
+        assert tot == ref.total_spikes
+        if exact:
+            assert kpn == ref.kmer_per_neuron().tolist()

@@ -312,3 +312,23 @@ def test_width128_oracle_matches_golden():
     assert list(o.refractory()) == e["refractory"]
     assert o.total_spikes == e["total_spikes"]
     assert [list(t) for t in o.top_abundant_neurons(20)] == e["top20"]
+
+
+def test_oracle_fast_paths_equal_the_plain_loops():
+    """The oracle's test-speed shortcuts (top-N by selection instead of a full
+    sort; the LIF loop run once per distinct count of fresh neurons) give the
+    same rows / states as the plain forms: the sort path (n > 4096) and
+    per-neuron nko_lif on each neuron."""
+    bases, offs = synth.make_records(200_000, 4, seed=21, repeats_per_mb=20_000, motif_len=60)
+    for streaming in (False, True):
+        r = cbind.OracleCounter(19, 1.0, 0.95, 2, 1.0, 50_021, True)
+        (r.process_streaming_arrays if streaming else r.process_parallel_arrays)(bases, offs)
+        assert r.top_abundant_neurons(5000)[:20] == r.top_abundant_neurons(20)
+        assert r.top_abundant_neurons(4097)[:300] == r.top_abundant_neurons(300)
+        cur, sc, v, rr = r.currents(), r.spike_counts(), r.voltages(), r.refractory()
+        for i in range(0, 50_021, 37):
+            if cur[i] == 0 and not streaming:
+                continue
+            vv, r1, s1 = cbind.lif(int(cur[i]), 1000, 1.0, 0.95, 2, not streaming)
+            assert (s1, r1) == (int(sc[i]), int(rr[i]))
+            assert np.float32(vv).view(np.uint32) == v[i].view(np.uint32)

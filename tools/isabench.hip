@@ -66,6 +66,26 @@ __global__ __launch_bounds__(256) void kop(uint32_t *out, uint64_t *clk) {
     if (OP == 31) { CHAIN8("v_sub_u32_e32 %0, %0, %1") }
     if (OP == 32) { CHAIN8("v_lshlrev_b32_e64 %0, 13, %0") }
     if (OP == 33) { CHAIN8("v_xor_b32_e64 %0, %0, %1") }
+    if (OP == 34) {  // canonical min as compiled: v_cmp_lt_u64 -> SGPR pair, two v_cndmask
+#define CMIN(A, B) asm volatile("v_cmp_lt_u64_e64 s[40:41], %0, %1\n\tv_cndmask_b32_e64 %0, %1, %0, s[40:41]" : "+v"(A) : "v"(B) : "s40", "s41");
+      uint64_t p0 = ((uint64_t)a1 << 32) | a0, p1 = ((uint64_t)a3 << 32) | a2;
+      uint64_t q0 = ((uint64_t)b0 << 32) | c0;
+      asm volatile("v_cmp_lt_u64_e64 s[40:41], %0, %2\n\tv_cndmask_b32_e64 %1, %1, %3, s[40:41]" : "+v"(p0), "+v"(a4) : "v"(q0), "v"(b0) : "s40", "s41");
+      asm volatile("v_cmp_lt_u64_e64 s[42:43], %0, %2\n\tv_cndmask_b32_e64 %1, %1, %3, s[42:43]" : "+v"(p1), "+v"(a5) : "v"(q0), "v"(c0) : "s42", "s43");
+      asm volatile("v_cndmask_b32_e64 %0, %0, %1, s[40:41]\n\tv_cndmask_b32_e64 %2, %2, %1, s[42:43]" : "+v"(a6), "+v"(b0), "+v"(a7) :: "s40", "s41", "s42", "s43");
+      asm volatile("v_cndmask_b32_e64 %0, %0, %1, s[40:41]\n\tv_cndmask_b32_e64 %2, %2, %1, s[42:43]" : "+v"(a0), "+v"(c0), "+v"(a1) :: "s40", "s41", "s42", "s43");
+      a2 ^= (uint32_t)p0; a3 ^= (uint32_t)p1;
+    }
+    if (OP == 35) { CHAIN8("v_cndmask_b32_e64 %0, %0, %1, s[4:5]") }
+    if (OP == 36) {  // mix: 4 v_xor + 4 v_alignbit
+      asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a0) : "v"(b0)); asm volatile("v_alignbit_b32 %0, %0, %1, 13" : "+v"(a1) : "v"(b0));
+      asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a2) : "v"(b0)); asm volatile("v_alignbit_b32 %0, %0, %1, 13" : "+v"(a3) : "v"(b0));
+      asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a4) : "v"(b0)); asm volatile("v_alignbit_b32 %0, %0, %1, 13" : "+v"(a5) : "v"(b0));
+      asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a6) : "v"(b0)); asm volatile("v_alignbit_b32 %0, %0, %1, 13" : "+v"(a7) : "v"(b0));
+    }
+    if (OP == 37) { CHAIN8("v_lshlrev_b32_e32 %0, 2, %0") }
+    if (OP == 38) { CHAIN8("v_add_lshl_u32 %0, %0, %1, 2") }
+    if (OP == 39) { CHAIN8("v_mov_b32_e32 %0, %0") }
     if (OP == 24) {  // 64-bit add as a VOP2 carry pair through VCC
 #define ADC(L, H) asm volatile("v_add_co_u32_e32 %0, vcc, %0, %2\n\tv_addc_co_u32_e32 %1, vcc, %1, %3, vcc" : "+v"(L), "+v"(H) : "v"(b0), "v"(c0) : "vcc");
       ADC(a0, a1) ADC(a2, a3) ADC(a4, a5) ADC(a6, a7)
@@ -171,6 +191,12 @@ int main() {
   run("v_sub_u32_e32", kop<31>, out, clk);
   run("v_lshlrev_b32_e64", kop<32>, out, clk);
   run("v_xor_b32_e64", kop<33>, out, clk);
+  run("cmp_lt_u64 + cndmask (mix)", kop<34>, out, clk);
+  run("v_cndmask_b32_e64 s[4:5]", kop<35>, out, clk);
+  run("4 xor + 4 alignbit", kop<36>, out, clk);
+  run("v_lshlrev_b32_e32 by 2", kop<37>, out, clk);
+  run("v_add_lshl_u32", kop<38>, out, clk);
+  run("v_mov_b32 self", kop<39>, out, clk);
   run("v_lshl_add_u64", kop64<0>, out, clk);
   run("v_pk_mov_b32 swap", kop64<3>, out, clk);
   run("v_mov_b64_e32", kop64<4>, out, clk);
