@@ -2,47 +2,67 @@
 """bench.py — NeuroKmer k-mer -> spike hot path on MI355X.
 
 Metric (BASELINE.json): Mk-mers/s at k=31, pool=2M, total spikes bit-exact vs
-the CPU reference restatement.  Workload = config 2: 115,000,000 synthetic
-bases in 7 records per GPU (weak scaling), k=31, pool_size=2,000,000,
---canonical, in-memory semantics (process_parallel).  One step = reset the
-neuron pool, then one full pass of the hot path over the resident input:
-tile/record index -> K1 hash+count -> [N>1: RCCL all-reduce of the u64
-currents] -> closed-form LIF -> exact top-20 -> unique-k-mer pass for the
-top-20 rows [N>1: all-gather of the top k-mer keys].  Inputs are resident in
-HBM before the timed region.
+the CPU reference restatement.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+Workloads (--workload):
+  config2 (default, weak scaling): 115,000,000 synthetic bases in 7 records
+      per GPU, k=31, pool_size=2,000,000, --canonical, in-memory semantics
+      (process_parallel).  The metric's configuration (BASELINE.json configs[1]).
+  config4 (strong scaling): one fixed input of --total-bases bases in records
+      of 115e6/7 bases (default 8 x 115e6 bases), split over the ranks by
+      dist.shard_records (byte ranges, records cut with a k-1 halo), k=31,
+      pool 2M; currents all-reduced over RCCL (u32 wire while the total k-mers
+      stay below 2^31).
+
+One step = reset the neuron pool, then one full pass of the hot path over the
+resident input: tile/record index -> K1a hash + partition -> K1b bucket
+histograms -> [N>1: RCCL all-reduce of the currents] -> closed-form LIF ->
+exact top-20 -> unique-k-mer pass for the top-20 rows [N>1: all-gather of the
+top k-mer keys + merge] -> results in host memory.  Inputs are resident in HBM
+before the timed region; timed steps run with no event between kernels
+(stage_timing 2), K1a's duration comes from in-kernel s_memrealtime stamps.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload config2|config4]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+Without WORLD_SIZE in the environment, --gpus N > 1 starts N ranks itself
+(torch.distributed.run on 127.0.0.1) before anything touches the GPU.  With
+fewer visible devices than ranks the ranks share devices over gloo (a launch
+rehearsal, labelled as such in config.parallelism; not a throughput figure).
+
+Rank 0 at N=1 adds (config2):
+  cpu_baseline  oracle/nk_oracle.c process_parallel restatement on the WHOLE
+                115 Mbase input, parallel over the 7 records like rayon, and a
+                full bit-compare of its outputs with the timed GPU run;
+  end_to_end    file -> results (nk_process_file_parallel on a FASTA in the
+                page cache) and host records -> results (nk_process_parallel,
+                PCIe copy included): not `value`;
+  exact_counts  the step with the exact k-mer table on (the drop-in shim's
+                configuration, INTEGRATION.md).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402  (import before the HIP library: one shared runtime)
-import torch.distributed as dist  # noqa: E402
 
 METRIC = "Mk-mers/sec at k=31, pool=2M; total-spikes bit-exact vs CPU ref"
 K = 31
 POOL = 2_000_000
 BASES = 115_000_000
 RECS = 7
+REC_LEN4 = BASES // RECS  # config 4 record length
 HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md chip table)
-
-
-class _CAI:
-    """Wraps a raw device pointer for torch.as_tensor (no copy)."""
-
-    def __init__(self, ptr: int, n: int, typestr: str = "<i8"):
-        self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr,
-                                         "data": (ptr, False), "version": 3}
 
 
 def n_kmers(offsets: np.ndarray, k: int) -> int:
@@ -50,44 +70,74 @@ def n_kmers(offsets: np.ndarray, k: int) -> int:
     return int(np.clip(lens - k + 1, 0, None).sum())
 
 
-# VALU issue cycles per instruction of K1a's mix: the per-k-mer loop body's
-# 142 instructions cost 470 issue clocks at the measured gfx950 rates (VOP1/2
-# e32 2.45 clk, v_bitop3 2.37, VOP3 4.2; tools/isabench.hip)
-K1A_ISSUE_CLK_PER_INSTR = 3.31
-
-
 def load_pmc():
-    """The committed rocprofv3 PMC summary of K1 (profiles/pmc_count_kernel.json):
-    HBM bytes per launch, VALU instructions and busy cycles per launch."""
-    path = os.path.join(ROOT, "profiles", "pmc_count_kernel.json")
+    """The committed rocprofv3 PMC summary of K1a (profiles/pmc_count_kernel.json):
+    HBM bytes and VALU instructions per launch of the config-2 workload."""
     try:
-        with open(path) as f:
+        with open(os.path.join(ROOT, "profiles", "pmc_count_kernel.json")) as f:
             return json.load(f)
     except Exception:
         return {}
 
 
-def cpu_baseline(bases: np.ndarray, offsets: np.ndarray, per_record: int = 2_000_000,
-                 pool: int = POOL):
-    """The C restatement of process_parallel (oracle/nk_oracle.c, 'port') on a
-    bounded sample of the same workload: the first `per_record` bases of each
-    of the 7 records, parallel over records like rayon (src/spiking_hash.rs:
-    94-95; 7 threads), exact k-mer map, serial merge, serial 2M-neuron LIF
-    (:157-200).  About 10 s of CPU work."""
+def spawn_ranks(n: int) -> int:
+    """Start n ranks of this script (torch.distributed.run, 127.0.0.1) and
+    return their exit code.  Runs before any GPU call in this process."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def cpu_baseline(bases: np.ndarray, offsets: np.ndarray, k: int, pool: int):
+    """oracle/nk_oracle.c's restatement of process_parallel (src/spiking_hash.rs:
+    84-201) over the whole input: one thread per record like rayon's par_iter
+    over records (:94-95), exact k-mer map, serial merge, serial 1000-step LIF."""
     from oracle import cbind
-    per = int(min(per_record, np.diff(offsets.astype(np.int64)).min()))
-    segs = [bases[int(offsets[i]):int(offsets[i]) + per] for i in range(offsets.size - 1)]
-    offs = np.zeros(len(segs) + 1, np.uint64)
-    np.cumsum([x.size for x in segs], out=offs[1:])
-    b = np.concatenate(segs)
-    threads = offsets.size - 1  # one rayon work unit per record
-    ref = cbind.OracleCounter(K, 1.0, 0.95, 2, 1.0, pool, True)
+    threads = offsets.size - 1
+    ref = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, True)
     t0 = time.perf_counter()
-    ref.process_parallel_arrays(b, offs, threads)
+    ref.process_parallel_arrays(bases, offsets, threads)
     dt = time.perf_counter() - t0
-    nk = n_kmers(offs, K)
-    return {"rate": nk / dt / 1e6, "seconds": dt, "kmers": nk, "bases": int(offs[-1]),
-            "per_record": per, "threads": threads, "ref": ref, "sample": (b, offs)}
+    return ref, dt, threads
+
+
+def parity(gpu, ref) -> dict:
+    """Bit-compare every output of the GPU handle with the restatement."""
+    out = {
+        "currents": bool(np.array_equal(gpu.currents(), ref.currents())),
+        "spike_counts": bool(np.array_equal(gpu.spike_counts(), ref.spike_counts())),
+        "voltages_bitwise": bool(np.array_equal(gpu.voltages().view(np.uint32),
+                                                ref.voltages().view(np.uint32))),
+        "refractory": bool(np.array_equal(gpu.refractory(), ref.refractory())),
+        "total_spikes": [gpu.energy.total_spikes(), ref.total_spikes],
+        "energy_used": [gpu.energy_used(), ref.energy_used()],
+        "top20_with_uniques": gpu.top_abundant_neurons(20) == ref.top_abundant_neurons(20),
+    }
+    out["all_equal"] = bool(out["currents"] and out["spike_counts"] and out["voltages_bitwise"]
+                            and out["refractory"] and out["top20_with_uniques"]
+                            and out["total_spikes"][0] == out["total_spikes"][1]
+                            and out["energy_used"][0] == out["energy_used"][1])
+    return out
+
+
+def log(msg: str) -> None:
+    """Progress on stderr (a long run keeps its log growing)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def timed(fn, reps: int):
+    """(best, median) wall seconds of fn() over reps runs after one warm run."""
+    fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return min(ts), float(np.median(ts))
 
 
 def main() -> int:
@@ -95,52 +145,85 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--bases", type=int, default=BASES)
+    ap.add_argument("--workload", choices=("config2", "config4"), default="config2")
+    ap.add_argument("--bases", type=int, default=BASES, help="config2: bases per rank")
+    ap.add_argument("--total-bases", type=int, default=8 * BASES, help="config4: bases in all")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip end_to_end and the exact_counts step (rank 0, N=1)")
     ap.add_argument("--settle", type=float, default=0.25,
                     help="seconds of untimed steps after the warmup (GPU clock settle)")
-    # side measurements only (the metric is pool 2M): e.g. config 3's 16 M pool
+    # side measurements only (the metric is k=31, pool 2M)
     ap.add_argument("--pool", type=int, default=POOL)
     ap.add_argument("--k", type=int, default=K)
     ap.add_argument("--kmer-width", type=int, default=64, choices=(64, 128))
-    # test-only: rehearse the multi-rank path on a 1-GPU box (gloo, all ranks on cuda:0)
-    ap.add_argument("--dist-backend", default="nccl")
-    ap.add_argument("--same-device", action="store_true")
-    # rehearsal: run the multi-rank step (all-reduce, key all-gather, merge)
-    # in a 1-rank process group, to measure its overhead on a 1-GPU box
+    ap.add_argument("--dist-backend", default=None, help="default: nccl (RCCL), gloo if ranks share a GPU")
+    # rehearsal: the multi-rank step (wire all-reduce, key all-gather, merge) in
+    # a 1-rank process group, to measure its overhead on a 1-GPU box
     ap.add_argument("--force-dist", action="store_true")
     args = ap.parse_args()
-    pool = args.pool
-    k = args.k
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.same_device:
-        local = 0
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch with "
+              f"torchrun --nproc-per-node {args.gpus} (or no torchrun)", file=sys.stderr)
+        return 2
+
+    import torch
+    import torch.distributed as dist
+
+    pool, k = args.pool, args.k
+    ndev = torch.cuda.device_count()  # counts devices without initialising them
+    shared = world > ndev  # rehearsal: ranks share devices
+    dev_idx = local % max(ndev, 1)
+    backend = args.dist_backend or ("gloo" if shared else "nccl")
     dist_on = world > 1 or args.force_dist
     if dist_on:
-        torch.cuda.set_device(local)
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(dev_idx)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
         else:
-            dist.init_process_group(args.dist_backend)
-    dev = torch.device("cuda", local)
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", dev_idx)
 
     from neurokmer_amd import SpikingKmerCounter, synth
     from neurokmer_amd import dist as nkdist
+    from neurokmer_amd.counter import diag_hash_ms
 
-    # ---- this rank's shard of the synthetic input (resident in HBM) --------
-    bases, offsets = synth.make_records(args.bases, RECS, seed=synth.SEED ^ (rank * 0x9E37),
-                                        repeats_per_mb=64, motif_len=200)
-    nk = n_kmers(offsets, k)
+    # ---- this rank's input (resident in HBM) -------------------------------
+    if args.workload == "config2":
+        bases, offsets = synth.make_records(args.bases, RECS, seed=synth.SEED ^ (rank * 0x9E37),
+                                            repeats_per_mb=64, motif_len=200)
+        nk_rank = n_kmers(offsets, k)
+        total_kmers = world * nk_rank  # same size on every rank
+        scaling = "weak"
+        workload = (f"config 2: {bases.size:,} bases in {RECS} records per GPU, k={k}, "
+                    f"pool_size={pool:,}, --canonical, process_parallel")
+    else:
+        T = args.total_bases
+        n_rec = max(1, -(-T // REC_LEN4))
+        glob = np.minimum(np.arange(n_rec + 1, dtype=np.int64) * REC_LEN4, T).astype(np.uint64)
+        lo, hi, rel = nkdist.shard_records(glob, world, k)[rank]
+        bases = synth.random_bases(hi - lo, seed=synth.SEED, start=lo)
+        offsets = rel.astype(np.uint64)
+        nk_rank = n_kmers(offsets, k)
+        total_kmers = n_kmers(glob, k)
+        scaling = "strong"
+        workload = (f"config 4 (strong scaling): {T:,} bases in {n_rec} records of {REC_LEN4:,}, "
+                    f"split by shard_records over {world} rank(s), k={k}, pool_size={pool:,}, "
+                    f"--canonical")
+    n_recs = offsets.size - 1
+    log(f"rank {rank}/{world}: {bases.size:,} bases, {n_recs} records on cuda:{dev_idx}")
     d_bases = torch.from_numpy(bases).to(dev)
     d_offs = torch.from_numpy(offsets.view(np.int64)).to(dev)
     torch.cuda.synchronize()
 
-    ctr = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, True, device=local,
+    ctr = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, True, device=dev_idx,
                              kmer_width=args.kmer_width)
-
     # one non-default stream for the whole run: the library's kernels, its
     # events and the collectives all go on it (a NULL stream handle would mean
     # the library's own stream)
@@ -149,17 +232,17 @@ def main() -> int:
     s_handle = run_stream.cuda_stream
 
     def step():
-        s = s_handle
-        ctr.reset(s, blocking=False)
+        ctr.reset(s_handle, blocking=False)
         if not dist_on:
-            ctr.process_parallel_device(d_bases.data_ptr(), d_offs.data_ptr(), RECS, bases.size, s)
+            ctr.process_parallel_device(d_bases.data_ptr(), d_offs.data_ptr(), n_recs, bases.size,
+                                        s_handle)
             return
-        ctr.accumulate_device(d_bases.data_ptr(), d_offs.data_ptr(), RECS, bases.size, s)
-        # RCCL over xGMI: the currents as u32 (every rank's k-mers together stay
-        # below 2^31), then LIF + top-N + this shard's top k-mers into a
+        ctr.accumulate_device(d_bases.data_ptr(), d_offs.data_ptr(), n_recs, bases.size, s_handle)
+        # RCCL over xGMI: the currents as u32 while every rank's k-mers together
+        # stay below 2^31, then LIF + top-N + this shard's top k-mers into a
         # fixed-size all-gather segment, the union merged on the device: one
         # host synchronisation per step
-        nkdist.finalize_step(ctr, total_kmers=world * args.bases)
+        nkdist.finalize_step(ctr, total_kmers=total_kmers)
 
     per = float("inf")  # fastest warmup step (the first one allocates)
     for _ in range(max(args.warmup, 1 if args.settle > 0 else 0)):
@@ -168,9 +251,8 @@ def main() -> int:
         torch.cuda.synchronize()
         per = min(per, time.perf_counter() - t_w)
     # clock settle: the GPU reaches its sustained clock only after ~10-30 ms of
-    # load (5 timed steps straight after 2 warmup steps run ~15% slower), so
-    # untimed steps continue for about --settle seconds; every rank runs the
-    # same number (the steps contain collectives).  Reported as "settle_steps".
+    # load, so untimed steps continue for about --settle seconds; every rank
+    # runs the same number (the steps contain collectives)
     settle = 0
     if args.settle > 0:
         settle = min(int(args.settle / max(per, 1e-4)) + 1, 5000)
@@ -181,6 +263,9 @@ def main() -> int:
         for _ in range(settle):
             step()
         torch.cuda.synchronize()
+    # timed steps: no event between kernels (the count kernel's own duration
+    # comes from its in-kernel stamps, nk_count_spans)
+    ctr.set_stage_timing(2)
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
@@ -199,90 +284,162 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
-    # K1's hipEvent times of every timed step (a ring of event pairs in the
-    # library, read after the loop so no event query sits in the timed region)
-    count_ms = ctr.count_history(args.steps)
-    timings = ctr.last_timings()
+    log(f"timed {args.steps} steps: {dt / args.steps * 1e3:.4f} ms/step")
+    spans = ctr.count_spans(args.steps)  # K1a of every timed step (in-kernel stamps)
     total_spikes = ctr.energy.total_spikes()
-    top = ctr.top_abundant_neurons(20)
+    # cross-check: K1a between hipEvents in 5 extra (untimed) steps
+    ctr.set_stage_timing(0)
+    for _ in range(5):
+        step()
+    torch.cuda.synchronize()
+    ev_ms = [x for x in ctr.count_history(5) if x == x and x > 0]
+    stages = ctr.last_timings()
+    ctr.set_stage_timing(2)
 
     if rank == 0:
         ms_step = dt / args.steps * 1e3
-        value = world * nk / (dt / args.steps) / 1e6
-        # roofline of the dominant kernel (K1: hash + count), algorithmic bytes
-        # per launch = input bases read once + one 8-B counter update per k-mer
-        c_ms = [x for x in count_ms if x is not None and x == x and x > 0]
-        k1_ms = float(np.mean(c_ms)) if c_ms else timings.get("count", float("nan"))
-        alg_bytes = bases.size + 8 * nk
+        value = total_kmers / (dt / args.steps) / 1e6 if scaling == "strong" else \
+            world * nk_rank / (dt / args.steps) / 1e6
+        sp = [x for x in spans if x > 0]
+        k1_ms = float(np.mean(sp)) if sp else (float(np.mean(ev_ms)) if ev_ms else float("nan"))
+        # roofline of the dominant kernel (K1a), algorithmic bytes per launch =
+        # input bases read once + one 8-B counter update per k-mer
+        alg_bytes = bases.size + 8 * nk_rank
         achieved = alg_bytes / (k1_ms * 1e-3)
         pmc = load_pmc()
-        traffic, traffic_src = pmc.get("hbm_bytes_per_launch"), pmc.get("source")
-        valu = None
-        if pmc.get("valu_instr_per_launch") and pmc.get("sclk_ghz") and pmc.get("pmc_launch_ns"):
-            # K1a is VALU-issue bound: issue cycles its instructions need per SIMD
-            # (1024 SIMDs) vs the cycles the launch took (PMC GRBM_GUI_ACTIVE)
-            busy = pmc["sclk_ghz"] * pmc["pmc_launch_ns"]  # cycles per launch
-            need = pmc["valu_instr_per_launch"] / 1024.0 * K1A_ISSUE_CLK_PER_INSTR
-            valu = {"instr_per_launch": pmc["valu_instr_per_launch"],
-                    "issue_clk_per_instr": K1A_ISSUE_CLK_PER_INSTR,
-                    "busy_cycles_per_launch": round(busy),
-                    "issue_frac": round(need / busy, 4),
-                    "sclk_ghz_live": round(busy / (k1_ms * 1e6), 3),
-                    "source": traffic_src}
+        cfg2 = args.workload == "config2" and args.bases == BASES and k == K and pool == POOL
+        traffic = pmc.get("hbm_bytes_per_launch") if cfg2 else None
+        # the limiter, measured in this run: the same GPU's rate for the hash
+        # work alone (SipHash-1-3 + exact % pool of register-generated keys, no
+        # memory traffic: nk_diag_hash_ms) against K1a's k-mer rate
+        floor_ms = diag_hash_ms(nk_rank, pool, dev_idx, reps=5) if args.kmer_width == 64 else None
+        valu = {"kmers_per_launch": nk_rank,
+                "k1a_gkmers_per_s": round(nk_rank / (k1_ms * 1e-3) / 1e9, 2)}
+        if floor_ms:
+            valu.update({"hash_only_ms": round(floor_ms, 4),
+                         "hash_only_gkmers_per_s": round(nk_rank / (floor_ms * 1e-3) / 1e9, 2),
+                         "frac_of_hash_only": round(floor_ms / k1_ms, 4)})
+        if cfg2 and pmc.get("valu_instr_per_launch"):
+            valu["valu_instr_per_launch"] = pmc["valu_instr_per_launch"]
+            valu["pmc_source"] = pmc.get("source")
+        hbm_frac = achieved / HBM_PEAK
+        frac_h = valu.get("frac_of_hash_only", 0.0)
+        bound = "valu" if frac_h >= 0.6 and frac_h >= hbm_frac else ("hbm" if hbm_frac >= 0.6 else "latency")
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "Mk-mers/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "settle_steps": settle,
             "ms_per_step": round(ms_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
-            "data": "synthetic (splitmix64 i.i.d. ACGT, seed 0x4E4B4D52^rank, 64x200-bp planted "
-                    "repeats per MB)",
-            "config": {"workload": (f"config 2: {bases.size:,} bases in 7 records per GPU, k={k}, "
-                                    f"pool_size={pool:,}, --canonical, process_parallel"),
-                       "k": k, "kmer_width": args.kmer_width, "pool_size": pool, "bases_per_gpu": int(bases.size),
-                       "records_per_gpu": RECS, "kmers_per_gpu": nk,
-                       "parallelism": f"dp{world}"},
-            "roofline": {"bound": "hbm", "kernel": "k_part<canonical> (K1a)",
+            "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "u64",
+            "data": ("synthetic (splitmix64 i.i.d. ACGT, seed 0x4E4B4D52" +
+                     ("^rank, 64x200-bp planted repeats per MB)" if args.workload == "config2"
+                      else ", one global stream sharded by byte range)")),
+            "config": {"workload": workload, "k": k, "kmer_width": args.kmer_width,
+                       "pool_size": pool, "bases_rank0": int(bases.size), "records_rank0": n_recs,
+                       "kmers_rank0": nk_rank, "kmers_total": total_kmers,
+                       "parallelism": f"dp{world}" + (f" (rehearsal: {world} ranks on {ndev} GPU, "
+                                                      f"{backend})" if shared else "")},
+            "roofline": {"bound": bound, "kernel": "k_part<canonical> (K1a)",
                          "achieved": round(achieved / 1e9, 2), "peak": HBM_PEAK / 1e9,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
-                         "traffic": traffic, "traffic_source": traffic_src,
+                         "unit": "GB/s", "frac": round(hbm_frac, 4),
+                         "traffic": traffic, "traffic_source": pmc.get("source") if traffic else None,
                          "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(k1_ms, 4),
-                         "launches_timed": len(c_ms), "valu": valu},
-            "stage_ms": {k2: round(v, 4) for k2, v in timings.items()},
+                         "avg_launch_source": ("in-kernel s_memrealtime span over the timed steps"
+                                               if sp else "hipEvents"),
+                         "launches_timed": len(sp),
+                         "avg_launch_ms_events": round(float(np.mean(ev_ms)), 4) if ev_ms else None,
+                         "valu": valu},
+            "stage_ms_event_steps": {k2: round(v, 4) for k2, v in stages.items()},
             "step_ms_host": [round((b - a) * 1e3, 4) for a, b in zip([t0] + marks[:-1], marks)],
-            "k1_ms_steps": [round(x, 4) for x in count_ms],
+            "k1a_ms_steps": [round(x, 4) for x in spans],
             "total_spikes": total_spikes,
         }
-        if world == 1 and not args.no_cpu_baseline and k == K and args.kmer_width == 64:
-            cb = cpu_baseline(bases, offsets, pool=pool)
-            # parity on the same sample: GPU vs the restatement, bit-exact
-            sb, so = cb["sample"]
-            g = SpikingKmerCounter(K, 1.0, 0.95, 2, 1.0, pool, True, device=local)
-            g.process_parallel_arrays(sb, so)
-            ref = cb["ref"]
-            parity = {
-                "sample_bases": int(so[-1]),
-                "currents": bool(np.array_equal(g.currents(), ref.currents())),
-                "spike_counts": bool(np.array_equal(g.spike_counts(), ref.spike_counts())),
-                "voltages_bitwise": bool(np.array_equal(g.voltages().view(np.uint32),
-                                                        ref.voltages().view(np.uint32))),
-                "total_spikes": [g.energy.total_spikes(), ref.total_spikes],
-                "top20": g.top_abundant_neurons(20) == ref.top_abundant_neurons(20),
-            }
-            g.close()
-            out["cpu_baseline"] = {
-                "value": round(cb["rate"], 4), "unit": "Mk-mers/s", "cores": cb["threads"],
-                "kind": "port",
-                "sample": f"first {cb['per_record']} bases of each of the {RECS} records of "
-                          f"rank 0's workload ({cb['bases']} bases, {cb['kmers']} k-mers, "
-                          f"pool {pool:,}, k=31, canonical) in {cb['seconds']:.2f} s: oracle/nk_oracle.c "
-                          f"process_parallel restatement (parallel over records, exact k-mer "
-                          f"map, serial merge and 1000-step LIF)"}
-            out["parity_on_cpu_sample"] = parity
+        if world == 1 and args.workload == "config2" and args.kmer_width == 64:
+            out.update(extras(args, ctr, bases, offsets, nk_rank, d_bases, d_offs, s_handle,
+                              dev_idx, SpikingKmerCounter, synth))
         print(json.dumps(out), flush=True)
     ctr.close()
     if dist_on:
         dist.destroy_process_group()
     return 0
+
+
+def extras(args, ctr, bases, offsets, nk, d_bases, d_offs, s_handle, dev_idx, Counter, synth):
+    """Rank 0 at N=1: the full-size CPU baseline with a full bit-compare, the
+    end-to-end figures and the exact_counts step."""
+    import torch
+    out = {}
+    k, pool, n_recs = args.k, args.pool, offsets.size - 1
+    if not args.no_extras:
+        e2e = {}
+        # host records -> results (nk_process_parallel: PCIe copy of the input)
+        g = Counter(k, 1.0, 0.95, 2, 1.0, pool, True, device=dev_idx)
+
+        def host_run():
+            g.reset()
+            g.process_parallel_arrays(bases, offsets)
+        log("end_to_end: host records")
+        best, med = timed(host_run, 3)
+        e2e["host_records"] = {"entry": "nk_process_parallel", "s_best": round(best, 5),
+                               "s_median": round(med, 5),
+                               "mkmers_per_s": round(nk / best / 1e6, 1),
+                               "total_spikes": g.energy.total_spikes()}
+        # file in the page cache -> results (stream_sequences + process_parallel,
+        # src/main.rs:40-46; GPU FASTA ingest)
+        with tempfile.TemporaryDirectory(dir="/tmp") as td:
+            path = os.path.join(td, "config2.fa")
+            synth.write_fasta(path, bases, offsets)
+            fsize = os.path.getsize(path)
+
+            def file_run():
+                g.reset()
+                g.process_file_parallel(path)
+            log("end_to_end: FASTA file")
+            best, med = timed(file_run, 3)
+            e2e["fasta_file"] = {"entry": "nk_process_file_parallel", "file_bytes": fsize,
+                                 "s_best": round(best, 5), "s_median": round(med, 5),
+                                 "mkmers_per_s": round(nk / best / 1e6, 1),
+                                 "gb_per_s": round(fsize / best / 1e9, 2),
+                                 "total_spikes": g.energy.total_spikes(),
+                                 "same_results": g.top_abundant_neurons(20) == ctr.top_abundant_neurons(20)
+                                 and g.energy.total_spikes() == ctr.energy.total_spikes()}
+        g.close()
+        out["end_to_end"] = e2e
+        # the step with the exact k-mer table (counts / get_count / full
+        # kmer_per_neuron, src/spiking_hash.rs:157-172): the shim's configuration
+        x = Counter(k, 1.0, 0.95, 2, 1.0, pool, True, device=dev_idx, exact_counts=True)
+
+        def exact_step():
+            x.reset(s_handle, blocking=False)
+            x.process_parallel_device(d_bases.data_ptr(), d_offs.data_ptr(), n_recs, bases.size,
+                                      s_handle)
+        log("exact_counts step")
+        exact_step()
+        torch.cuda.synchronize()
+        best, med = timed(exact_step, 5)
+        out["exact_counts_step"] = {"ms_best": round(best * 1e3, 3), "ms_median": round(med * 1e3, 3),
+                                    "mkmers_per_s": round(nk / med / 1e6, 1),
+                                    "distinct_kmers": x.distinct_kmers(),
+                                    "same_results": x.top_abundant_neurons(20) == ctr.top_abundant_neurons(20)}
+        x.close()
+    if not args.no_cpu_baseline:
+        log("cpu_baseline: oracle process_parallel on the whole input")
+        ref, dt, threads = cpu_baseline(bases, offsets, k, pool)
+        log(f"cpu_baseline: {dt:.1f} s")
+        out["cpu_baseline"] = {
+            "value": round(nk / dt / 1e6, 4), "unit": "Mk-mers/s", "cores": threads,
+            "host_cpus": os.cpu_count(), "kind": "port", "seconds": round(dt, 3),
+            "sample": (f"the whole rank-0 config-2 input ({bases.size:,} bases, {nk:,} k-mers, "
+                       f"{n_recs} records, pool {pool:,}, k={k}, canonical): oracle/nk_oracle.c "
+                       f"process_parallel restatement, one thread per record like rayon over "
+                       f"records (src/spiking_hash.rs:94-95), exact k-mer map, serial merge and "
+                       f"1000-step LIF")}
+        # the timed GPU run's final state (the last step) vs the restatement
+        out["parity_full"] = parity(ctr, ref)
+        if "exact_counts_step" in out:  # counts.len() of the exact table vs the map
+            out["parity_full"]["distinct_kmers"] = [out["exact_counts_step"]["distinct_kmers"],
+                                                    ref.distinct_kmers()]
+        del ref
+    return out
 
 
 if __name__ == "__main__":

@@ -261,6 +261,13 @@ int nk_count_history(const nk_counter *c, float *ms, int cap);
  * for timed benchmark steps and 0 for a separate count-kernel measurement.
  * (No reference counterpart: measurement only.) */
 int nk_set_stage_timing(nk_counter *c, uint32_t level);
+/* Duration in ms of the partitioned count kernel (K1a) of each of the last
+ * min(cap, 256) accumulate/process calls that ran it, oldest first, from
+ * in-kernel s_memrealtime stamps (earliest workgroup start to latest
+ * workgroup end): no event sits in the stream, so it is also valid with
+ * stage_timing 2.  Synchronises the handle's stream.  -> count, or < 0.
+ * (No reference counterpart: measurement only.) */
+int nk_count_spans(nk_counter *c, float *ms, int cap);
 /* Diagnostic: the best of `reps` device times (ms) of a kernel that computes
  * SipHash-1-3 (key 0) of n_keys u64 keys generated in registers plus the exact
  * `% pool` (nk_device.h: sip13_u64 + fastmod32, the count kernel's per-k-mer

@@ -40,7 +40,7 @@ EXPORTS = (
     "nk_count_history", "nk_wire32", "nk_finalize_export", "nk_merge_export", "nk_finalize_redo",
     "nk_top_kmers_padded", "nk_merge_top_kmers_padded",
     "nk_exact_owner", "nk_exact_partition", "nk_exact_adopt", "nk_device_kmer_per_neuron",
-    "nk_set_stage_timing", "nk_diag_hash_ms",
+    "nk_set_stage_timing", "nk_diag_hash_ms", "nk_count_spans",
     "nk_last_error",
     "nk_version",
 )
@@ -129,6 +129,7 @@ def load(share_torch: bool = True):
         "nk_reset_async": (C.c_int, [vp, vp]),
         "nk_last_timings": (C.c_int, [vp, P(C.c_char_p), P(C.c_float), C.c_int]),
         "nk_count_history": (C.c_int, [vp, P(C.c_float), C.c_int]),
+        "nk_count_spans": (C.c_int, [vp, P(C.c_float), C.c_int]),
         "nk_set_stage_timing": (C.c_int, [vp, C.c_uint32]),
         "nk_diag_hash_ms": (C.c_int, [C.c_int, u64, u64, C.c_int, P(C.c_float)]),
         "nk_wire32": (C.c_int, [vp, vp, vp]),

@@ -274,6 +274,14 @@ class SpikingKmerCounter:
         m = self._L.nk_count_history(self._h, buf, n)
         return [float(buf[i]) for i in range(m)]
 
+    def count_spans(self, n: int) -> list:
+        """K1a (partitioned count kernel) duration in ms of each of the last
+        min(n, 256) calls that ran it, oldest first, from in-kernel
+        s_memrealtime stamps (no event in the stream; valid at stage_timing 2)."""
+        buf = (C.c_float * max(n, 1))()
+        m = _lib.check(self._L.nk_count_spans(self._h, buf, n))
+        return [float(buf[i]) for i in range(m)]
+
 
 def diag_hash_ms(n_keys: int, pool: int, device: int = 0, reps: int = 5) -> float:
     """Best device time (ms) of SipHash-1-3 + exact % pool over n_keys keys

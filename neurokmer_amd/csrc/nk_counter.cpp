@@ -202,6 +202,11 @@ struct nk_counter {
   static constexpr int kCountRing = 256;
   hipEvent_t cnt_ev[kCountRing][2] = {};
   uint64_t cnt_calls = 0;
+  // in-kernel [start, end] s_memrealtime words of the partitioned count kernel,
+  // one pair per launch in a ring (nk_count_spans): its duration with no event
+  // between kernels (stage_timing 2)
+  DevBuf<unsigned long long> span;
+  uint64_t span_calls = 0;
 };
 
 // ev[i] for the stage timings; the inner stage boundaries only in full mode
@@ -397,7 +402,7 @@ nk_counter *nk_new(size_t k, float threshold, float leak, uint32_t refractory, d
        !c->uniq.ensure(kMaxTopN) && !c->special.ensure(kMaxTopN) &&
        !c->top_keys_n.ensure(1) && !c->radix_h.ensure(256) && !c->set_mask_d.ensure(1) &&
        !c->set_need_d.ensure(1) && !c->post_flags.ensure(4) && !c->set_keys.ensure((o.kmer_width == NK_KMER_128 ? 3 : 1) << 20) &&
-       !c->n_hits.ensure(1) &&
+       !c->n_hits.ensure(1) && !c->span.ensure(2 * nk_counter::kCountRing) &&
        hipHostMalloc((void **)&c->res_h, nk_counter::kResFlagOff + 64,
                      hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
        hipHostGetDevicePointer((void **)&c->res_hd, c->res_h, 0) == hipSuccess;
@@ -426,6 +431,7 @@ void nk_free(nk_counter *c) {
   c->x_pres.release(); c->x_tmp.release(); c->x_n.release();
   c->d_keys.release(); c->d_meta.release(); c->d_vals.release(); c->touched.release();
   c->tile_rec.release(); c->hist.release(); c->tie_cnt.release(); c->uniq.release();
+  c->span.release();
   c->special.release(); c->stats.release(); c->lif_tbl.release(); c->topst.release();
   c->cand.release(); c->top_cur.release(); c->set_keys.release(); c->top_keys.release();
   c->top_keys_n.release(); c->radix_h.release(); c->set_mask_d.release();
@@ -680,8 +686,13 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
     c->ev[1] = c->cnt_ev[slot][0];
     c->ev[2] = c->cnt_ev[slot][1];
   }
+  unsigned long long *span = nullptr;
+  if (c->part_used) {
+    span = c->span.p + 2 * (c->span_calls++ % nk_counter::kCountRing);
+    cp.pa.span = span;
+  }
   HIPCHK(mark(c, 0, s));
-  HIPCHK(launch_prep(in, cp.tile, c->tile_rec.p, z, s));
+  HIPCHK(launch_prep(in, cp.tile, c->tile_rec.p, z, s, span));
   c->cur_fresh = false;
   HIPCHK(mark(c, 1, s));
   if (c->part_used) {
@@ -2066,6 +2077,23 @@ int nk_set_stage_timing(nk_counter *c, uint32_t level) {
   if (level > 2) return fail(NK_E_INVALID, "stage timing level must be 0, 1 or 2");
   c->opts.stage_timing = level;
   return NK_OK;
+}
+
+int nk_count_spans(nk_counter *c, float *ms, int cap) {
+  if (!c || (!ms && cap > 0) || cap < 0) return fail(NK_E_INVALID, "null argument");
+  (void)hipSetDevice(c->device);
+  const uint64_t have = std::min<uint64_t>(c->span_calls, nk_counter::kCountRing);
+  const int n = (int)std::min<uint64_t>(have, (uint64_t)cap);
+  if (!n) return 0;
+  std::vector<unsigned long long> h(2 * nk_counter::kCountRing);
+  if (c->last_s) HIPCHK(hipStreamSynchronize(c->last_s));
+  HIPCHK(hipMemcpy(h.data(), c->span.p, h.size() * 8, hipMemcpyDeviceToHost));
+  for (int i = 0; i < n; ++i) {
+    const uint64_t call = c->span_calls - (uint64_t)n + (uint64_t)i;
+    const unsigned long long *w = &h[2 * (call % nk_counter::kCountRing)];
+    ms[i] = w[1] > w[0] ? (float)((double)(w[1] - w[0]) * 1e-5) : -1.0f;  // 10 ns ticks
+  }
+  return n;
 }
 
 int nk_count_history(const nk_counter *c, float *ms, int cap) {

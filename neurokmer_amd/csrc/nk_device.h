@@ -113,16 +113,19 @@ __device__ __forceinline__ uint64_t fastmod(uint64_t h, FastMod fm) {
 // 2^31 and ONE branch-free correction min(r, r - P) is exact.  Only the low
 // word of q is needed (one mul_hi + two v_mad_u64_u32 + one mul_lo).  Model
 // and edge cases: tests/test_oracle.py::test_fastmod32_model.
-__device__ __forceinline__ uint32_t fastmod32(uint64_t h, FastMod fm) {
+// (p: the modulus, possibly a VGPR copy of fm.p)
+__device__ __forceinline__ uint32_t fastmod32_p(uint64_t h, FastMod fm, uint32_t p) {
   const uint32_t h0 = (uint32_t)h, h1 = (uint32_t)(h >> 32);
   const uint32_t m0 = (uint32_t)fm.magic, m1 = (uint32_t)(fm.magic >> 32);
-  const uint32_t p = (uint32_t)fm.p;
   const uint32_t ahi = __umulhi(h0, m0);
   uint64_t mid = (uint64_t)h1 * m0 + ahi;
   mid = (uint64_t)h0 * m1 + mid;
   const uint32_t qlo = h1 * m1 + (uint32_t)(mid >> 32);
   const uint32_t r = h0 - qlo * p;
   return min(r, r - p);
+}
+__device__ __forceinline__ uint32_t fastmod32(uint64_t h, FastMod fm) {
+  return fastmod32_p(h, fm, (uint32_t)fm.p);
 }
 
 // ---- LIF -------------------------------------------------------------------

@@ -117,6 +117,10 @@ struct PartArgs {
   uint32_t *overflow;             // [bucket] region overflowed (records counted directly)
   unsigned long long *currents;   // overflow target
   uint32_t bin_bits = kBinBits;   // bucket = neuron >> bin_bits (13..15 on the partitioned path)
+  // [2] or null: earliest workgroup start and latest workgroup end of the
+  // launch (s_memrealtime, 100 MHz), folded with atomicMin / atomicMax by one
+  // lane per workgroup: the kernel's duration without an event in the stream
+  unsigned long long *span = nullptr;
 };
 
 // Generic partition (nk_wide.hip): any key mode; narrow (u16 offsets into
@@ -212,8 +216,9 @@ hipError_t launch_set_compact128(const unsigned long long *set3, uint64_t cap, u
 hipError_t launch_set_merge128(const MergeSrc &m, uint64_t pool, const UniqArgs &u, hipStream_t s);
 hipError_t launch_set_word(uint64_t *w, uint64_t v, hipStream_t s);
 // tile -> first record index for the count kernels, fused with a zero list
+// span (optional): the count kernel's [start, end] words, set to [~0, 0]
 hipError_t launch_prep(const KmerInput &in, uint64_t tile_size, uint32_t *tile_rec,
-                       const ZeroList &z, hipStream_t s);
+                       const ZeroList &z, hipStream_t s, unsigned long long *span = nullptr);
 hipError_t launch_zero(const ZeroList &z, hipStream_t s);
 hipError_t launch_merge_prep(unsigned long long *set_keys, uint64_t *mask, uint64_t cap, int w128,
                              uint32_t *uniq, uint32_t *special, uint32_t m, uint32_t *trunc,

@@ -439,7 +439,22 @@ __device__ unsigned long long g_stamps[1 << 18];
 #else
 #define NK_STAMP(I) do {} while (0)
 #endif
-template <bool CANON, int MAXB>
+// A launch-uniform value moved into a VGPR: a VALU instruction that reads an
+// SGPR operand issues at half rate on gfx950 (tools/isabench.hip: v_xor with an
+// SGPR 4.15 clk vs 2.35 with a literal or VGPR), so the per-k-mer loop reads its
+// masks, shift and dummy bucket from VGPRs.
+__device__ __forceinline__ uint32_t in_vgpr(uint32_t x) {
+#if defined(NK_K1A_VUNI)
+  uint32_t v;
+  asm("v_mov_b32 %0, %1" : "=v"(v) : "s"(x));
+  return v;
+#else
+  return x;
+#endif
+}
+
+// K16: k >= 16, so the low word of the window mask is all ones
+template <bool CANON, int MAXB, bool K16 = false>
 __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMod fm, PartArgs pa) {
   using S = PartShape<MAXB>;
   constexpr int kSortSlots = S::kSortSlots;
@@ -459,6 +474,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
   const uint32_t B = pa.n_buckets;
   NK_STAMP(0);
   NK_STAMP(8);
+  if (pa.span && tid == 0) atomicMin(pa.span, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   for (uint32_t b = tid; b <= B; b += kPartBlock) s_cnt[b] = 0;
   stage_tile<kPartTile, kPartBlock, !CANON, !CANON>(L, in, tile, k);  // syncs (INV: pack_kmer only)
   NK_STAMP(2);
@@ -506,7 +522,8 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
     invz = (uint64_t)L.INV[iw] | ((uint64_t)L.INV[iw + 1] << 16) | ((uint64_t)L.INV[iw + 2] << 32);
   }
   const uint32_t kmask = (k >= 32) ? 0xFFFFFFFFu : ((1u << k) - 1u);
-  const uint32_t bbits = pa.bin_bits, bmask = (1u << bbits) - 1u;
+  const uint32_t bbits = in_vgpr(pa.bin_bits), bmask = in_vgpr((1u << pa.bin_bits) - 1u);
+  const uint32_t Bv = in_vgpr(B), pv = in_vgpr((uint32_t)fm.p);
   uint32_t E[kPartPerThread];  // bucket << 16 | rank
   uint32_t O[kPartPerThread];  // bin offset within the bucket
   // Window j as a funnel shift of two 96-bit words (no serial roll):
@@ -518,14 +535,16 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
   const uint32_t g0 = inF, g1 = (uint32_t)fwd, g2 = (uint32_t)(fwd >> 32);
   const unsigned __int128 X = ((unsigned __int128)inR << twok) | rev;
   const uint32_t x0 = (uint32_t)X, x1 = (uint32_t)(X >> 32), x2 = (uint32_t)(X >> 64);
-  const uint32_t mlo = (uint32_t)mask2k, mhi = (uint32_t)(mask2k >> 32);
+  const uint32_t mlo = in_vgpr((uint32_t)mask2k), mhi = in_vgpr((uint32_t)(mask2k >> 32));
 #pragma unroll
   for (int j = 0; j < kPartPerThread; ++j) {
     if (j) {
+      const uint32_t flo = __builtin_amdgcn_alignbit(g1, g0, 32 - 2 * j);
+      const uint32_t rlo = __builtin_amdgcn_alignbit(x1, x0, 2 * j);
       fwd = ((uint64_t)(__builtin_amdgcn_alignbit(g2, g1, 32 - 2 * j) & mhi) << 32) |
-            (__builtin_amdgcn_alignbit(g1, g0, 32 - 2 * j) & mlo);
+            (K16 ? flo : flo & mlo);
       rev = ((uint64_t)(__builtin_amdgcn_alignbit(x2, x1, 2 * j) & mhi) << 32) |
-            (__builtin_amdgcn_alignbit(x1, x0, 2 * j) & mlo);
+            (K16 ? rlo : rlo & mlo);
     }
     uint64_t key;
     if (CANON) {
@@ -545,9 +564,9 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
 #if defined(NK_ABL_NOHASH)  // ablation builds only (tools/ablate_k1a.sh): hash -> identity
     const uint32_t idx = fastmod32(key, fm);
 #else
-    const uint32_t idx = fastmod32(sip13_u64(key), fm);
+    const uint32_t idx = fastmod32_p(sip13_u64(key), fm, pv);
 #endif
-    const uint32_t b = ((ok >> j) & 1u) ? (idx >> bbits) : B;
+    const uint32_t b = ((ok >> j) & 1u) ? (idx >> bbits) : Bv;
 #if defined(NK_ABL_NORANK)  // ablation: no LDS rank atomic (records collide; timing only)
     const uint32_t rank = (uint32_t)j;
     if (tid == 0 && j == 0) atomicAdd(&s_cnt[b], 1u);
@@ -658,6 +677,10 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
         if ((w[i] & 0xFFFFu) != kPadOff)
           atomicAdd(&pa.currents[((uint64_t)b << pa.bin_bits) | (w[i] & 0xFFFFu)], 1ULL);
     }
+  }
+  if (pa.span) {  // this workgroup's last stores are issued: its end time
+    __syncthreads();
+    if (tid == 0) atomicMax(pa.span + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   }
 #if defined(NK_ABL_STAMPS)
   __syncthreads();
@@ -2078,6 +2101,10 @@ hipError_t launch_part(const KmerInput &in, int k, int canonical, uint64_t pool,
   const dim3 g((unsigned)in.n_tiles), bl(kPartBlock);
   if (pa.n_buckets > (uint32_t)kMaxBuckets) return hipErrorInvalidValue;
   if (pa.n_buckets <= 256) {
+#if defined(NK_K1A_K16)
+    if (canonical && k >= 16) hipLaunchKernelGGL((k_part<true, 256, true>), g, bl, 0, s, in, k, fm, pa);
+    else
+#endif
     if (canonical) hipLaunchKernelGGL((k_part<true, 256>), g, bl, 0, s, in, k, fm, pa);
     else hipLaunchKernelGGL((k_part<false, 256>), g, bl, 0, s, in, k, fm, pa);
   } else {
@@ -2167,7 +2194,8 @@ __global__ void k_zero(ZeroList z) {
 // tile -> first record (blocks [0, tr_blocks)) + the zero list (the rest)
 __global__ void k_prep(const uint64_t *__restrict__ offsets, uint64_t n_recs, uint64_t n_tiles,
                        uint64_t tile_size, uint64_t tile_base, uint32_t *__restrict__ tile_rec,
-                       unsigned tr_blocks, ZeroList z) {
+                       unsigned tr_blocks, ZeroList z, unsigned long long *span) {
+  if (span && blockIdx.x == 0 && threadIdx.x < 2) span[threadIdx.x] = threadIdx.x ? 0ull : ~0ull;
   if (blockIdx.x < tr_blocks) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n_tiles) return;
@@ -2194,7 +2222,7 @@ __global__ void k_prep(const uint64_t *__restrict__ offsets, uint64_t n_recs, ui
 }
 
 hipError_t launch_prep(const KmerInput &in, uint64_t tile_size, uint32_t *tile_rec,
-                       const ZeroList &z, hipStream_t s) {
+                       const ZeroList &z, hipStream_t s, unsigned long long *span) {
   uint64_t tot = 0;
   for (int b = 0; b < z.n; ++b) tot += z.bytes[b];
   const unsigned tr = (unsigned)((in.n_tiles + 255) / 256);
@@ -2202,7 +2230,7 @@ hipError_t launch_prep(const KmerInput &in, uint64_t tile_size, uint32_t *tile_r
   if (g > 1024) g = 1024;
   if (!g) g = 1;
   hipLaunchKernelGGL(k_prep, dim3(tr + g), dim3(256), 0, s, in.offsets, in.n_recs, in.n_tiles,
-                     tile_size, in.tile_base, tile_rec, tr, z);
+                     tile_size, in.tile_base, tile_rec, tr, z, span);
   return hipGetLastError();
 }
 

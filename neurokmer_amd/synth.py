@@ -40,16 +40,18 @@ def random_words(n_words: int, seed: int = SEED, start: int = 0) -> np.ndarray:
         return _mix(np.uint64(seed & 0xFFFFFFFFFFFFFFFF) + j * GAMMA)
 
 
-def random_bases(n: int, seed: int = SEED, chunk: int = 1 << 24) -> np.ndarray:
-    """n bases of the splitmix64 stream as ASCII ACGT (uint8)."""
+def random_bases(n: int, seed: int = SEED, chunk: int = 1 << 24, start: int = 0) -> np.ndarray:
+    """Bases start .. start+n-1 of the splitmix64 stream as ASCII ACGT (uint8):
+    any slice of a long stream (e.g. one rank's shard) without the rest."""
     out = np.empty(n, dtype=np.uint8)
     shifts = (np.arange(32, dtype=np.uint64) * np.uint64(2))
     for s in range(0, n, chunk):
         e = min(n, s + chunk)
-        w0, w1 = s >> 5, (e + 31) >> 5
+        gs, ge = start + s, start + e
+        w0, w1 = gs >> 5, (ge + 31) >> 5
         words = random_words(w1 - w0, seed, w0)
         codes = ((words[:, None] >> shifts[None, :]) & np.uint64(3)).astype(np.uint8).ravel()
-        off = s - (w0 << 5)
+        off = gs - (w0 << 5)
         out[s:e] = _ACGT[codes[off:off + (e - s)]]
     return out
 

@@ -15,8 +15,8 @@ for round in 1 2; do
       *) lib=tools/bin/ab/$tag/libneurokmer.so ;;
     esac
     log=gpurun_out/ab_$(echo "$tag" | tr ':=' '__')_$round.log
-    env NK_AB_LIB=$lib $envs timeout -k 10 90 python bench.py --steps 20 --warmup 2 --no-cpu-baseline \
+    env NK_AB_LIB=$lib $envs timeout -k 10 90 python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-extras \
       > "$log" 2>&1 || exit $?
-    python3 -c "import json,sys; d=json.loads(open('$log').read().strip().splitlines()[-1]); print('$tag', $round, d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'], d['stage_ms'])"
+    python3 -c "import json,sys; d=json.loads(open('$log').read().strip().splitlines()[-1]); print('$tag', $round, d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'], d['roofline']['avg_launch_ms_events'])"
   done
 done

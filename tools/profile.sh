@@ -10,9 +10,9 @@ OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-BENCH="python3 $ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline"
+BENCH="python3 $ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extras"
 # counters do not depend on the clock: no settle steps under --pmc
-BENCH_PMC="python3 $ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --settle 0"
+BENCH_PMC="python3 $ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extras --settle 0"
 case $MODE in
   list)
     timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1
