@@ -266,6 +266,11 @@ def main() -> int:
     # timed steps: no event between kernels (the count kernel's own duration
     # comes from its in-kernel stamps, nk_count_spans)
     ctr.set_stage_timing(2)
+    # one more untimed step in the timed mode: the first step after the switch
+    # measured ~0.18 ms slower on the host side (profiles/r02_s2/bench_default.log,
+    # step_ms_host[0]) while its K1a span was normal
+    step()
+    torch.cuda.synchronize()
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize()

@@ -58,13 +58,21 @@ typedef struct nk_opts {
                             of GPU idle time on MI355X);
                             2: events at both ends of a call only (no event
                             between two kernels; no count-kernel time) */
-  uint32_t exact_counts; /* 1: also build the exact k-mer count table on the
-                            device (the reference's `counts` DashMap and the full
-                            `kmer_per_neuron`, src/spiking_hash.rs:27,157-172):
-                            enables nk_get_count(s), nk_copy_kmer_per_neuron,
-                            nk_distinct_kmers and nk_process_sequence.
-                            NK_KMER_COMPAT only.  Default 0: the metric's path,
-                            uniques for the top rows only. */
+  uint32_t exact_counts; /* 1: build the exact k-mer count table on the device
+                            (the reference's `counts` DashMap and the full
+                            `kmer_per_neuron`, src/spiking_hash.rs:27,157-172)
+                            in every process/accumulate call.  Default 0: the
+                            metric's path (uniques of the top_n rows only); the
+                            table of the last input is then built on demand by
+                            nk_get_count(s)/nk_get_counts128, nk_distinct_kmers,
+                            nk_copy_kmer_per_neuron, nk_top_abundant_neurons
+                            past top_n rows and nk_process_sequence — provided
+                            the handle holds that input (host-array and file
+                            entry points; device input passed by pointer is the
+                            caller's: those calls then return NK_E_UNSUPPORTED
+                            unless exact_counts = 1).  The multi-GPU exact
+                            table (nk_exact_*) needs exact_counts = 1 and
+                            NK_KMER_COMPAT keys. */
   uint32_t reserved[11];
 } nk_opts;
 
@@ -167,9 +175,11 @@ int nk_merge_top_kmers_padded(nk_counter *c, const uint64_t *d_buf, size_t world
  * Writes min(n, pool_size) rows into out (caller-allocated), returns the count
  * written, or a negative error.  Rows are ordered by spikes descending, ties
  * by ascending neuron index (the reference's stable sort).  `uniques` is the
- * number of distinct k-mers of the last process call mapped to that neuron;
- * it is exact for rows < opts.top_n and NK_E_UNSUPPORTED is returned for
- * n > opts.top_n. */
+ * neuron's kmer_per_neuron: the distinct k-mers of the last process call
+ * mapped to it (+1 per process_sequence record touching it).  Any n: the
+ * opts.top_n rows come with every process call; more rows rank the whole pool
+ * on the device and take the uniques from the exact table (see exact_counts
+ * for when that table can be built on demand). */
 typedef struct nk_top_row {
   uint64_t idx;
   uint64_t spikes;
@@ -180,18 +190,26 @@ long nk_top_abundant_neurons(nk_counter *c, size_t n, nk_top_row *out);
 
 /* SpikingKmerCounter::get_count(&self, kmer) — src/spiking_hash.rs:675-682:
  * *present = 1 and *out = the k-mer's count (u32, wrapping like AtomicU32), or
- * *present = 0.  Needs nk_opts.exact_counts (else NK_E_UNSUPPORTED). */
+ * *present = 0.  The table: see nk_opts.exact_counts.  NK_KMER_COMPAT keys
+ * (NK_KMER_128 handles: nk_get_counts128). */
 int nk_get_count(nk_counter *c, uint64_t kmer, uint32_t *out, int *present);
 /* SpikingKmerCounter::process_sequence(&mut self, seq) — src/spiking_hash.rs:
  * 203-273: one record; counts[key] += 1 per k-mer, currents[H(key) % P] += 1
  * on top of the currents already held, kmer_per_neuron[idx] += 1 per neuron
  * the record touches, then ONE LifNeuron::update(current as f32) for every
- * neuron with current > 0 and currents = 0.  len < k: no-op.  Needs
- * nk_opts.exact_counts (the uniques column is kmer_per_neuron). */
+ * neuron with current > 0 and currents = 0.  len < k: no-op.  The uniques
+ * column is kmer_per_neuron, so the table of the previous process call is
+ * built first when it is still pending (see exact_counts).  NK_KMER_COMPAT
+ * keys (the reference's u64 map); NK_E_UNSUPPORTED for NK_KMER_128. */
 int nk_process_sequence(nk_counter *c, const uint8_t *seq, size_t len);
 /* Batched get_count over host arrays (out[i], present[i] per key). */
 int nk_get_counts(nk_counter *c, const uint64_t *kmers, size_t n, uint32_t *out,
                   uint8_t *present);
+/* NK_KMER_128 handles: get_count of n u128 keys given as (lo, hi) pairs
+ * (kmers2[2i], kmers2[2i+1]).  (No reference counterpart: the reference keys
+ * are u64; the table's counts wrap at 2^32 like the u64 table's.) */
+int nk_get_counts128(nk_counter *c, const uint64_t *kmers2, size_t n, uint32_t *out,
+                     uint8_t *present);
 /* Number of distinct k-mers in the table (the reference's counts.len()). */
 long nk_distinct_kmers(nk_counter *c);
 /* The full `kmer_per_neuron` (src/spiking_hash.rs:28,167-172,262-267): out[i]

@@ -33,6 +33,7 @@ EXPORTS = (
     "nk_opts_default", "nk_new", "nk_free", "nk_process_parallel", "nk_process_parallel_device",
     "nk_process_file_streaming", "nk_process_file_parallel", "nk_accumulate_device", "nk_finalize", "nk_top_kmers",
     "nk_merge_top_kmers", "nk_top_abundant_neurons", "nk_get_count", "nk_get_counts",
+    "nk_get_counts128",
     "nk_distinct_kmers", "nk_copy_kmer_per_neuron", "nk_process_sequence", "nk_total_spikes",
     "nk_energy_used", "nk_set_steps", "nk_get_steps", "nk_pool_size", "nk_k",
     "nk_use_canonical", "nk_copy_currents", "nk_copy_spike_counts", "nk_copy_voltages",
@@ -106,6 +107,7 @@ def load(share_torch: bool = True):
         "nk_top_abundant_neurons": (C.c_long, [vp, sz, P(NkTopRow)]),
         "nk_get_count": (C.c_int, [vp, u64, P(u32), P(C.c_int)]),
         "nk_get_counts": (C.c_int, [vp, vp, sz, vp, vp]),
+        "nk_get_counts128": (C.c_int, [vp, vp, sz, vp, vp]),
         "nk_distinct_kmers": (C.c_long, [vp]),
         "nk_copy_kmer_per_neuron": (C.c_int, [vp, vp, sz]),
         "nk_process_sequence": (C.c_int, [vp, vp, sz]),

@@ -198,14 +198,15 @@ class SpikingKmerCounter:
         return [(int(rows[i].idx), int(rows[i].spikes), int(rows[i].uniques)) for i in range(m)]
 
     def get_count(self, kmer: int) -> Optional[int]:
-        """src/spiking_hash.rs:675-682 (needs exact_counts=True)."""
+        """src/spiking_hash.rs:675-682.  The table is built with every process call
+        (exact_counts=True) or on demand from the last input the handle holds."""
         out = C.c_uint32()
         present = C.c_int()
         check(self._L.nk_get_count(self._h, kmer, C.byref(out), C.byref(present)))
         return int(out.value) if present.value else None
 
     def process_sequence(self, seq: bytes) -> None:
-        """src/spiking_hash.rs:203-273 (needs exact_counts=True)."""
+        """src/spiking_hash.rs:203-273 (u64 keys; the previous call's table first)."""
         buf = np.frombuffer(bytes(seq), dtype=np.uint8)
         check(self._L.nk_process_sequence(self._h, buf.ctypes.data if buf.size else None,
                                           buf.size))
@@ -219,15 +220,28 @@ class SpikingKmerCounter:
                                     out.ctypes.data, pres.ctypes.data))
         return out[:q.size], pres[:q.size].astype(bool)
 
+    def get_counts128(self, kmers) -> tuple:
+        """kmer_width=128 handles: get_count of u128 keys (python ints) -> (counts, present)."""
+        ks = [int(x) for x in kmers]
+        q = np.zeros(max(2 * len(ks), 2), np.uint64)
+        for i, x in enumerate(ks):
+            q[2 * i] = x & 0xFFFFFFFFFFFFFFFF
+            q[2 * i + 1] = x >> 64
+        out = np.zeros(max(len(ks), 1), np.uint32)
+        pres = np.zeros(max(len(ks), 1), np.uint8)
+        check(self._L.nk_get_counts128(self._h, q.ctypes.data if ks else None, len(ks),
+                                       out.ctypes.data, pres.ctypes.data))
+        return out[:len(ks)], pres[:len(ks)].astype(bool)
+
     def distinct_kmers(self) -> int:
-        """counts.len() (needs exact_counts=True)."""
+        """counts.len()."""
         n = int(self._L.nk_distinct_kmers(self._h))
         if n < 0:
             check(n)
         return n
 
     def kmer_per_neuron(self) -> np.ndarray:
-        """The full kmer_per_neuron map as a dense u32 array (needs exact_counts=True)."""
+        """The full kmer_per_neuron map as a dense u32 array."""
         return self._copy("nk_copy_kmer_per_neuron", np.uint32)
 
     def energy_used(self) -> float:

@@ -177,6 +177,17 @@ struct nk_counter {
   bool d_dirty = true;              // delta must be cleared before use
   bool kpn_valid = false;           // kpn holds kmer_per_neuron (else it is all zero)
   bool kpn_global = false;          // table adopted across ranks: nk_finalize's uniques from kpn
+  // without opts.exact_counts the table of the last process/accumulate input is
+  // built on demand (get_count, kmer_per_neuron, top rows past top_n,
+  // process_sequence) from that input, while it is still resident
+  bool x_lazy = false;              // the table is the last input's, not built yet
+  bool input_owned = false;         // last_in is the handle's own copy (host/file entry points)
+  // top_abundant_neurons(n) past the rows the last call selected
+  DevBuf<uint64_t> rk_keys;         // [2P]: keys | sorted keys
+  DevBuf<uint32_t> rk_idx;          // [2P]: indices | sorted indices
+  DevBuf<uint8_t> rk_tmp;
+  DevBuf<TopCand> rk_cand;          // the rows as TopCand (uniques gather)
+  DevBuf<uint32_t> rk_uniq;
   // top-N selection fused into the LIF kernel (TopFuse)
   DevBuf<uint64_t> bcand;
   DevBuf<uint32_t> bcnt;
@@ -257,6 +268,7 @@ static int zero_state_on(nk_counter *c, hipStream_t) {
   c->d_dirty = true;
   c->d_bound = 0;
   c->kpn_valid = false;
+  c->x_lazy = false;
   return NK_OK;
 }
 
@@ -338,10 +350,6 @@ nk_counter *nk_new(size_t k, float threshold, float leak, uint32_t refractory, d
   else nk_opts_default(&o);
   if (o.kmer_width != NK_KMER_COMPAT && o.kmer_width != NK_KMER_128) {
     fail(NK_E_INVALID, "kmer_width %d unknown", o.kmer_width);
-    return nullptr;
-  }
-  if (o.kmer_width == NK_KMER_128 && o.exact_counts) {
-    fail(NK_E_UNSUPPORTED, "exact_counts is implemented for NK_KMER_COMPAT keys only");
     return nullptr;
   }
   if (o.kmer_width == NK_KMER_128 && k > 64) {
@@ -432,6 +440,8 @@ void nk_free(nk_counter *c) {
   c->d_keys.release(); c->d_meta.release(); c->d_vals.release(); c->touched.release();
   c->tile_rec.release(); c->hist.release(); c->tie_cnt.release(); c->uniq.release();
   c->span.release();
+  c->rk_keys.release(); c->rk_idx.release(); c->rk_tmp.release(); c->rk_cand.release();
+  c->rk_uniq.release();
   c->special.release(); c->stats.release(); c->lif_tbl.release(); c->topst.release();
   c->cand.release(); c->top_cur.release(); c->set_keys.release(); c->top_keys.release();
   c->top_keys_n.release(); c->radix_h.release(); c->set_mask_d.release();
@@ -468,33 +478,72 @@ int nk_reset_async(nk_counter *c, void *stream) {
 // host synchronisation (the key count sizes the sort).
 static int build_exact(nk_counter *c, const KmerInput &in0, hipStream_t s) {
   int rc;
-  const int end_bit = c->k <= 32 ? (int)(2 * c->k) : 64;
+  // NK_KMER_128: u128 keys (two u64 words each) over their 2k significant bits
+  const int w = c->w128 ? 2 : 1;
+  const int end_bit = c->w128 ? (int)(2 * c->k) : (c->k <= 32 ? (int)(2 * c->k) : 64);
   KmerInput in = in0;
   in.n_tiles = n_tiles_for(in.n_bases, kTile);
   if ((rc = c->x_n.ensure(2)) || (rc = c->x_tile_rec.ensure(std::max<uint64_t>(in.n_tiles, 1))) ||
-      (rc = c->x_keys.ensure(std::max<uint64_t>(in.n_bases, 1))) || (rc = c->kpn.ensure(c->pool)))
+      (rc = c->x_keys.ensure(w * std::max<uint64_t>(in.n_bases, 1))) || (rc = c->kpn.ensure(c->pool)))
     return rc;
   in.tile_rec = c->x_tile_rec.p;
   HIPCHK(hipMemsetAsync(c->x_n.p, 0, 16, s));
   HIPCHK(launch_tile_rec(in, kTile, c->x_tile_rec.p, s));
-  HIPCHK(exact_keys(in, (int)c->k, c->canonical, c->x_keys.p, c->x_n.p, s));
+  if (c->w128)
+    HIPCHK(exact_keys128(in, (int)c->k, c->canonical, c->x_keys.p, c->x_n.p, s));
+  else
+    HIPCHK(exact_keys(in, (int)c->k, c->canonical, c->x_keys.p, c->x_n.p, s));
   unsigned long long n = 0;
   HIPCHK(hipMemcpyAsync(&n, c->x_n.p, 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   const uint64_t nn = std::max<uint64_t>(n, 1);
-  if ((rc = c->x_sorted.ensure(nn)) || (rc = c->x_uniq.ensure(nn)) || (rc = c->x_cnt.ensure(nn)) ||
-      (rc = c->x_tmp.ensure(exact_temp_bytes(nn, end_bit))))
+  if ((rc = c->x_sorted.ensure(w * nn)) || (rc = c->x_uniq.ensure(w * nn)) ||
+      (rc = c->x_cnt.ensure(nn)) ||
+      (rc = c->x_tmp.ensure(c->w128 ? exact_temp_bytes128(nn, end_bit) : exact_temp_bytes(nn, end_bit))))
     return rc;
-  HIPCHK(exact_sort_rle(c->x_keys.p, c->x_sorted.p, n, end_bit, c->x_uniq.p, c->x_cnt.p,
-                        c->x_n.p + 1, c->x_tmp.p, c->x_tmp.n, s));
   HIPCHK(hipMemsetAsync(c->kpn.p, 0, c->pool * 4, s));
-  HIPCHK(exact_kpn(c->x_uniq.p, c->x_n.p + 1, n, c->pool, c->kpn.p, s));
+  if (c->w128) {
+    HIPCHK(exact_sort_rle128(c->x_keys.p, c->x_sorted.p, n, end_bit, c->x_uniq.p, c->x_cnt.p,
+                             c->x_n.p + 1, c->x_tmp.p, c->x_tmp.n, s));
+    HIPCHK(exact_kpn128(c->x_uniq.p, c->x_n.p + 1, n, c->pool, c->kpn.p, s));
+  } else {
+    HIPCHK(exact_sort_rle(c->x_keys.p, c->x_sorted.p, n, end_bit, c->x_uniq.p, c->x_cnt.p,
+                          c->x_n.p + 1, c->x_tmp.p, c->x_tmp.n, s));
+    HIPCHK(exact_kpn(c->x_uniq.p, c->x_n.p + 1, n, c->pool, c->kpn.p, s));
+  }
+  c->x_lazy = false;
   c->exact_built = true;
   c->kpn_valid = true;
   c->kpn_global = false;
   c->d_dirty = true;  // counts.clear() (src/spiking_hash.rs:157,426)
   c->d_bound = 0;
   return NK_OK;
+}
+
+// A process/accumulate call replaces `counts` and `kmer_per_neuron` with its
+// input's (src/spiking_hash.rs:157-172,426-427,467-473): built now with
+// opts.exact_counts, else marked to be built from that input on demand.
+static int table_for_input(nk_counter *c, const KmerInput &in, hipStream_t s) {
+  if (c->opts.exact_counts) return build_exact(c, in, s);
+  c->exact_built = false;
+  c->kpn_valid = false;
+  c->kpn_global = false;
+  c->d_dirty = true;
+  c->d_bound = 0;
+  c->x_lazy = true;
+  return NK_OK;
+}
+
+// The table on demand (no opts.exact_counts): built from the last input, which
+// must still be resident.  Device input passed by pointer is the caller's and
+// may be gone: such a handle needs opts.exact_counts (eager build).
+static int ensure_table(nk_counter *c, hipStream_t s) {
+  if (!c->x_lazy) return NK_OK;
+  if (!c->input_owned)
+    return fail(NK_E_UNSUPPORTED,
+                "the last input was device memory of the caller (not kept by the handle): "
+                "set nk_opts.exact_counts = 1 for counts / kmer_per_neuron / rows past top_n");
+  return build_exact(c, c->last_in, s);
 }
 
 // How one count batch runs:
@@ -716,10 +765,11 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
     HIPCHK(mark(c, 2, s));
   }
   HIPCHK(mark(c, 3, s));
-  if (c->opts.exact_counts && (rc = build_exact(c, in, s))) return rc;
   c->last_in = in;
   c->have_input = true;
   c->top_valid = false;
+  c->input_owned = d_bases == c->in_bases.p;
+  if ((rc = table_for_input(c, in, s))) return rc;
   return NK_OK;
 }
 
@@ -1473,21 +1523,52 @@ int nk_finalize_redo(nk_counter *c, void *stream) {
   return NK_OK;
 }
 
+static int table_ready(nk_counter *c, hipStream_t *s);
+
+// Rows past the ones the last call selected: the whole pool ranked on the
+// device (stable radix sort, ties by index, src/spiking_hash.rs:661-673) and
+// the uniques column from kmer_per_neuron (built on demand from the last input
+// without opts.exact_counts).
+static long extended_top(nk_counter *c, size_t m, nk_top_row *out) {
+  hipStream_t s;
+  int rc = table_ready(c, &s);
+  if (rc) return rc;
+  const uint64_t P = c->pool;
+  if (P > 0xFFFFFFFFull) return fail(NK_E_UNSUPPORTED, "rows past top_n need pool_size < 2^32");
+  if ((rc = materialize(c, false, s))) return rc;
+  if ((rc = c->rk_keys.ensure(2 * P)) || (rc = c->rk_idx.ensure(2 * P)) ||
+      (rc = c->rk_tmp.ensure(rank_rows_temp_bytes(P))) || (rc = c->rk_cand.ensure(m)) ||
+      (rc = c->rk_uniq.ensure(m)))
+    return rc;
+  HIPCHK(rank_rows(c->sc.p, P, ~0ull, c->rk_keys.p, c->rk_keys.p + P, c->rk_idx.p, c->rk_idx.p + P,
+                   c->rk_tmp.p, c->rk_tmp.n, s));
+  std::vector<uint64_t> key(m);
+  std::vector<uint32_t> idx(m), uq(m, 0);
+  HIPCHK(hipMemcpyAsync(key.data(), c->rk_keys.p + P, m * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(idx.data(), c->rk_idx.p + P, m * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (c->kpn_valid) {
+    std::vector<TopCand> tc(m);
+    for (size_t i = 0; i < m; ++i) tc[i] = TopCand{idx[i], ~key[i]};
+    HIPCHK(hipMemcpyAsync(c->rk_cand.p, tc.data(), m * sizeof(TopCand), hipMemcpyHostToDevice, s));
+    HIPCHK(exact_top_uniques(c->rk_cand.p, (uint32_t)m, c->kpn.p, c->rk_uniq.p, s));
+    HIPCHK(hipMemcpyAsync(uq.data(), c->rk_uniq.p, m * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+  }
+  for (size_t i = 0; i < m; ++i) out[i] = nk_top_row{idx[i], ~key[i], uq[i], 0};
+  return (long)m;
+}
+
 long nk_top_abundant_neurons(nk_counter *c, size_t n, nk_top_row *out) {
   if (!c) return fail(NK_E_INVALID, "null counter");
   size_t m = std::min(n, c->pool);
   if (m && !out) return fail(NK_E_INVALID, "null output");
   if (!c->top_valid) {
     // fresh (or reset) neurons: all spike counts 0 -> indices in order, no k-mers
-    if (n > c->opts.top_n)
-      return fail(NK_E_UNSUPPORTED, "uniques tracked for top_n=%u rows only", c->opts.top_n);
     for (size_t i = 0; i < m; ++i) out[i] = nk_top_row{i, 0, 0, 0};
     return (long)m;
   }
-  if (n > c->opts.top_n && n > c->top.size())
-    return fail(NK_E_UNSUPPORTED, "uniques tracked for top_n=%u rows only (opts.top_n)",
-                c->opts.top_n);
-  m = std::min(m, c->top.size());
+  if (m > c->top.size()) return extended_top(c, m, out);
   for (size_t i = 0; i < m; ++i) out[i] = c->top[i];
   return (long)m;
 }
@@ -1632,7 +1713,8 @@ static int acc_end(nk_counter *c, StreamAcc &sa, const KmerInput &whole, hipStre
   c->last_in.n_tiles = n_tiles_for(whole.n_bases, sa.cp.tile);
   c->have_input = true;
   c->top_valid = false;
-  if (c->opts.exact_counts && (rc = build_exact(c, whole, s))) return rc;
+  c->input_owned = whole.bases == c->in_bases.p;
+  if ((rc = table_for_input(c, whole, s))) return rc;
   return NK_OK;
 }
 
@@ -1796,14 +1878,18 @@ static int ingest_file(nk_counter *c, const char *path, bool *fallback) {
 
 // SpikingKmerCounter::process_sequence (src/spiking_hash.rs:203-273)
 int nk_process_sequence(nk_counter *c, const uint8_t *seq, size_t len) {
-  int rc = need_exact(c);
-  if (rc) return rc;
+  if (!c) return fail(NK_E_INVALID, "null counter");
+  if (c->w128)
+    return fail(NK_E_UNSUPPORTED, "process_sequence takes the reference's u64 keys (NK_KMER_COMPAT)");
   if (len && !seq) return fail(NK_E_INVALID, "null sequence");
   if (len < c->k) return NK_OK;  // :205-207: no k-mers, no LIF step
   if (c->pool == 0)
     return fail(NK_E_INVALID, "pool_size 0 with k-mers present (the reference panics on % 0)");
-  (void)hipSetDevice(c->device);
-  hipStream_t s = pick_stream(c, nullptr);
+  hipStream_t s;
+  // counts / kmer_per_neuron of the last process call first (its input is
+  // about to be replaced by this sequence in the handle's input buffer)
+  int rc = table_ready(c, &s);
+  if (rc) return rc;
   if (c->cur_in_wire)
     return fail(NK_E_INVALID, "the currents are in the wire vector until nk_finalize_export");
   if ((rc = materialize(c, true, s)) || (rc = fold_pending(c, s))) return rc;
@@ -1854,10 +1940,20 @@ int nk_process_sequence(nk_counter *c, const uint8_t *seq, size_t len) {
   return NK_OK;
 }
 
+// the table for a query: built now from the last input when it is lazy
+static int table_ready(nk_counter *c, hipStream_t *s) {
+  if (!c) return fail(NK_E_INVALID, "null counter");
+  (void)hipSetDevice(c->device);
+  *s = pick_stream(c, nullptr);
+  return ensure_table(c, *s);
+}
+
 int nk_get_counts(nk_counter *c, const uint64_t *kmers, size_t n, uint32_t *out,
                   uint8_t *present) {
-  int rc = need_exact(c);
+  hipStream_t s;
+  int rc = table_ready(c, &s);
   if (rc) return rc;
+  if (c->w128) return fail(NK_E_INVALID, "128-bit keys: use nk_get_counts128");
   if (n && (!kmers || !out || !present)) return fail(NK_E_INVALID, "null argument");
   if (!n) return NK_OK;
   if (!c->exact_built && c->d_dirty) {  // empty table (fresh or reset counter)
@@ -1865,8 +1961,6 @@ int nk_get_counts(nk_counter *c, const uint64_t *kmers, size_t n, uint32_t *out,
     memset(present, 0, n);
     return NK_OK;
   }
-  (void)hipSetDevice(c->device);
-  hipStream_t s = pick_stream(c, nullptr);
   if ((rc = c->x_q.ensure(n)) || (rc = c->x_out.ensure(n)) || (rc = c->x_pres.ensure(n)))
     return rc;
   HIPCHK(hipMemcpyAsync(c->x_q.p, kmers, n * 8, hipMemcpyHostToDevice, s));
@@ -1889,11 +1983,37 @@ int nk_get_count(nk_counter *c, uint64_t kmer, uint32_t *out, int *present) {
   return rc;
 }
 
-long nk_distinct_kmers(nk_counter *c) {
-  int rc = need_exact(c);
+int nk_get_counts128(nk_counter *c, const uint64_t *kmers2, size_t n, uint32_t *out,
+                     uint8_t *present) {
+  hipStream_t s;
+  int rc = table_ready(c, &s);
   if (rc) return rc;
-  (void)hipSetDevice(c->device);
-  HIPCHK(hipStreamSynchronize(pick_stream(c, nullptr)));
+  if (!c->w128) return fail(NK_E_INVALID, "64-bit keys: use nk_get_counts");
+  if (n && (!kmers2 || !out || !present)) return fail(NK_E_INVALID, "null argument");
+  if (!n) return NK_OK;
+  if (!c->exact_built) {  // empty table (fresh or reset counter)
+    memset(out, 0, n * 4);
+    memset(present, 0, n);
+    return NK_OK;
+  }
+  if ((rc = c->x_q.ensure(2 * n)) || (rc = c->x_out.ensure(n)) || (rc = c->x_pres.ensure(n)))
+    return rc;
+  HIPCHK(hipMemcpyAsync(c->x_q.p, kmers2, n * 16, hipMemcpyHostToDevice, s));
+  HIPCHK(exact_lookup128(c->x_uniq.p, c->x_cnt.p, c->x_n.p + 1, c->x_q.p, n, c->x_out.p,
+                         c->x_pres.p, s));
+  std::vector<uint32_t> pres(n);
+  HIPCHK(hipMemcpyAsync(out, c->x_out.p, n * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(pres.data(), c->x_pres.p, n * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  for (size_t i = 0; i < n; ++i) present[i] = pres[i] ? 1 : 0;
+  return NK_OK;
+}
+
+long nk_distinct_kmers(nk_counter *c) {
+  hipStream_t s;
+  int rc = table_ready(c, &s);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(s));
   unsigned long long n = 0, m[2] = {0, 0};
   if (c->exact_built) HIPCHK(hipMemcpy(&n, c->x_n.p + 1, 8, hipMemcpyDeviceToHost));
   if (!c->d_dirty) HIPCHK(hipMemcpy(m, c->d_meta.p, 16, hipMemcpyDeviceToHost));
@@ -1908,6 +2028,7 @@ int nk_exact_partition(nk_counter *c, uint32_t world, uint64_t *send_counts,
                        const uint64_t **d_keys, const uint32_t **d_counts, void *stream) {
   int rc = need_exact(c);
   if (rc) return rc;
+  if (c->w128) return fail(NK_E_UNSUPPORTED, "the multi-GPU exact table takes NK_KMER_COMPAT keys");
   if (!world || world > 4096) return fail(NK_E_INVALID, "world must be in 1..4096");
   if (!send_counts || !d_keys || !d_counts) return fail(NK_E_INVALID, "null argument");
   if (!c->exact_built) return fail(NK_E_INVALID, "no exact table: run a process/accumulate call first");
@@ -1948,6 +2069,7 @@ int nk_exact_adopt(nk_counter *c, const uint64_t *d_keys, const uint32_t *d_coun
                    void *stream) {
   int rc = need_exact(c);
   if (rc) return rc;
+  if (c->w128) return fail(NK_E_UNSUPPORTED, "the multi-GPU exact table takes NK_KMER_COMPAT keys");
   if (n && (!d_keys || !d_counts)) return fail(NK_E_INVALID, "null argument");
   (void)hipSetDevice(c->device);
   hipStream_t s = pick_stream(c, stream);
@@ -1973,7 +2095,9 @@ int nk_exact_adopt(nk_counter *c, const uint64_t *d_keys, const uint32_t *d_coun
 }
 
 uint32_t *nk_device_kmer_per_neuron(nk_counter *c) {
-  if (!c || !c->opts.exact_counts || !c->pool) return nullptr;
+  if (!c || !c->pool) return nullptr;
+  hipStream_t s;
+  if (table_ready(c, &s)) return nullptr;
   if (!c->kpn_valid) {
     (void)hipSetDevice(c->device);
     if (c->kpn.ensure(c->pool) || hipMemset(c->kpn.p, 0, c->pool * 4) != hipSuccess) return nullptr;
@@ -1983,7 +2107,8 @@ uint32_t *nk_device_kmer_per_neuron(nk_counter *c) {
 }
 
 int nk_copy_kmer_per_neuron(nk_counter *c, uint32_t *out, size_t n) {
-  int rc = need_exact(c);
+  hipStream_t s;
+  int rc = table_ready(c, &s);
   if (rc) return rc;
   if (n != c->pool) return fail(NK_E_INVALID, "n (%zu) must equal pool_size (%zu)", n, c->pool);
   if (!n) return NK_OK;

@@ -98,4 +98,33 @@ hipError_t exact_merge_pairs(const uint64_t *keys, const uint32_t *cnt, size_t n
 hipError_t exact_top_uniques(const TopCand *cand, uint32_t m, const uint32_t *kpn, uint32_t *uniq,
                              hipStream_t s);
 
+// ---- NK_KMER_128 table (k <= 64; no reference counterpart: the build's true
+// k <= 64 mode) -------------------------------------------------
+// keys are u128 (lo | hi << 64), 16-byte aligned arrays of 2 u64 words each;
+// the same steps as above: extraction, rocPRIM radix sort over 2k bits, RLE,
+// kpn[SipHash-1-3(16 LE bytes) % P] += 1 per distinct key, binary-search lookup
+hipError_t exact_keys128(const KmerInput &in, int k, int canonical, uint64_t *keys2,
+                         unsigned long long *n_keys, hipStream_t s);
+size_t exact_temp_bytes128(size_t n, int end_bit);
+hipError_t exact_sort_rle128(uint64_t *keys2, uint64_t *sorted2, size_t n, int end_bit,
+                             uint64_t *uniq2, uint32_t *cnt, unsigned long long *n_uniq, void *tmp,
+                             size_t tmp_bytes, hipStream_t s);
+hipError_t exact_kpn128(const uint64_t *uniq2, const unsigned long long *n_uniq, size_t max_n,
+                        uint64_t pool, uint32_t *kpn, hipStream_t s);
+// q2: nq (lo, hi) pairs
+hipError_t exact_lookup128(const uint64_t *uniq2, const uint32_t *cnt,
+                           const unsigned long long *n_uniq, const uint64_t *q2, size_t nq,
+                           uint32_t *out, uint32_t *present, hipStream_t s);
+
+// ---- top_abundant_neurons(n) for any n (src/spiking_hash.rs:661-673) --------
+// The reference's stable sort of (idx, spike_count) by spikes descending over
+// the whole pool: a stable rocPRIM radix sort of (max_sc - sc[i], i) pairs, i
+// ascending on entry, so ties keep index order.  rows_idx/rows_key receive the
+// first `m` rows (key = max_sc - spikes).  Returns the scratch size when tmp is
+// null (as rocPRIM does).
+size_t rank_rows_temp_bytes(size_t pool);
+hipError_t rank_rows(const uint64_t *sc, uint64_t pool, uint64_t max_sc, uint64_t *keys,
+                     uint64_t *keys_sorted, uint32_t *idx, uint32_t *idx_sorted, void *tmp,
+                     size_t tmp_bytes, hipStream_t s);
+
 }  // namespace nk

@@ -103,6 +103,79 @@ __global__ __launch_bounds__(kXBlock) void k_keys_compat(KmerInput in, int k,
     if ((ok >> j) & 1u) keys[at++] = kv[j];
 }
 
+// NK_KMER_128 (k <= 64): the 128-bit keys of the staged tile, exactly as the
+// 128-bit count kernels derive them (nk_tile.h window_key128)
+using u128 = unsigned __int128;
+template <bool CANON>
+__global__ __launch_bounds__(kXBlock) void k_keys_tile128(KmerInput in, int k,
+                                                          u128 *__restrict__ keys,
+                                                          unsigned long long *__restrict__ n_keys) {
+  __shared__ TileLds<kXTile, !CANON> L;
+  __shared__ uint32_t s_w[kXBlock / 64];
+  __shared__ unsigned long long s_base;
+  const uint64_t tile = in.tile_base + blockIdx.x;
+  const uint64_t T0 = tile * kXTile;
+  stage_tile<kXTile, kXBlock, !CANON>(L, in, tile, k);
+  uint32_t ok = 0;
+#pragma unroll
+  for (int j = 0; j < kXPer; ++j) {
+    const int q = j * kXBlock + threadIdx.x;
+    if (T0 + (uint64_t)q + (uint64_t)k > in.n_bases) continue;
+    if (window_valid(L, T0, q, k, in.n_bases, in.pos_lo, in.pos_hi)) ok |= 1u << j;
+  }
+  uint32_t total;
+  const uint32_t pre = scan256((uint32_t)__popc(ok), s_w, &total);
+  if (threadIdx.x == 0) s_base = total ? atomicAdd(n_keys, (unsigned long long)total) : 0ull;
+  __syncthreads();
+  uint64_t at = s_base + pre;
+  for (int j = 0; j < kXPer; ++j) {
+    if (!((ok >> j) & 1u)) continue;
+    const Key128 key = window_key128<kXTile, !CANON, CANON>(L, j * kXBlock + threadIdx.x, k);
+    keys[at++] = ((u128)key.hi << 64) | key.lo;
+  }
+}
+
+__global__ void k_kpn128(const u128 *__restrict__ uniq, const unsigned long long *__restrict__ n_uniq,
+                         FastMod fm, uint32_t *__restrict__ kpn) {
+  const uint64_t n = *n_uniq;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const u128 x = uniq[i];
+    atomicAdd(&kpn[fastmod(sip13_u128((uint64_t)x, (uint64_t)(x >> 64)), fm)], 1u);
+  }
+}
+
+__global__ void k_lookup128(const u128 *__restrict__ uniq, const uint32_t *__restrict__ cnt,
+                            const unsigned long long *__restrict__ n_uniq,
+                            const uint64_t *__restrict__ q2, uint64_t nq, uint32_t *__restrict__ out,
+                            uint32_t *__restrict__ present) {
+  const uint64_t n = n_uniq ? *n_uniq : 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nq;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const u128 key = ((u128)q2[2 * i + 1] << 64) | q2[2 * i];
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (uniq[mid] < key) lo = mid + 1;
+      else hi = mid;
+    }
+    const bool hit = lo < n && uniq[lo] == key;
+    out[i] = hit ? cnt[lo] : 0u;
+    present[i] = hit ? 1u : 0u;
+  }
+}
+
+// (max_sc - sc[i], i): ascending keys = spikes descending; i ascending on
+// entry, so the stable radix sort keeps ties in index order
+__global__ void k_rank_keys(const uint64_t *__restrict__ sc, uint64_t pool, uint64_t max_sc,
+                            uint64_t *__restrict__ keys, uint32_t *__restrict__ idx) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < pool;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    keys[i] = max_sc - sc[i];
+    idx[i] = (uint32_t)i;
+  }
+}
+
 __global__ void k_kpn(const uint64_t *__restrict__ uniq, const unsigned long long *__restrict__ n_uniq,
                       FastMod fm, uint32_t *__restrict__ kpn) {
   const uint64_t n = *n_uniq;
@@ -516,6 +589,84 @@ hipError_t exact_top_uniques(const TopCand *cand, uint32_t m, const uint32_t *kp
   if (!m) return hipSuccess;
   hipLaunchKernelGGL(k_top_uniques, dim3((m + 255) / 256), dim3(256), 0, s, cand, m, kpn, uniq);
   return hipGetLastError();
+}
+
+// ---- NK_KMER_128 table ---------------------------------------------------------
+hipError_t exact_keys128(const KmerInput &in, int k, int canonical, uint64_t *keys2,
+                         unsigned long long *n_keys, hipStream_t s) {
+  if (!in.n_tiles) return hipSuccess;
+  if (k > 64) return hipErrorInvalidValue;
+  u128 *keys = reinterpret_cast<u128 *>(keys2);
+  const dim3 g((unsigned)in.n_tiles), b(kXBlock);
+  if (canonical) hipLaunchKernelGGL(k_keys_tile128<true>, g, b, 0, s, in, k, keys, n_keys);
+  else hipLaunchKernelGGL(k_keys_tile128<false>, g, b, 0, s, in, k, keys, n_keys);
+  return hipGetLastError();
+}
+
+size_t exact_temp_bytes128(size_t n, int end_bit) {
+  size_t a = 0, b = 0;
+  (void)rocprim::radix_sort_keys(nullptr, a, (const u128 *)nullptr, (u128 *)nullptr, n, 0, end_bit);
+  (void)rocprim::run_length_encode(nullptr, b, (const u128 *)nullptr, n, (u128 *)nullptr,
+                                   (uint32_t *)nullptr, (unsigned long long *)nullptr);
+  return (a > b ? a : b) + 256;
+}
+
+hipError_t exact_sort_rle128(uint64_t *keys2, uint64_t *sorted2, size_t n, int end_bit,
+                             uint64_t *uniq2, uint32_t *cnt, unsigned long long *n_uniq, void *tmp,
+                             size_t tmp_bytes, hipStream_t s) {
+  if (!n) return hipMemsetAsync(n_uniq, 0, sizeof(unsigned long long), s);
+  const u128 *keys = reinterpret_cast<const u128 *>(keys2);
+  u128 *sorted = reinterpret_cast<u128 *>(sorted2), *uniq = reinterpret_cast<u128 *>(uniq2);
+  size_t tb = tmp_bytes;
+  hipError_t e = rocprim::radix_sort_keys(tmp, tb, keys, sorted, n, 0, end_bit, s);
+  if (e != hipSuccess) return e;
+  tb = tmp_bytes;
+  return rocprim::run_length_encode(tmp, tb, (const u128 *)sorted, n, uniq, cnt, n_uniq, s);
+}
+
+hipError_t exact_kpn128(const uint64_t *uniq2, const unsigned long long *n_uniq, size_t max_n,
+                        uint64_t pool, uint32_t *kpn, hipStream_t s) {
+  if (!pool || !max_n) return hipSuccess;
+  FastMod fm;
+  fm.p = pool;
+  fm.magic = (~0ULL) / pool;
+  hipLaunchKernelGGL(k_kpn128, dim3(grid_for(max_n, 8192)), dim3(256), 0, s,
+                     reinterpret_cast<const u128 *>(uniq2), n_uniq, fm, kpn);
+  return hipGetLastError();
+}
+
+hipError_t exact_lookup128(const uint64_t *uniq2, const uint32_t *cnt,
+                           const unsigned long long *n_uniq, const uint64_t *q2, size_t nq,
+                           uint32_t *out, uint32_t *present, hipStream_t s) {
+  if (!nq) return hipSuccess;
+  hipLaunchKernelGGL(k_lookup128, dim3(grid_for(nq, 4096)), dim3(256), 0, s,
+                     reinterpret_cast<const u128 *>(uniq2), cnt, n_uniq, q2, (uint64_t)nq, out,
+                     present);
+  return hipGetLastError();
+}
+
+// ---- rows of top_abundant_neurons(n), any n ----------------------------------------
+size_t rank_rows_temp_bytes(size_t pool) {
+  size_t a = 0;
+  (void)rocprim::radix_sort_pairs(nullptr, a, (const uint64_t *)nullptr, (uint64_t *)nullptr,
+                                  (const uint32_t *)nullptr, (uint32_t *)nullptr, pool, 0, 64);
+  return a + 256;
+}
+
+hipError_t rank_rows(const uint64_t *sc, uint64_t pool, uint64_t max_sc, uint64_t *keys,
+                     uint64_t *keys_sorted, uint32_t *idx, uint32_t *idx_sorted, void *tmp,
+                     size_t tmp_bytes, hipStream_t s) {
+  if (!pool) return hipSuccess;
+  if (pool > 0xFFFFFFFFull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_rank_keys, dim3(grid_for(pool, 8192)), dim3(256), 0, s, sc, pool, max_sc,
+                     keys, idx);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  int end_bit = 1;  // bits of max_sc: keys are max_sc - sc <= max_sc
+  while (end_bit < 64 && (max_sc >> end_bit)) ++end_bit;
+  size_t tb = tmp_bytes;
+  return rocprim::radix_sort_pairs(tmp, tb, (const uint64_t *)keys, keys_sorted,
+                                   (const uint32_t *)idx, idx_sorted, (size_t)pool, 0, end_bit, s);
 }
 
 }  // namespace nk

@@ -1,0 +1,130 @@
+"""The drop-in boundary without preconditions the reference does not have
+(VERDICT r1 "What's weak" 10): top_abundant_neurons(n) for any n, get_count /
+kmer_per_neuron / process_sequence without opts.exact_counts (the table of the
+last input built on demand), and the exact table for 128-bit keys.
+
+Reference: src/spiking_hash.rs:157-172 (counts, kmer_per_neuron), :203-273
+(process_sequence), :661-673 (top_abundant_neurons, any n), :675-682
+(get_count).  Every comparison is bit-exact against oracle/nk_oracle.c.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+from neurokmer_amd import SpikingKmerCounter, synth  # noqa: E402
+from oracle import cbind  # noqa: E402
+
+from test_gpu_parity import _keys_of, assert_exact_same, assert_same, ragged_records  # noqa: E402
+
+
+def _pair(k, pool, canon, width=64, exact=False, top_n=20):
+    g = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, canon, top_n=top_n, kmer_width=width,
+                           exact_counts=exact)
+    r = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, canon, width=width)
+    return g, r
+
+
+@pytest.mark.parametrize("k,pool,canon,width", [(31, 2_000_000, True, 64), (21, 100_000, True, 64),
+                                                (15, 5_003, False, 64), (40, 50_021, True, 64),
+                                                (63, 1_000_003, True, 128), (25, 7_001, False, 128)])
+def test_top_rows_any_n(k, pool, canon, width):
+    """Rows past top_n: the whole pool ranked on the device (ties by index) and
+    the uniques of every row from the table of the last input."""
+    bases, offs = synth.make_records(400_000, 9, repeats_per_mb=5_000, motif_len=90, seed=k,
+                                     n_rate=0.002, mixed_case=True)
+    g, r = _pair(k, pool, canon, width)
+    g.process_parallel_arrays(bases, offs)
+    r.process_parallel_arrays(bases, offs)
+    assert_same(g, r)
+    for n in (21, 64, 1000, 4097, pool, pool + 5):
+        assert g.top_abundant_neurons(n) == r.top_abundant_neurons(n), n
+    assert g.top_abundant_neurons(7) == r.top_abundant_neurons(7)  # the call's own rows
+
+
+def test_top_rows_any_n_streaming_file(tmp_path):
+    """process_file_streaming (held input: the device-parsed file), rows past top_n."""
+    reads, roffs = synth.make_reads(3000, 150, seed=21)
+    path = str(tmp_path / "r.fq")
+    synth.write_fastq(path, reads, roffs)
+    g, r = _pair(31, 16_000_000, True)
+    g.process_file_streaming(path)
+    from neurokmer_amd.fastx import stream_sequences
+    r.process_streaming(list(stream_sequences(path)))
+    assert_same(g, r)
+    for n in (20, 500, 10_000):
+        assert g.top_abundant_neurons(n) == r.top_abundant_neurons(n), n
+
+
+@pytest.mark.parametrize("k,canon", [(21, True), (31, False), (33, True), (5, True)])
+def test_table_on_demand(k, canon):
+    """get_count / distinct / kmer_per_neuron without exact_counts: built from the
+    held input when first asked, equal to the eager table."""
+    bases, offs = ragged_records(total=80_000, n_rate=0.01, mixed_case=True, seed=500 + k,
+                                 repeats_per_mb=20_000, motif_len=70)
+    g, r = _pair(k, 4099, canon)
+    g.process_parallel_arrays(bases, offs)
+    r.process_parallel_arrays(bases, offs)
+    assert_same(g, r)
+    assert_exact_same(g, r, _keys_of(bases, offs, k, canon), 4099)
+    # a second call replaces counts (src/spiking_hash.rs:157): the table follows
+    b2, o2 = ragged_records(total=30_000, seed=600 + k)
+    g.process_parallel_arrays(b2, o2)
+    r.process_parallel_arrays(b2, o2)
+    assert_exact_same(g, r, _keys_of(b2, o2, k, canon), 4099)
+
+
+@pytest.mark.parametrize("canon", [True, False])
+def test_process_sequence_without_exact_counts(canon):
+    """process_parallel then process_sequence reads with the default options:
+    the previous call's table is built first, then counts and kmer_per_neuron
+    accumulate as in the reference."""
+    k, pool = 17, 997
+    bases, offs = synth.make_records(60_000, 4, repeats_per_mb=30_000, motif_len=50, seed=18,
+                                     n_rate=0.003)
+    reads, roffs = synth.make_reads(60, 90, seed=19)
+    rl = synth.records_list(reads, roffs)
+    g, r = _pair(k, pool, canon)
+    g.process_parallel_arrays(bases, offs)
+    r.process_parallel_arrays(bases, offs)
+    keys = _keys_of(bases, offs, k, canon)
+    for rd in rl:
+        g.process_sequence(rd)
+        r.process_sequence(rd)
+        keys.update(int(x) for x in cbind.kmer_keys(rd, k, canon))
+    assert_same(g, r)
+    assert_exact_same(g, r, keys, pool)
+    assert g.top_abundant_neurons(300) == r.top_abundant_neurons(300)
+
+
+@pytest.mark.parametrize("k,canon,exact", [(63, True, True), (40, False, True), (21, True, False),
+                                           (64, True, False)])
+def test_exact_table_128(k, canon, exact):
+    """kmer_width=128: the exact table (eager or on demand): distinct keys,
+    kmer_per_neuron, get_count of u128 keys, uniques of rows past top_n."""
+    bases, offs = ragged_records(total=70_000, n_rate=0.01, mixed_case=True, seed=700 + k,
+                                 repeats_per_mb=20_000, motif_len=90)
+    pool = 20_011
+    g, r = _pair(k, pool, canon, width=128, exact=exact)
+    g.process_parallel_arrays(bases, offs)
+    r.process_parallel_arrays(bases, offs)
+    assert_same(g, r)
+    np.testing.assert_array_equal(g.kmer_per_neuron(), r.kmer_per_neuron())
+    assert g.distinct_kmers() == r.distinct_kmers()
+    keys = set()
+    for i in range(offs.size - 1):
+        keys.update(cbind.kmer_keys128(bases[int(offs[i]):int(offs[i + 1])].tobytes(), k, canon))
+    probe = sorted(keys)[:3000]
+    rng = np.random.default_rng(k)
+    probe += [int(a) | (int(b) << 64) for a, b in zip(rng.integers(0, 2**63, 300, dtype=np.uint64),
+                                                       rng.integers(0, 2**20, 300, dtype=np.uint64))]
+    cnt, pres = g.get_counts128(probe)
+    for kk, c, p in zip(probe, cnt, pres):
+        assert (int(c) if p else None) == r.get_count(kk), hex(kk)
+    assert g.top_abundant_neurons(2000) == r.top_abundant_neurons(2000)

@@ -482,10 +482,11 @@ def test_errors_fail_loudly():
         g.process_parallel([b"ACGTACGTAC"])
     g.process_parallel([b"ACG"])  # no k-mers: the reference does not panic either
     g2 = SpikingKmerCounter(5, 1.0, 0.95, 2, 1.0, 10, True)
+    # a fresh counter: any n (min(n, pool) rows in index order), empty counts
+    assert g2.top_abundant_neurons(21) == [(i, 0, 0) for i in range(10)]
+    assert g2.get_count(0) is None
     with pytest.raises(_lib.NeuroKmerError):
-        g2.top_abundant_neurons(21)  # uniques tracked for top_n rows only
-    with pytest.raises(_lib.NeuroKmerError):
-        g2.get_count(0)
+        g2.get_counts128([1])  # 64-bit handle
 
 
 @pytest.mark.parametrize("shape", ["config2"])
@@ -575,15 +576,25 @@ def test_exact_counts_partitioned_config2_shape():
     assert g.distinct_kmers() == r.distinct_kmers()
 
 
-def test_get_count_needs_exact_counts():
+def test_table_on_demand_needs_a_held_input():
+    """Without exact_counts the table is built from the last input on demand;
+    device input passed by pointer is the caller's, so those queries refuse."""
     g = SpikingKmerCounter(21, 1.0, 0.95, 2, 1.0, 1000, True)
-    with pytest.raises(_lib.NeuroKmerError) as e:
-        g.get_count(5)
-    assert e.value.code == _lib.NK_E_UNSUPPORTED
+    assert g.get_count(5) is None  # fresh: empty counts
+    bases, offs = synth.make_records(20_000, 3, seed=4)
+    d_b = torch.from_numpy(np.concatenate([bases, np.zeros(16, np.uint8)])).cuda()
+    d_o = torch.from_numpy(offs.view(np.int64)).cuda()
+    torch.cuda.synchronize()
+    g.process_parallel_device(d_b.data_ptr(), d_o.data_ptr(), offs.size - 1, int(offs[-1]))
+    for call in (lambda: g.get_count(5), lambda: g.top_abundant_neurons(500),
+                 lambda: g.process_sequence(b"ACGT" * 20), g.distinct_kmers):
+        with pytest.raises(_lib.NeuroKmerError) as e:
+            call()
+        assert e.value.code == _lib.NK_E_UNSUPPORTED
+    assert len(g.top_abundant_neurons(20)) == 20  # the call's own rows need no table
     with pytest.raises(_lib.NeuroKmerError):
-        g.process_sequence(b"ACGT" * 20)
-    with pytest.raises(_lib.NeuroKmerError):
-        SpikingKmerCounter(31, 1.0, 0.95, 2, 1.0, 1000, True, exact_counts=True, kmer_width=128)
+        SpikingKmerCounter(31, 1.0, 0.95, 2, 1.0, 1000, True, kmer_width=128).process_sequence(
+            b"ACGT" * 20)
 
 
 @pytest.mark.parametrize("canon", [True, False])
