@@ -13,6 +13,10 @@ Workloads (--workload):
       dist.shard_records (byte ranges, records cut with a k-1 halo), k=31,
       pool 2M; currents all-reduced over RCCL (u32 wire while the total k-mers
       stay below 2^31).
+  config5 (weak scaling, a side line: BASELINE.json configs[4]): k=63 with
+      128-bit keys, pool 256,000,000, --bases per rank (default 115e6 in 7
+      records); N>1 finishes pool-sliced (dist.finalize_step_sliced: reduce-
+      scatter of the currents, LIF + top rows of each rank's 1/N of the pool).
 
 One step = reset the neuron pool, then one full pass of the hot path over the
 resident input: tile/record index -> K1a hash + partition -> K1b bucket
@@ -145,7 +149,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=("config2", "config4"), default="config2")
+    ap.add_argument("--workload", choices=("config2", "config4", "config5"), default="config2")
     ap.add_argument("--bases", type=int, default=BASES, help="config2: bases per rank")
     ap.add_argument("--total-bases", type=int, default=8 * BASES, help="config4: bases in all")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -176,6 +180,8 @@ def main() -> int:
     import torch
     import torch.distributed as dist
 
+    if args.workload == "config5":  # BASELINE.json configs[4]
+        args.k, args.pool, args.kmer_width = 63, 256_000_000, 128
     pool, k = args.pool, args.k
     ndev = torch.cuda.device_count()  # counts devices without initialising them
     shared = world > ndev  # rehearsal: ranks share devices
@@ -195,19 +201,21 @@ def main() -> int:
     from neurokmer_amd.counter import diag_hash_ms
 
     # ---- this rank's input (resident in HBM) -------------------------------
-    if args.workload == "config2":
+    if args.workload in ("config2", "config5"):
         bases, offsets = synth.make_records(args.bases, RECS, seed=synth.SEED ^ (rank * 0x9E37),
                                             repeats_per_mb=64, motif_len=200)
         nk_rank = n_kmers(offsets, k)
         total_kmers = world * nk_rank  # same size on every rank
         scaling = "weak"
-        workload = (f"config 2: {bases.size:,} bases in {RECS} records per GPU, k={k}, "
-                    f"pool_size={pool:,}, --canonical, process_parallel")
+        workload = (f"config {args.workload[-1]}: {bases.size:,} bases in {RECS} records per GPU, "
+                    f"k={k}, kmer_width={args.kmer_width}, pool_size={pool:,}, --canonical, "
+                    + ("process_parallel" if args.workload == "config2" or world == 1 else
+                       "pool-sliced finish"))
     else:
         T = args.total_bases
         n_rec = max(1, -(-T // REC_LEN4))
         glob = np.minimum(np.arange(n_rec + 1, dtype=np.int64) * REC_LEN4, T).astype(np.uint64)
-        lo, hi, rel = nkdist.shard_records(glob, world, k)[rank]
+        lo, hi, rel, _skip = nkdist.shard_records(glob, world, k)[rank]  # k <= 32: no warm-up
         bases = synth.random_bases(hi - lo, seed=synth.SEED, start=lo)
         offsets = rel.astype(np.uint64)
         nk_rank = n_kmers(offsets, k)
@@ -242,7 +250,10 @@ def main() -> int:
         # stay below 2^31, then LIF + top-N + this shard's top k-mers into a
         # fixed-size all-gather segment, the union merged on the device: one
         # host synchronisation per step
-        nkdist.finalize_step(ctr, total_kmers=total_kmers)
+        if args.workload == "config5":
+            nkdist.finalize_step_sliced(ctr, total_kmers=total_kmers)
+        else:
+            nkdist.finalize_step(ctr, total_kmers=total_kmers)
 
     per = float("inf")  # fastest warmup step (the first one allocates)
     for _ in range(max(args.warmup, 1 if args.settle > 0 else 0)):
@@ -336,7 +347,7 @@ def main() -> int:
             "ms_per_step": round(ms_step, 4),
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "u64",
             "data": ("synthetic (splitmix64 i.i.d. ACGT, seed 0x4E4B4D52" +
-                     ("^rank, 64x200-bp planted repeats per MB)" if args.workload == "config2"
+                     ("^rank, 64x200-bp planted repeats per MB)" if args.workload != "config4"
                       else ", one global stream sharded by byte range)")),
             "config": {"workload": workload, "k": k, "kmer_width": args.kmer_width,
                        "pool_size": pool, "bases_rank0": int(bases.size), "records_rank0": n_recs,

@@ -152,6 +152,38 @@ int nk_finalize_export(nk_counter *c, int streaming_semantics, const uint32_t *d
 int nk_merge_export(nk_counter *c, const uint64_t *d_buf, size_t world, size_t stride,
                     size_t cap, int *redo, void *stream);
 int nk_finalize_redo(nk_counter *c, void *stream);
+/* Pool-sliced finish for very large pools (config 5: P up to 2^31 over W ranks;
+ * neurokmer_amd/dist.py::finalize_step_sliced).  Rank r owns the neurons
+ * [lo, hi) = [r*S, min(P, (r+1)*S)), S = ceil(P / W):
+ *   nk_accumulate_device (+ nk_wire32 into a W*S-entry wire, zero-padded, or the
+ *                          u64 currents copied into a W*S-entry buffer)
+ *   <caller: reduce_scatter(wire) -> this rank's S summed entries d_slice>
+ *   nk_finalize_slice   — LIF of [lo, hi) only from d_slice (u32 or u64 per
+ *                         slice_bits), the slice's top rows into d_seg:
+ *                         [rows, new spikes, max spike count, (idx, spikes,
+ *                         current) x rows], seg_rows >= min(top_n, pool);
+ *                         one host synchronisation
+ *   <caller: all-gather(d_seg) -> d_all[world * stride], stride >= 3 + 3*seg_rows>
+ *   nk_adopt_slices     — the global top rows (every global top row is among
+ *                         its slice's), total spikes and energy, this shard's
+ *                         uniques pass for those rows
+ *   <caller: the union of the shards' keys — nk_top_kmers_padded /
+ *                         nk_merge_top_kmers_padded, as after nk_finalize>
+ * Afterwards v / refractory / spike counts / currents are authoritative on
+ * [lo, hi) only (the other ranks own the rest).  Replaces the reference's
+ * single-process pool (src/spiking_hash.rs:49-53,97,186-200). */
+int nk_finalize_slice(nk_counter *c, int streaming_semantics, const void *d_slice, int slice_bits,
+                      size_t lo, size_t hi, uint64_t *d_seg, size_t seg_rows, void *stream);
+int nk_adopt_slices(nk_counter *c, const uint64_t *d_all, size_t world, size_t stride,
+                    void *stream);
+/* nk_accumulate_device counting only the windows that start at or after
+ * first_pos (bases before it are context: a shard cut inside a record of a
+ * k > 32 NK_KMER_COMPAT input keeps a 32-base warm-up, after which the
+ * reference's rolling reverse strand no longer depends on the record start,
+ * src/models.rs:260-266). */
+int nk_accumulate_device_from(nk_counter *c, const uint8_t *d_bases,
+                              const uint64_t *d_rec_offsets, size_t n_recs, size_t n_bases,
+                              size_t first_pos, void *stream);
 /* After nk_finalize on a shard: the distinct k-mer keys of this shard that map
  * to the current top-N neurons (device buffer owned by the handle, valid until
  * the next call).  The caller gathers every shard's list and hands the union

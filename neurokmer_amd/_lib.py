@@ -40,6 +40,7 @@ EXPORTS = (
     "nk_copy_refractory", "nk_device_currents", "nk_reset", "nk_reset_async", "nk_last_timings",
     "nk_count_history", "nk_wire32", "nk_finalize_export", "nk_merge_export", "nk_finalize_redo",
     "nk_top_kmers_padded", "nk_merge_top_kmers_padded",
+    "nk_finalize_slice", "nk_adopt_slices", "nk_accumulate_device_from",
     "nk_exact_owner", "nk_exact_partition", "nk_exact_adopt", "nk_device_kmer_per_neuron",
     "nk_set_stage_timing", "nk_diag_hash_ms", "nk_count_spans",
     "nk_last_error",
@@ -100,6 +101,9 @@ def load(share_torch: bool = True):
         "nk_process_file_parallel": (C.c_int, [vp, C.c_char_p]),
         "nk_accumulate_device": (C.c_int, [vp, vp, vp, sz, sz, vp]),
         "nk_finalize": (C.c_int, [vp, C.c_int, vp]),
+        "nk_finalize_slice": (C.c_int, [vp, C.c_int, vp, C.c_int, sz, sz, vp, sz, vp]),
+        "nk_adopt_slices": (C.c_int, [vp, vp, sz, sz, vp]),
+        "nk_accumulate_device_from": (C.c_int, [vp, vp, vp, sz, sz, sz, vp]),
         "nk_top_kmers": (C.c_int, [vp, P(vp), P(sz)]),
         "nk_merge_top_kmers": (C.c_int, [vp, vp, sz, vp]),
         "nk_top_kmers_padded": (C.c_int, [vp, vp, sz, vp]),

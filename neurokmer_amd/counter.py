@@ -117,6 +117,22 @@ class SpikingKmerCounter:
         check(self._L.nk_accumulate_device(self._h, d_bases, d_offsets, n_recs, n_bases,
                                            stream or None))
 
+    def accumulate_device_from(self, d_bases: int, d_offsets: int, n_recs: int, n_bases: int,
+                               first_pos: int, stream: int = 0) -> None:
+        """accumulate_device counting only windows that start at >= first_pos."""
+        check(self._L.nk_accumulate_device_from(self._h, d_bases, d_offsets, n_recs,
+                                                n_bases, first_pos, stream or None))
+
+    def finalize_slice(self, d_slice: int, slice_bits: int, lo: int, hi: int, d_seg: int,
+                       seg_rows: int, streaming: bool = False, stream: int = 0) -> None:
+        """Pool-sliced finish, step 1 (include/neurokmer.h nk_finalize_slice)."""
+        check(self._L.nk_finalize_slice(self._h, 1 if streaming else 0, d_slice or None,
+                                        slice_bits, lo, hi, d_seg, seg_rows, stream or None))
+
+    def adopt_slices(self, d_all: int, world: int, stride: int, stream: int = 0) -> None:
+        """Pool-sliced finish, step 2 (nk_adopt_slices)."""
+        check(self._L.nk_adopt_slices(self._h, d_all, world, stride, stream or None))
+
     def finalize(self, streaming: bool = False, stream: int = 0) -> None:
         check(self._L.nk_finalize(self._h, 1 if streaming else 0, stream or None))
 

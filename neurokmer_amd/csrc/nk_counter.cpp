@@ -181,6 +181,7 @@ struct nk_counter {
   // built on demand (get_count, kmer_per_neuron, top rows past top_n,
   // process_sequence) from that input, while it is still resident
   bool x_lazy = false;              // the table is the last input's, not built yet
+  bool slice_ready = false;         // nk_finalize_slice ran; nk_adopt_slices next
   bool input_owned = false;         // last_in is the handle's own copy (host/file entry points)
   // top_abundant_neurons(n) past the rows the last call selected
   DevBuf<uint64_t> rk_keys;         // [2P]: keys | sorted keys
@@ -685,7 +686,8 @@ static hipError_t gen_count(nk_counter *c, const CountPlan &cp, const KmerInput 
 // defer_partials: leave K1c (currents += partials) to the LIF kernel of the
 // same process call instead of a separate pass
 static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_offs,
-                      size_t n_recs, size_t n_bases, void *stream, bool defer_partials) {
+                      size_t n_recs, size_t n_bases, void *stream, bool defer_partials,
+                      uint64_t first_pos = 0) {
   if (!c) return fail(NK_E_INVALID, "null counter");
   if (n_bases && ((uintptr_t)d_bases & 15))
     return fail(NK_E_INVALID, "device bases must be 16-byte aligned");
@@ -702,6 +704,7 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
   in.offsets = d_offs;
   in.n_recs = n_recs;
   in.n_bases = n_bases;
+  in.pos_lo = first_pos;
   // one prep kernel: tile -> first record index, and every buffer the count
   // (and, for a process call, the LIF) accumulates into zeroed
   ZeroList z{};
@@ -780,18 +783,29 @@ int nk_accumulate_device(nk_counter *c, const uint8_t *d_bases, const uint64_t *
   return accumulate(c, d_bases, d_offs, n_recs, n_bases, stream, true);
 }
 
+int nk_accumulate_device_from(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_offs,
+                              size_t n_recs, size_t n_bases, size_t first_pos, void *stream) {
+  return accumulate(c, d_bases, d_offs, n_recs, n_bases, stream, true, first_pos);
+}
+
 // ---------------------------------------------------------------------------
 // exact radix refine of the top-N threshold (spike counts >= 4095; rare)
 // ---------------------------------------------------------------------------
+// (sc, n): the spike counts ranked — the whole pool, or a rank's slice of it
+// (nk_finalize_slice); sc == nullptr means the handle's own pool
 static int refine_threshold(nk_counter *c, uint64_t want, uint64_t max_sc, TopState &st,
-                            hipStream_t s) {
+                            hipStream_t s, const uint64_t *sc = nullptr, uint64_t n = 0) {
+  if (!sc) {
+    sc = c->sc.p;
+    n = c->pool;
+  }
   int top_bit = 63;
   while (top_bit > 0 && !((max_sc >> top_bit) & 1)) --top_bit;
   int shift = (top_bit / 8) * 8;
   uint64_t prefix = 0, above = 0;
   for (;;) {
     HIPCHK(hipMemsetAsync(c->radix_h.p, 0, 256 * 4, s));
-    HIPCHK(launch_radix_hist(c->sc.p, c->pool, shift, prefix, c->radix_h.p, s));
+    HIPCHK(launch_radix_hist(sc, n, shift, prefix, c->radix_h.p, s));
     uint32_t h[256];
     HIPCHK(hipMemcpyAsync(h, c->radix_h.p, sizeof h, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -817,9 +831,9 @@ static int refine_threshold(nk_counter *c, uint64_t want, uint64_t max_sc, TopSt
 // uniques post step (part: the partitioned count's records are used)
 // wire != nullptr: the currents are the (all-reduced) u32 wire vector of
 // nk_wire32; the LIF reads them from it and writes the u64 currents
-static int enqueue_lif(nk_counter *c, int streaming, uint32_t fuse_want, bool part,
-                       hipStream_t s, const uint32_t *wire = nullptr) {
-  LifParams lp;
+// LIF parameters of a finalize, the closed-form table for them (cached), and
+// the spike histogram + stats zeroed unless this call's prep already did it
+static int lif_prepare(nk_counter *c, int streaming, LifParams &lp, hipStream_t s) {
   lp.steps = c->steps;
   lp.thr = c->thr;
   lp.leak = c->leak;
@@ -841,6 +855,15 @@ static int enqueue_lif(nk_counter *c, int streaming, uint32_t fuse_want, bool pa
     z.n = 2;
     HIPCHK(launch_zero(z, s));
   }
+  c->lif_zeroed = false;
+  return NK_OK;
+}
+
+static int enqueue_lif(nk_counter *c, int streaming, uint32_t fuse_want, bool part,
+                       hipStream_t s, const uint32_t *wire = nullptr) {
+  LifParams lp;
+  int rc = lif_prepare(c, streaming, lp, s);
+  if (rc) return rc;
   TopFuse tf{};
   if (fuse_want) {
     const uint32_t nb = lif_blocks(c->pool);
@@ -857,7 +880,6 @@ static int enqueue_lif(nk_counter *c, int streaming, uint32_t fuse_want, bool pa
                        c->tbuckets.p, c->post_flags.p, c->uniq.p, c->special.p, c->n_hits.p,
                        c->last_pa.bin_bits};
   }
-  c->lif_zeroed = false;
   // steps == 0: the kernel leaves every neuron as it is (streaming returns early,
   // src/spiking_hash.rs:549-551; in-memory runs zero iterations)
   if (wire) {
@@ -879,13 +901,21 @@ static int enqueue_lif(nk_counter *c, int streaming, uint32_t fuse_want, bool pa
   return NK_OK;
 }
 
-static int enqueue_select(nk_counter *c, uint64_t want, hipStream_t s) {
-  const unsigned nb = (unsigned)((c->pool + 2047) / 2048);
+// (sc, n, cur): as refine_threshold; candidate indices are relative to sc
+static int enqueue_select(nk_counter *c, uint64_t want, hipStream_t s,
+                          const uint64_t *sc = nullptr, uint64_t n = 0,
+                          const uint64_t *cur = nullptr) {
+  if (!sc) {
+    sc = c->sc.p;
+    n = c->pool;
+    cur = c->cur.p;
+  }
+  const unsigned nb = (unsigned)((n + 2047) / 2048);
   int rc;
   if ((rc = c->tie_cnt.ensure(nb))) return rc;
-  HIPCHK(launch_topn_count(c->sc.p, c->pool, c->topst.p, c->tie_cnt.p, s));
-  HIPCHK(launch_topn_emit(c->sc.p, c->pool, c->topst.p, c->tie_cnt.p, c->cand.p, s));
-  HIPCHK(launch_topn_sort(c->cand.p, (uint32_t)want, c->cur.p, c->top_cur.p, s));
+  HIPCHK(launch_topn_count(sc, n, c->topst.p, c->tie_cnt.p, s));
+  HIPCHK(launch_topn_emit(sc, n, c->topst.p, c->tie_cnt.p, c->cand.p, s));
+  HIPCHK(launch_topn_sort(c->cand.p, (uint32_t)want, cur, c->top_cur.p, s));
   return NK_OK;
 }
 
@@ -1520,6 +1550,143 @@ int nk_finalize_redo(nk_counter *c, void *stream) {
   HIPCHK(hipStreamSynchronize(s));
   c->top_keys_ready = false;
   c->top_valid = true;
+  return NK_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Pool-sliced multi-GPU finish (P up to 2^31):
+//   reduce-scatter(currents) -> nk_finalize_slice: LIF + top rows of this
+//   rank's neurons [lo, hi) only -> all-gather the slices' candidate rows ->
+//   nk_adopt_slices: the global top rows, total spikes, this shard's uniques
+//   pass for them -> (dist.union_top_kmers: the union of the shards' keys).
+// The neuron state is sharded: after it, a rank's v / refractory / spike
+// counts / currents are authoritative on [lo, hi) only.
+// ---------------------------------------------------------------------------
+static constexpr size_t kSliceHdr = 3;  // [rows, new spikes, max spike count]
+
+int nk_finalize_slice(nk_counter *c, int streaming, const void *d_slice, int slice_bits,
+                      size_t lo, size_t hi, uint64_t *d_seg, size_t seg_rows, void *stream) {
+  if (!c || !d_seg) return fail(NK_E_INVALID, "null argument");
+  if (lo > hi || hi > c->pool) return fail(NK_E_INVALID, "slice [%zu, %zu) outside the pool", lo, hi);
+  if (slice_bits != 32 && slice_bits != 64) return fail(NK_E_INVALID, "slice_bits must be 32 or 64");
+  if (hi > lo && !d_slice) return fail(NK_E_INVALID, "null slice");
+  const uint64_t want = std::min<uint64_t>(c->opts.top_n, c->pool);
+  if (seg_rows < want) return fail(NK_E_INVALID, "seg_rows (%zu) < top_n rows (%llu)", seg_rows,
+                                   (unsigned long long)want);
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  HIPCHK(mark(c, 7, s));
+  const uint64_t n = hi - lo;
+  const uint64_t m = std::min<uint64_t>(want, n);
+  LifParams lp;
+  int rc = lif_prepare(c, streaming, lp, s);
+  if (rc) return rc;
+  // the reduced slice replaces this shard's currents and pending partials
+  c->pend_slices = 0;
+  c->cur_in_wire = false;
+  c->cur_fresh = false;
+  c->top_valid = false;
+  c->top_keys_ready = false;
+  if (n) {
+    if (slice_bits == 64)
+      HIPCHK(hipMemcpyAsync(c->cur.p + lo, d_slice, n * 8, hipMemcpyDeviceToDevice, s));
+    const bool w32 = slice_bits == 32;
+    HIPCHK(launch_lif_apply(c->cur.p + lo, w32 ? (const uint32_t *)d_slice : nullptr, w32 ? 1u : 0u,
+                            w32 ? 1 : 0, nullptr, (int)c->last_pa.bin_bits, c->state_fresh ? 1 : 0,
+                            c->v.p + lo, c->r.p + lo, c->sc.p + lo, n, lp, c->lif_tbl.p, kLifTable,
+                            c->hist.p, c->stats.p, TopFuse{}, s));
+  }
+  c->state_fresh = false;
+  if (m) {
+    HIPCHK(launch_topn_threshold(c->hist.p, m, n, c->topst.p, s));
+    if ((rc = enqueue_select(c, m, s, c->sc.p + lo, n, c->cur.p + lo))) return rc;
+  }
+  if ((rc = enqueue_readback(c, (uint32_t)m, false, s))) return rc;
+  if ((rc = wait_readback(c, s))) return rc;
+  const ResultHdr *h = reinterpret_cast<const ResultHdr *>(c->res_h);
+  const uint64_t new_spikes = h->stats[0], max_sc = h->stats[1];
+  if (m && h->st.refine) {  // spike counts >= 4095: exact radix refine over the slice
+    TopState st = h->st;
+    if ((rc = refine_threshold(c, m, max_sc, st, s, c->sc.p + lo, n))) return rc;
+    HIPCHK(hipMemcpyAsync(c->topst.p, &st, sizeof st, hipMemcpyHostToDevice, s));
+    if ((rc = enqueue_select(c, m, s, c->sc.p + lo, n, c->cur.p + lo))) return rc;
+  }
+  std::vector<TopCand> rows(m);
+  std::vector<uint64_t> rcur(m);
+  if (m) {
+    HIPCHK(hipMemcpyAsync(rows.data(), c->cand.p, m * sizeof(TopCand), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(rcur.data(), c->top_cur.p, m * 8, hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  std::vector<uint64_t> seg(kSliceHdr + 3 * m);
+  seg[0] = m;
+  seg[1] = new_spikes;
+  seg[2] = max_sc;
+  for (uint64_t i = 0; i < m; ++i) {
+    seg[kSliceHdr + 3 * i] = rows[i].idx + lo;  // global neuron index
+    seg[kSliceHdr + 3 * i + 1] = rows[i].sc;
+    seg[kSliceHdr + 3 * i + 2] = rcur[i];
+  }
+  HIPCHK(hipMemcpyAsync(d_seg, seg.data(), seg.size() * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));  // seg is host memory the copy reads
+  c->slice_ready = true;
+  return NK_OK;
+}
+
+int nk_adopt_slices(nk_counter *c, const uint64_t *d_all, size_t world, size_t stride,
+                    void *stream) {
+  if (!c || !d_all) return fail(NK_E_INVALID, "null argument");
+  if (!c->slice_ready) return fail(NK_E_INVALID, "nk_finalize_slice first");
+  const uint64_t want = std::min<uint64_t>(c->opts.top_n, c->pool);
+  if (!world || world > (1u << 20) || stride < kSliceHdr + 3 * want)
+    return fail(NK_E_INVALID, "bad all-gather layout (world %zu, stride %zu)", world, stride);
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  c->slice_ready = false;
+  std::vector<uint64_t> all(world * stride);
+  HIPCHK(hipMemcpyAsync(all.data(), d_all, all.size() * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  // every global top row is among its slice's top rows: rank the union by
+  // (spikes desc, index asc) — src/spiking_hash.rs:661-673's stable order
+  struct Row { uint64_t idx, sc, cur; };
+  std::vector<Row> cand;
+  uint64_t new_spikes = 0;
+  for (size_t r = 0; r < world; ++r) {
+    const uint64_t *g = all.data() + r * stride;
+    if (g[0] > want || kSliceHdr + 3 * g[0] > stride)
+      return fail(NK_E_INVALID, "segment %zu holds %llu rows", r, (unsigned long long)g[0]);
+    new_spikes += g[1];
+    for (uint64_t i = 0; i < g[0]; ++i)
+      cand.push_back(Row{g[kSliceHdr + 3 * i], g[kSliceHdr + 3 * i + 1], g[kSliceHdr + 3 * i + 2]});
+  }
+  const uint64_t m = std::min<uint64_t>(want, cand.size());
+  std::partial_sort(cand.begin(), cand.begin() + m, cand.end(), [](const Row &a, const Row &b) {
+    return a.sc != b.sc ? a.sc > b.sc : a.idx < b.idx;
+  });
+  std::vector<TopCand> tc(m);
+  std::vector<uint64_t> tcur(m);
+  for (uint64_t i = 0; i < m; ++i) {
+    tc[i] = TopCand{cand[i].idx, cand[i].sc};
+    tcur[i] = cand[i].cur;
+  }
+  TopState st{};
+  if (m) {
+    HIPCHK(hipMemcpyAsync(c->cand.p, tc.data(), m * sizeof(TopCand), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->top_cur.p, tcur.data(), m * 8, hipMemcpyHostToDevice, s));
+  }
+  HIPCHK(hipMemcpyAsync(c->topst.p, &st, sizeof st, hipMemcpyHostToDevice, s));
+  c->total_spikes += new_spikes;
+  c->total_energy += new_spikes * cost_fixed(c->cost);
+  // this shard's distinct keys of the global rows (the caller unions them)
+  const bool uniq = m && c->have_input && c->last_in.n_tiles;
+  int rc;
+  if (uniq && (rc = enqueue_uniques(c, (uint32_t)m, false, false, s))) return rc;
+  if ((rc = enqueue_readback(c, (uint32_t)m, uniq, s))) return rc;
+  if ((rc = wait_readback(c, s))) return rc;
+  if ((rc = settle_top(c, m, uniq, false, false, s))) return rc;
+  HIPCHK(hipStreamSynchronize(s));  // tc / tcur are host memory the copies read
+  c->top_valid = true;
+  collect_timings(c, c->have_input);
   return NK_OK;
 }
 

@@ -19,9 +19,19 @@ contributions are all-reduced; get_counts() routes queries to the owners.
 
 shard_records() splits one input into world shards at record boundaries and,
 where a record is longer than a shard, inside the record with a k-1 base halo,
-so every window is counted by exactly one rank.  k > 32 (compat mode) keeps
-whole records: its reverse strand depends on the record start
-(src/models.rs:260-266).
+so every window is counted by exactly one rank.  k > 32 canonical keys of the
+reference's release build (NK_KMER_COMPAT) depend on the record start for the
+first 32 windows of a record only (the rolling reverse strand's init residue,
+src/models.rs:260-266): a cut at least 32 bases into a record keeps a 32-base
+warm-up before it whose windows the shard does not count (`skip`, passed to
+accumulate_device_from); a cut closer to the record start moves to it.  The
+128-bit keys and non-canonical pack_kmer keys are pure functions of the window:
+the k-1 halo alone suffices.
+
+For very large pools (config 5) finalize_step_sliced() replaces the all-reduce
+of the whole currents vector by a reduce-scatter: each rank runs the LIF and
+the top-N selection on its 1/world slice of the pool only, the slices' top
+rows are all-gathered (nk_finalize_slice / nk_adopt_slices).
 """
 from __future__ import annotations
 
@@ -30,39 +40,49 @@ from typing import List, Tuple
 import numpy as np
 
 
-def shard_records(offsets: np.ndarray, world: int, k: int) -> List[Tuple[int, int, np.ndarray]]:
-    """-> per rank (byte_lo, byte_hi, shard_offsets) with shard_offsets relative to
-    byte_lo.  The k-mer start positions of the input are split into world
-    contiguous ranges of (nearly) equal size."""
+WARMUP = 32  # bases of context before a cut inside a k > 32 compat record
+
+
+def shard_records(offsets: np.ndarray, world: int, k: int, kmer_width: int = 64,
+                  canonical: bool = True) -> List[Tuple[int, int, np.ndarray, int]]:
+    """-> per rank (byte_lo, byte_hi, shard_offsets, skip) with shard_offsets
+    relative to byte_lo; the shard counts the windows that start at >= skip
+    (accumulate_device_from).  The k-mer start positions of the input are split
+    into world contiguous ranges of (nearly) equal size."""
     offsets = np.asarray(offsets, dtype=np.int64)
     n = int(offsets[-1])
     if world <= 1 or n == 0:
-        return [(0, n, offsets.astype(np.uint64))] + [(n, n, np.zeros(1, np.uint64))] * (world - 1)
+        return [(0, n, offsets.astype(np.uint64), 0)] + \
+            [(n, n, np.zeros(1, np.uint64), 0)] * (world - 1)
+    warm = WARMUP if (k > 32 and kmer_width == 64 and canonical) else 0
     cuts = [n * r // world for r in range(world + 1)]
-    if k > 32:  # snap to record starts
-        cuts = [int(offsets[np.searchsorted(offsets, c, side="left")]) if c < n else n
-                for c in cuts]
-        cuts[0] = 0
+    if warm:  # a cut within the first `warm` bases of a record moves to its start
+        for r in range(1, world):
+            c = cuts[r]
+            s0 = int(offsets[np.searchsorted(offsets, c, side="right") - 1])
+            if c - s0 < warm:
+                cuts[r] = s0
+        cuts = [max(cuts[:i + 1]) for i in range(world + 1)]  # monotone
     out = []
     for r in range(world):
         lo, hi = cuts[r], cuts[r + 1]
         if hi <= lo:
-            out.append((lo, lo, np.zeros(1, np.uint64)))
+            out.append((lo, lo, np.zeros(1, np.uint64), 0))
             continue
         # records overlapping [lo, hi): starts in [lo, hi), the record holding lo
         i0 = int(np.searchsorted(offsets, lo, side="right")) - 1
+        skip = warm if (warm and lo > int(offsets[i0])) else 0
         ends = []
-        b_hi = hi
         j = i0
         while j < offsets.size - 1 and offsets[j] < hi:
             e = int(offsets[j + 1])
             if e > hi:  # record continues past the cut: keep k-1 halo bases
                 e = min(e, hi + k - 1)
             ends.append(e)
-            b_hi = max(b_hi, e)
             j += 1
-        rel = np.array([0] + [e - lo for e in ends], dtype=np.uint64)
-        out.append((lo, int(lo + rel[-1]), rel))
+        b_lo = lo - skip
+        rel = np.array([0] + [e - b_lo for e in ends], dtype=np.uint64)
+        out.append((b_lo, int(b_lo + rel[-1]), rel, skip))
     return out
 
 
@@ -142,6 +162,119 @@ def finalize_step(ctr, group=None, total_kmers=None, cap: int = 4096,
     if ctr.merge_export(allb.data_ptr(), world, stride, cap, stream):
         ctr.finalize_redo(stream)
         union_top_kmers(ctr, group=group, cap=cap)
+
+
+def slice_bounds(pool: int, world: int, rank: int) -> Tuple[int, int, int]:
+    """-> (lo, hi, S): rank's neurons [lo, hi) of the pool-sliced finish, S =
+    ceil(pool / world) entries per slice (the last slice may be short)."""
+    S = -(-pool // world) if pool else 0
+    lo = min(pool, rank * S)
+    return lo, min(pool, lo + S), S
+
+
+def finalize_step_sliced(ctr, group=None, total_kmers=None, cap: int = 4096,
+                         streaming: bool = False) -> None:
+    """After every rank's accumulate: the finish for very large pools
+    (SURVEY.md §5/§8e, config 5).  Instead of all-reducing the whole currents
+    vector and running the LIF of the whole pool on every rank:
+
+      wire (u32, or u64 when total_kmers is unknown or >= 2^31), zero-padded to
+      world * S entries
+      reduce-scatter(wire) -> this rank's S summed entries    RCCL over xGMI
+      LIF + top rows of neurons [lo, hi) only                  (nk_finalize_slice)
+      all-gather of the slices' top rows (3 + 3*N words each)
+      global top rows, total spikes, this shard's uniques     (nk_adopt_slices)
+      union of the shards' top keys                            (union_top_kmers)
+
+    Afterwards a rank's neuron state is authoritative on its slice only
+    (gather_state assembles the whole pool)."""
+    import torch
+    import torch.distributed as dist
+    if torch.cuda.current_stream().cuda_stream == 0:
+        _on_side_stream(ctr, lambda: finalize_step_sliced(ctr, group, total_kmers, cap, streaming))
+        return
+    stream = torch.cuda.current_stream().cuda_stream
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    pool = ctr.pool_size
+    lo, hi, S = slice_bounds(pool, world, rank)
+    bufs = ctr.__dict__.setdefault("_dist_bufs", {})
+    small = total_kmers is not None and 0 <= total_kmers < (1 << 31)
+    dt = torch.int32 if small else torch.int64
+    key = ("slice", world, S, small)
+    if key not in bufs:  # the padding past the pool stays zero
+        bufs[key] = (torch.zeros(max(world * S, 1), dtype=dt, device=dev),
+                     torch.empty(max(S, 1), dtype=dt, device=dev))
+    wire, part = bufs[key]
+    if small:
+        ctr.wire32(wire.data_ptr(), stream)
+    elif pool:
+        wire[:pool].copy_(_currents_view(ctr, dev))
+    if S:
+        _reduce_scatter(part[:S], wire[:world * S], group=group)
+    rows = min(ctr.top_n, pool)
+    stride = 3 + 3 * rows
+    skey = ("sseg", world, stride)
+    if skey not in bufs:
+        bufs[skey] = (torch.zeros(stride, dtype=torch.int64, device=dev),
+                      torch.zeros(world * stride, dtype=torch.int64, device=dev))
+    seg, allseg = bufs[skey]
+    ctr.finalize_slice(part.data_ptr(), 32 if small else 64, lo, hi, seg.data_ptr(), rows,
+                       streaming, stream)
+    _all_gather_into(allseg, seg, group=group)
+    ctr.adopt_slices(allseg.data_ptr(), world, stride, stream)
+    union_top_kmers(ctr, group=group, cap=cap)
+
+
+def _reduce_scatter(out, inp, group=None):
+    """reduce_scatter_tensor (sum); gloo (CPU rehearsals) has none: the same
+    result through an all-reduce in host memory."""
+    import torch.distributed as dist
+    if dist.get_backend(group) == "gloo":
+        full = inp.cpu()
+        dist.all_reduce(full, op=dist.ReduceOp.SUM, group=group)
+        r, n = dist.get_rank(group), out.numel()
+        out.copy_(full[r * n:(r + 1) * n])
+        return
+    dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=group)
+
+
+def gather_state(ctr, group=None) -> dict:
+    """After finalize_step_sliced: the whole pool's state assembled from every
+    rank's slice (host arrays; collective)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    pool = ctr.pool_size
+    lo, hi, S = slice_bounds(pool, world, rank)
+    out = {}
+    for name, arr in (("currents", ctr.currents()), ("spike_counts", ctr.spike_counts()),
+                      ("voltages", ctr.voltages()), ("refractory", ctr.refractory())):
+        a64 = np.zeros(max(S, 1), np.int64)  # one slot per rank even for an empty pool
+        a64[:hi - lo] = arr[lo:hi].view(np.int64) if arr.dtype.itemsize == 8 else \
+            arr[lo:hi].view(np.int32).astype(np.int64)
+        t = torch.from_numpy(a64)
+        allt = torch.zeros(max(world * S, world), dtype=torch.int64)
+        _all_gather_host(allt, t, group)
+        full = allt.numpy()[:pool]
+        out[name] = full.view(arr.dtype) if arr.dtype.itemsize == 8 else \
+            full.astype(np.int32).view(arr.dtype)
+    return out
+
+
+def _all_gather_host(out, inp, group=None):
+    """all_gather_into_tensor of host tensors (through the device for RCCL)."""
+    import torch
+    import torch.distributed as dist
+    if dist.get_backend(group) == "gloo":
+        dist.all_gather_into_tensor(out, inp, group=group)
+        return
+    dev = torch.device("cuda", torch.cuda.current_device())
+    o = out.to(dev)
+    dist.all_gather_into_tensor(o, inp.to(dev), group=group)
+    out.copy_(o.cpu())
 
 
 def _on_side_stream(ctr, fn):

@@ -33,7 +33,7 @@ def _worker(rank, world, port, k, pool, q):
         from oracle import cbind
         bases, offs = synth.make_records(90_000, 3, seed=7, repeats_per_mb=30000, motif_len=50,
                                          n_rate=0.002)
-        lo, hi, soffs = nkdist.shard_records(offs, world, k)[rank]
+        lo, hi, soffs, _ = nkdist.shard_records(offs, world, k)[rank]
         shard = bases[lo:hi]
         ctr = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, True)
         ctr.process_parallel_arrays(shard, soffs, 1)
@@ -87,21 +87,31 @@ def test_gloo_two_ranks_match_whole_input(k, pool):
 
 
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
-@pytest.mark.parametrize("k", [5, 31, 40])
-def test_shard_records_cover_every_window_once(world, k):
+@pytest.mark.parametrize("k,canon", [(5, False), (31, True), (40, False), (40, True),
+                                     (63, True), (96, True)])
+def test_shard_records_cover_every_window_once(world, k, canon):
+    """Every window's key is counted by exactly one shard — for k > 32 canonical
+    (the reference's release-build keys, which depend on the record start for
+    a record's first 32 windows) through the 32-base warm-up of a cut inside a
+    record (the shard skips the windows that start in it)."""
     from oracle import cbind
     bases, offs = synth.make_records(20_000, 3, seed=world * 100 + k, n_rate=0.01)
     want = []
     for i in range(offs.size - 1):
         want += [int(x) for x in cbind.kmer_keys(bases[int(offs[i]):int(offs[i + 1])].tobytes(),
-                                                 k, False)]
+                                                 k, canon)]
     got = []
-    for lo, hi, so in nkdist.shard_records(offs, world, k):
+    splits = 0
+    for lo, hi, so, skip in nkdist.shard_records(offs, world, k, canonical=canon):
         sh = bases[lo:hi]
+        splits += skip > 0
         for i in range(so.size - 1):
-            got += [int(x) for x in cbind.kmer_keys(sh[int(so[i]):int(so[i + 1])].tobytes(), k,
-                                                    False)]
+            ks = [int(x) for x in cbind.kmer_keys(sh[int(so[i]):int(so[i + 1])].tobytes(), k,
+                                                  canon)]
+            got += ks[skip:] if i == 0 else ks  # windows starting before skip: context
     assert sorted(got) == sorted(want)
+    if k > 32 and canon and world >= 2:
+        assert splits > 0  # records were cut inside, not snapped to their starts
 
 
 def test_exact_table_partition_protocol():
@@ -123,7 +133,7 @@ def test_exact_table_partition_protocol():
 
     whole = table(bases, offs)
     owned = [dict() for _ in range(world)]
-    for lo, hi, so in nkdist.shard_records(offs, world, k):
+    for lo, hi, so, _ in nkdist.shard_records(offs, world, k):
         t = table(bases[lo:hi], so)
         keys = np.array(sorted(t), dtype=np.uint64)
         for key, r in zip(keys.tolist(), nkdist.exact_owner(keys, world).tolist()):

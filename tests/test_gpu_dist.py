@@ -48,7 +48,7 @@ def _rank(rank, world, port, keys, q):
         from neurokmer_amd import SpikingKmerCounter
         from neurokmer_amd import dist as nkdist
         bases, offs = _input()
-        lo, hi, so = nkdist.shard_records(offs, world, K)[rank]
+        lo, hi, so, _ = nkdist.shard_records(offs, world, K)[rank]
         b = bases[lo:hi]
         d_b = torch.from_numpy(np.concatenate([b, np.zeros(16, np.uint8)])).cuda()
         d_o = torch.from_numpy(so.astype(np.uint64).view(np.int64)).cuda()
@@ -110,13 +110,13 @@ def _rank_union(rank, world, port, width, cap, q):
         from neurokmer_amd import dist as nkdist
         bases, offs = _input()
         k = 41 if width == 128 else K
-        lo, hi, so = nkdist.shard_records(offs, world, k)[rank]
+        lo, hi, so, skip = nkdist.shard_records(offs, world, k, kmer_width=width)[rank]
         b = bases[lo:hi]
         d_b = torch.from_numpy(np.concatenate([b, np.zeros(16, np.uint8)])).cuda()
         d_o = torch.from_numpy(so.astype(np.uint64).view(np.int64)).cuda()
         torch.cuda.synchronize()
         c = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, POOL, True, kmer_width=width)
-        c.accumulate_device(d_b.data_ptr(), d_o.data_ptr(), so.size - 1, b.size)
+        c.accumulate_device_from(d_b.data_ptr(), d_o.data_ptr(), so.size - 1, b.size, skip)
         cur = torch.as_tensor(_CAI(c.device_currents_ptr(), POOL), device="cuda")
         nkdist.allreduce_currents_(cur)
         c.finalize(False)
@@ -175,7 +175,7 @@ def _rank_step(rank, world, port, width, cap, steps, wire, q, skew=False):
         from neurokmer_amd import dist as nkdist
         bases, offs = _skewed_input() if skew else _input()
         k = 41 if width == 128 else K
-        lo, hi, so = nkdist.shard_records(offs, world, k)[rank]
+        lo, hi, so, skip = nkdist.shard_records(offs, world, k, kmer_width=width)[rank]
         b = bases[lo:hi]
         d_b = torch.from_numpy(np.concatenate([b, np.zeros(16, np.uint8)])).cuda()
         d_o = torch.from_numpy(so.astype(np.uint64).view(np.int64)).cuda()
@@ -187,7 +187,7 @@ def _rank_step(rank, world, port, width, cap, steps, wire, q, skew=False):
         for it in range(3):
             if it == 1:
                 c.reset()
-            c.accumulate_device(d_b.data_ptr(), d_o.data_ptr(), so.size - 1, b.size)
+            c.accumulate_device_from(d_b.data_ptr(), d_o.data_ptr(), so.size - 1, b.size, skip)
             nkdist.finalize_step(c, total_kmers=int(offs[-1]) if wire else None, cap=cap)
             out.append((c.top_abundant_neurons(20), c.energy.total_spikes()))
         q.put((rank, out, c.currents().tolist(), c.spike_counts().tolist()))
@@ -258,7 +258,7 @@ def _rank_config4(rank, world, port, exact, q):
         from neurokmer_amd import SpikingKmerCounter
         from neurokmer_amd import dist as nkdist
         bases, offs = _config4_input()
-        lo, hi, so = nkdist.shard_records(offs, world, C4_K)[rank]
+        lo, hi, so, _ = nkdist.shard_records(offs, world, C4_K)[rank]
         b = bases[lo:hi]
         d_b = torch.from_numpy(np.concatenate([b, np.zeros(16, np.uint8)])).cuda()
         d_o = torch.from_numpy(so.astype(np.uint64).view(np.int64)).cuda()

@@ -264,7 +264,7 @@ def test_exact_table_across_shards(world):
     bases, offs = synth.make_records(300_000, 6, seed=31, repeats_per_mb=20000, motif_len=70,
                                      n_rate=0.002)
     ranks, keep = [], []
-    for lo, hi, so in nkdist.shard_records(offs, world, k):
+    for lo, hi, so, _ in nkdist.shard_records(offs, world, k):
         b = bases[lo:hi]
         d_b = torch.from_numpy(np.concatenate([b, np.zeros(16, np.uint8)])).cuda()
         d_o = torch.from_numpy(so.astype(np.uint64).view(np.int64)).cuda()
