@@ -913,7 +913,7 @@ static int enqueue_select(nk_counter *c, uint64_t want, hipStream_t s,
   const unsigned nb = (unsigned)((n + 2047) / 2048);
   int rc;
   if ((rc = c->tie_cnt.ensure(nb))) return rc;
-  HIPCHK(launch_topn_count(sc, n, c->topst.p, c->tie_cnt.p, s));
+  HIPCHK(launch_topn_count(sc, n, c->topst.p, c->tie_cnt.p, c->cand.p, s));
   HIPCHK(launch_topn_emit(sc, n, c->topst.p, c->tie_cnt.p, c->cand.p, s));
   HIPCHK(launch_topn_sort(c->cand.p, (uint32_t)want, cur, c->top_cur.p, s));
   return NK_OK;

@@ -314,6 +314,7 @@ __global__ __launch_bounds__(256) void k_seq_lif(uint64_t pool, unsigned long lo
   for (int i = threadIdx.x; i < kHistBins; i += 256) sh[i] = 0;
   __syncthreads();
   unsigned long long sp = 0, mx = 0;
+  uint32_t n_zero = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < pool;
        i += (uint64_t)gridDim.x * 256) {
     if (touched[i]) {  // :258-263 kmer_per_neuron[idx] += 1 per sequence
@@ -342,13 +343,16 @@ __global__ __launch_bounds__(256) void k_seq_lif(uint64_t pool, unsigned long lo
       currents[i] = 0;  // :270
     }
     mx = sc > mx ? sc : mx;
-    atomicAdd(&sh[sc < (uint64_t)(kHistBins - 1) ? (uint32_t)sc : (uint32_t)(kHistBins - 1)], 1u);
+    if (sc == 0) ++n_zero;  // bin 0 in a register (same-address atomics serialise)
+    else atomicAdd(&sh[sc < (uint64_t)(kHistBins - 1) ? (uint32_t)sc : (uint32_t)(kHistBins - 1)], 1u);
   }
   for (int o = 32; o > 0; o >>= 1) {
     sp += __shfl_down(sp, o, 64);
     const unsigned long long om = __shfl_down(mx, o, 64);
     mx = om > mx ? om : mx;
+    n_zero += __shfl_down(n_zero, o, 64);
   }
+  if ((threadIdx.x & 63) == 0 && n_zero) atomicAdd(&sh[0], n_zero);
   if ((threadIdx.x & 63) == 0) {
     if (sp) atomicAdd(&stats[0], sp);
     atomicMax(&stats[1], mx);

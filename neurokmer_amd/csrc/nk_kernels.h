@@ -189,8 +189,8 @@ hipError_t launch_topn_threshold(const uint32_t *hist, uint64_t n, uint64_t pool
                                  hipStream_t s);
 hipError_t launch_radix_hist(const uint64_t *sc, uint64_t pool, int shift, uint64_t prefix,
                              uint32_t *hist256, hipStream_t s);
-hipError_t launch_topn_count(const uint64_t *sc, uint64_t pool, const TopState *st,
-                             uint32_t *tie_cnt, hipStream_t s);
+hipError_t launch_topn_count(const uint64_t *sc, uint64_t pool, TopState *st,
+                             uint32_t *tie_cnt, TopCand *cand, hipStream_t s);
 hipError_t launch_topn_emit(const uint64_t *sc, uint64_t pool, TopState *st,
                             const uint32_t *tie_cnt, TopCand *cand, hipStream_t s);
 hipError_t launch_topn_sort(TopCand *cand, uint32_t m, const uint64_t *currents,

@@ -1406,6 +1406,7 @@ __global__ __launch_bounds__(kLifBlock) void k_lif_apply(uint64_t *__restrict__ 
   __syncthreads();
   const uint64_t base = (uint64_t)blockIdx.x * kLifBlock * kLifPerThread;
   unsigned long long my_sp = 0, my_mx = 0;
+  uint32_t n_zero = 0;  // neurons of this thread with spike count 0 (histogram bin 0)
   // all loads of this thread's neurons first (a few round trips), then the LIF
   uint64_t cntv[kLifPerThread], scv[kLifPerThread];
   float vin[kLifPerThread];
@@ -1472,14 +1473,19 @@ __global__ __launch_bounds__(kLifBlock) void k_lif_apply(uint64_t *__restrict__ 
     }
     scv[j] = sc;
     my_mx = sc > my_mx ? sc : my_mx;
-    atomicAdd(&sh[sc < (uint64_t)(kHistBins - 1) ? (uint32_t)sc : (uint32_t)(kHistBins - 1)], 1u);
+    // neurons that never spiked (most of a large pool) are counted in a
+    // register: same-address LDS atomics of a whole wave serialise
+    if (sc == 0) ++n_zero;
+    else atomicAdd(&sh[sc < (uint64_t)(kHistBins - 1) ? (uint32_t)sc : (uint32_t)(kHistBins - 1)], 1u);
   }
   // wave reductions
   for (int o = 32; o > 0; o >>= 1) {
     my_sp += __shfl_down(my_sp, o, 64);
     unsigned long long om = __shfl_down(my_mx, o, 64);
     my_mx = om > my_mx ? om : my_mx;
+    n_zero += __shfl_down(n_zero, o, 64);
   }
+  if ((threadIdx.x & 63) == 0 && n_zero) atomicAdd(&sh[0], n_zero);
   if ((threadIdx.x & 63) == 0) { s_sp[threadIdx.x >> 6] = my_sp; s_mx[threadIdx.x >> 6] = my_mx; }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1579,17 +1585,26 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t *__restric
 
 constexpr int kTopChunk = kBlock * 8;  // neurons per block in count/emit
 
+// one pass over the spike counts: the rows above T are emitted (any order:
+// k_topn_sort orders them) and each block's ties (== T) counted
 __global__ __launch_bounds__(kBlock) void k_topn_count(const uint64_t *__restrict__ sc,
-                                                       uint64_t pool,
-                                                       const TopState *__restrict__ st,
-                                                       uint32_t *__restrict__ tie_cnt) {
+                                                       uint64_t pool, TopState *__restrict__ st,
+                                                       uint32_t *__restrict__ tie_cnt,
+                                                       TopCand *__restrict__ cand) {
   __shared__ uint32_t s[kBlock / 64];
   const uint64_t T = st->T;
   const uint64_t base = (uint64_t)blockIdx.x * kTopChunk;
   uint32_t c = 0;
   for (int j = 0; j < 8; ++j) {
-    uint64_t i = base + (uint64_t)j * kBlock + threadIdx.x;
-    if (i < pool && sc[i] == T) ++c;
+    const uint64_t i = base + (uint64_t)j * kBlock + threadIdx.x;
+    if (i >= pool) break;
+    const uint64_t v = sc[i];
+    if (v == T) ++c;
+    if (v > T && T != ~0ULL) {
+      const unsigned long long pos = atomicAdd((unsigned long long *)&st->emit_above, 1ull);
+      cand[pos].idx = i;
+      cand[pos].sc = v;
+    }
   }
   for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
   if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
@@ -1598,22 +1613,41 @@ __global__ __launch_bounds__(kBlock) void k_topn_count(const uint64_t *__restric
 }
 
 // in-place exclusive scan of the per-block tie counts (one block; the counts
-// sum to <= pool < 2^32)
+// sum to <= pool < 2^32).  The counts pass through LDS a piece at a time with
+// coalesced loads; each thread sums a contiguous run of kPer entries of its
+// piece from LDS, stored one pad word per kPer entries so that the runs of a
+// wave's lanes start in different banks.
+constexpr uint32_t kTieScanPiece = 16384;
+__device__ __forceinline__ uint32_t tie_slot(uint32_t e) { return e + (e >> 4); }
 __global__ __launch_bounds__(1024) void k_tie_scan(uint32_t *__restrict__ cnt, uint32_t n) {
   __shared__ uint32_t s_w[16];
-  const uint32_t per = (n + 1023) / 1024;
-  const uint32_t lo = threadIdx.x * per, hi = lo + per < n ? lo + per : n;
-  uint32_t sum = 0;
-  for (uint32_t i = lo; i < hi; ++i) sum += cnt[i];
-  uint32_t tot;
-  uint32_t run = block_excl_scan<uint32_t>(sum, s_w, &tot);
-  for (uint32_t i = lo; i < hi; ++i) {
-    const uint32_t x = cnt[i];
-    cnt[i] = run;
-    run += x;
+  __shared__ uint32_t s_c[kTieScanPiece + kTieScanPiece / 16];
+  constexpr uint32_t kPer = kTieScanPiece / 1024;  // 16: matches tie_slot's pad
+  uint32_t carry = 0;
+  for (uint32_t p0 = 0; p0 < n; p0 += kTieScanPiece) {
+    const uint32_t m = n - p0 < kTieScanPiece ? n - p0 : kTieScanPiece;
+    for (uint32_t i = threadIdx.x; i < m; i += 1024) s_c[tie_slot(i)] = cnt[p0 + i];
+    __syncthreads();
+    const uint32_t lo = threadIdx.x * kPer;
+    uint32_t sum = 0;
+    for (uint32_t i = lo; i < lo + kPer && i < m; ++i) sum += s_c[tie_slot(i)];
+    uint32_t tot;
+    uint32_t run = carry + block_excl_scan<uint32_t>(sum, s_w, &tot);
+    for (uint32_t i = lo; i < lo + kPer && i < m; ++i) {
+      const uint32_t x = s_c[tie_slot(i)];
+      s_c[tie_slot(i)] = run;
+      run += x;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < m; i += 1024) cnt[p0 + i] = s_c[tie_slot(i)];
+    carry += tot;
+    __syncthreads();
   }
 }
 
+// the first `need` ties in index order (the rows above T were emitted by
+// k_topn_count): only blocks whose earlier ties fall short of `need` read
+// their spike counts
 __global__ __launch_bounds__(kBlock) void k_topn_emit(const uint64_t *__restrict__ sc,
                                                       uint64_t pool, TopState *__restrict__ st,
                                                       const uint32_t *__restrict__ tie_cnt,
@@ -1622,6 +1656,7 @@ __global__ __launch_bounds__(kBlock) void k_topn_emit(const uint64_t *__restrict
   const uint64_t T = st->T, need = st->need, n_above = st->n_above;
   // ties in earlier blocks (k_tie_scan turned the counts into an exclusive scan)
   const unsigned long long prefix = tie_cnt[blockIdx.x];
+  if (prefix >= need) return;  // uniform across the block
   // thread t owns 8 consecutive neurons -> ranks in index order
   const uint64_t base = (uint64_t)blockIdx.x * kTopChunk + (uint64_t)threadIdx.x * 8;
   uint32_t ties = 0;
@@ -1630,13 +1665,7 @@ __global__ __launch_bounds__(kBlock) void k_topn_emit(const uint64_t *__restrict
     uint64_t i = base + j;
     v[j] = i < pool ? sc[i] : 0;
     if (i < pool && v[j] == T) ++ties;
-    if (i < pool && v[j] > T && T != ~0ULL) {
-      unsigned long long pos = atomicAdd((unsigned long long *)&st->emit_above, 1ull);
-      cand[pos].idx = i;
-      cand[pos].sc = v[j];
-    }
   }
-  if (prefix >= need) return;  // uniform across the block
   s_scan[threadIdx.x] = ties;
   __syncthreads();
   for (int o = 1; o < kBlock; o <<= 1) {
@@ -1965,11 +1994,11 @@ static unsigned topn_blocks(uint64_t pool) {
   return (unsigned)((pool + kTopChunk - 1) / kTopChunk);
 }
 
-hipError_t launch_topn_count(const uint64_t *sc, uint64_t pool, const TopState *st,
-                             uint32_t *tie_cnt, hipStream_t s) {
+hipError_t launch_topn_count(const uint64_t *sc, uint64_t pool, TopState *st,
+                             uint32_t *tie_cnt, TopCand *cand, hipStream_t s) {
   if (!pool) return hipSuccess;
   hipLaunchKernelGGL(k_topn_count, dim3(topn_blocks(pool)), dim3(kBlock), 0, s, sc, pool, st,
-                     tie_cnt);
+                     tie_cnt, cand);
   hipLaunchKernelGGL(k_tie_scan, dim3(1), dim3(1024), 0, s, tie_cnt, (uint32_t)topn_blocks(pool));
   return hipGetLastError();
 }
