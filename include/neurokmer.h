@@ -325,6 +325,37 @@ int nk_count_spans(nk_counter *c, float *ms, int cap);
  * kernel live on the device.  (No reference counterpart.) */
 int nk_diag_hash_ms(int device, uint64_t n_keys, uint64_t pool, int reps, float *ms);
 
+/* ---- associative memory (src/associative.rs) -------------
+ * WillshawNetwork — :12-62.  Binary weights of pattern_size^2 bits on the
+ * device (bit-packed rows).  store: every pair of set bits of the pattern gets
+ * weight 1 (a pattern of another size: NK_E_INVALID "Pattern size mismatch");
+ * recall: up to `steps` synchronous updates state' = (W state > 0), stopping
+ * when the state repeats; out[i] = 255 or 0. */
+typedef struct nk_willshaw nk_willshaw;
+nk_willshaw *nk_willshaw_new(size_t pattern_size, int device);
+void nk_willshaw_free(nk_willshaw *w);
+int nk_willshaw_store(nk_willshaw *w, const uint8_t *pattern, size_t len);
+int nk_willshaw_recall(nk_willshaw *w, const uint8_t *noisy, size_t len, size_t steps,
+                       uint8_t *out);
+uint64_t nk_willshaw_stored(const nk_willshaw *w);  /* stored_count */
+/* KmerAssociativeMemory — :64-139.  pattern_size = 2^k for k <= 10, else 1024;
+ * a k-mer's pattern sets bit (byte i % 32 of BLAKE3(kmer as 8 LE bytes)) %
+ * pattern_size for i < pattern_size / 100, computed on the device.
+ * nk_assoc_store_kmers = store_kmer over a batch (counts may be NULL: the
+ * reference does not use them).  nk_assoc_find_similar = find_similar: the
+ * query's pattern recalled over 10 steps, then every distinct stored k-mer
+ * whose pattern is within max_distance bits (Hamming) of it, with similarity
+ * 1 - d / pattern_size (f32), by similarity descending (equal similarities by
+ * k-mer ascending: the reference's order there is HashMap iteration order).
+ * Writes min(count, cap) results, returns count (or < 0). */
+typedef struct nk_assoc nk_assoc;
+nk_assoc *nk_assoc_new(size_t k, int device);
+void nk_assoc_free(nk_assoc *a);
+size_t nk_assoc_pattern_size(const nk_assoc *a);
+int nk_assoc_store_kmers(nk_assoc *a, const uint64_t *kmers, const uint32_t *counts, size_t n);
+long nk_assoc_find_similar(nk_assoc *a, uint64_t query, size_t max_distance, uint64_t *kmers,
+                           float *sim, size_t cap);
+
 const char *nk_last_error(void);
 const char *nk_version(void);
 

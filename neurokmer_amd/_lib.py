@@ -41,6 +41,9 @@ EXPORTS = (
     "nk_count_history", "nk_wire32", "nk_finalize_export", "nk_merge_export", "nk_finalize_redo",
     "nk_top_kmers_padded", "nk_merge_top_kmers_padded",
     "nk_finalize_slice", "nk_adopt_slices", "nk_accumulate_device_from",
+    "nk_willshaw_new", "nk_willshaw_free", "nk_willshaw_store", "nk_willshaw_recall",
+    "nk_willshaw_stored", "nk_assoc_new", "nk_assoc_free", "nk_assoc_pattern_size",
+    "nk_assoc_store_kmers", "nk_assoc_find_similar",
     "nk_exact_owner", "nk_exact_partition", "nk_exact_adopt", "nk_device_kmer_per_neuron",
     "nk_set_stage_timing", "nk_diag_hash_ms", "nk_count_spans",
     "nk_last_error",
@@ -101,6 +104,16 @@ def load(share_torch: bool = True):
         "nk_process_file_parallel": (C.c_int, [vp, C.c_char_p]),
         "nk_accumulate_device": (C.c_int, [vp, vp, vp, sz, sz, vp]),
         "nk_finalize": (C.c_int, [vp, C.c_int, vp]),
+        "nk_willshaw_new": (vp, [sz, C.c_int]),
+        "nk_willshaw_free": (None, [vp]),
+        "nk_willshaw_store": (C.c_int, [vp, vp, sz]),
+        "nk_willshaw_recall": (C.c_int, [vp, vp, sz, sz, vp]),
+        "nk_willshaw_stored": (u64, [vp]),
+        "nk_assoc_new": (vp, [sz, C.c_int]),
+        "nk_assoc_free": (None, [vp]),
+        "nk_assoc_pattern_size": (sz, [vp]),
+        "nk_assoc_store_kmers": (C.c_int, [vp, vp, vp, sz]),
+        "nk_assoc_find_similar": (C.c_long, [vp, u64, sz, vp, vp, sz]),
         "nk_finalize_slice": (C.c_int, [vp, C.c_int, vp, C.c_int, sz, sz, vp, sz, vp]),
         "nk_adopt_slices": (C.c_int, [vp, vp, sz, sz, vp]),
         "nk_accumulate_device_from": (C.c_int, [vp, vp, vp, sz, sz, sz, vp]),

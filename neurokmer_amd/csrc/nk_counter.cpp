@@ -328,6 +328,9 @@ static int copy_out(nk_counter *c, const DevBuf<T> &b, T *out, size_t n) {
   return NK_OK;
 }
 
+// error text for the other translation units of the library (nk_assoc.hip)
+int nk_fail_msg(int code, const char *msg) { return fail(code, "%s", msg); }
+
 extern "C" {
 
 void nk_opts_default(nk_opts *o) {

@@ -232,3 +232,92 @@ class OracleCounter:
         else:
             ok = self._L.nko_get_count(self._h, kmer, C.byref(out))
         return int(out.value) if ok else None
+
+
+# ---- associative memory (oracle/nk_assoc_oracle.c; src/associative.rs) -------
+def _assoc_sigs(L):
+    if getattr(L, "_assoc_ready", False):
+        return L
+    vp, sz, u64 = C.c_void_p, C.c_size_t, C.c_uint64
+    for name, rt, args in (
+            ("nko_blake3", C.c_int, [vp, sz, vp]),
+            ("nko_willshaw_new", vp, [sz]), ("nko_willshaw_free", None, [vp]),
+            ("nko_willshaw_store", C.c_int, [vp, vp, sz]),
+            ("nko_willshaw_recall", C.c_int, [vp, vp, sz, sz, vp]),
+            ("nko_willshaw_stored", u64, [vp]),
+            ("nko_assoc_new", vp, [sz]), ("nko_assoc_free", None, [vp]),
+            ("nko_assoc_pattern_size", sz, [sz]),
+            ("nko_assoc_kmer_pattern", None, [sz, u64, vp]),
+            ("nko_assoc_store", C.c_int, [vp, u64, C.c_uint32]),
+            ("nko_assoc_find_similar", sz, [vp, u64, sz, vp, vp, sz])):
+        f = getattr(L, name)
+        f.restype, f.argtypes = rt, args
+    L._assoc_ready = True
+    return L
+
+
+def blake3(data: bytes) -> bytes:
+    """BLAKE3 digest of <= 1024 bytes (the oracle's one-chunk restatement)."""
+    L = _assoc_sigs(lib())
+    buf = np.frombuffer(bytes(data), np.uint8) if data else np.zeros(1, np.uint8)
+    out = np.zeros(32, np.uint8)
+    if L.nko_blake3(buf.ctypes.data, len(data), out.ctypes.data) != 0:
+        raise ValueError("input longer than one chunk")
+    return out.tobytes()
+
+
+class OracleWillshaw:
+    def __init__(self, n):
+        self._L = _assoc_sigs(lib())
+        self.n = n
+        self._h = self._L.nko_willshaw_new(n)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._L.nko_willshaw_free(self._h)
+            self._h = None
+
+    def store(self, pattern):
+        p = np.frombuffer(bytes(pattern), np.uint8) if len(pattern) else np.zeros(1, np.uint8)
+        if self._L.nko_willshaw_store(self._h, p.ctypes.data, len(pattern)) != 0:
+            raise ValueError("Pattern size mismatch")
+
+    def recall(self, noisy, steps):
+        p = np.frombuffer(bytes(noisy), np.uint8) if len(noisy) else np.zeros(1, np.uint8)
+        out = np.zeros(max(len(noisy), 1), np.uint8)
+        if self._L.nko_willshaw_recall(self._h, p.ctypes.data, len(noisy), steps,
+                                       out.ctypes.data) != 0:
+            raise ValueError("Noisy pattern size mismatch")
+        return out[:len(noisy)].tobytes()
+
+    @property
+    def stored_count(self):
+        return int(self._L.nko_willshaw_stored(self._h))
+
+
+class OracleAssoc:
+    def __init__(self, k):
+        self._L = _assoc_sigs(lib())
+        self._h = self._L.nko_assoc_new(k)
+        self.pattern_size = int(self._L.nko_assoc_pattern_size(k))
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._L.nko_assoc_free(self._h)
+            self._h = None
+
+    def kmer_pattern(self, kmer):
+        out = np.zeros(self.pattern_size, np.uint8)
+        self._L.nko_assoc_kmer_pattern(self.pattern_size, kmer, out.ctypes.data)
+        return out.tobytes()
+
+    def store_kmer(self, kmer, count=0):
+        self._L.nko_assoc_store(self._h, kmer, count)
+
+    def find_similar(self, query, max_distance):
+        n = self._L.nko_assoc_find_similar(self._h, query, max_distance, None, None, 0)
+        km = np.zeros(max(n, 1), np.uint64)
+        sim = np.zeros(max(n, 1), np.float32)
+        self._L.nko_assoc_find_similar(self._h, query, max_distance, km.ctypes.data,
+                                       sim.ctypes.data, n)
+        return [(int(km[i]), float(sim[i])) for i in range(n)]
