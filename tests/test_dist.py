@@ -151,3 +151,28 @@ def test_exact_table_partition_protocol():
     for key in whole:
         ref[int(cbind.lib().nko_map_kmer(key, pool))] += 1
     assert np.array_equal(kpn, ref)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_pool_slices_hold_the_global_top_rows(world):
+    """The pool-sliced finish (dist.finalize_step_sliced, nk_adopt_slices): the
+    slices [r*S, min(P, (r+1)*S)) tile the pool, and the global top rows
+    (spikes desc, index asc; src/spiking_hash.rs:661-673) are the top rows of
+    the union of every slice's own top rows — on the C restatement's state."""
+    from oracle import cbind
+    k, pool, n = 21, 10_007, 20
+    bases, offs = synth.make_records(200_000, 4, seed=5, repeats_per_mb=40_000, motif_len=60)
+    ref = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, True)
+    ref.process_parallel_arrays(bases, offs, 1)
+    sc = ref.spike_counts()
+    covered = np.zeros(pool, np.int64)
+    cand = []
+    for r in range(world):
+        lo, hi, S = nkdist.slice_bounds(pool, world, r)
+        assert S == -(-pool // world)
+        covered[lo:hi] += 1
+        rows = sorted(range(lo, hi), key=lambda i: (-int(sc[i]), i))[:n]
+        cand += [(int(sc[i]), i) for i in rows]
+    assert (covered == 1).all()
+    merged = [i for _, i in sorted(cand, key=lambda t: (-t[0], t[1]))[:n]]
+    assert merged == [t[0] for t in ref.top_abundant_neurons(n)]
