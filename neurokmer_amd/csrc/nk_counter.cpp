@@ -70,6 +70,27 @@ struct DevBuf {
   }
 };
 
+// pinned host memory (the file ingest's double buffer)
+struct PinnedBuf {
+  uint8_t *p = nullptr;
+  size_t n = 0;
+  int ensure(size_t want) {
+    if (want <= n) return NK_OK;
+    release();
+    if (hipHostMalloc((void **)&p, want) != hipSuccess) {
+      p = nullptr;
+      return fail(NK_E_OOM, "hipHostMalloc of %zu bytes failed", want);
+    }
+    n = want;
+    return NK_OK;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
 constexpr int kLifTable = 1 << 16;
 constexpr int kStages = 7;
 const char *kStageNames[kStages] = {"index", "count", "hist", "lif", "topn", "uniques", "total"};
@@ -129,6 +150,10 @@ struct nk_counter {
   // host copies of input (host-array entry points)
   DevBuf<uint8_t> in_bases;
   DevBuf<uint64_t> in_offs;
+  // GPU FASTX ingest buffers, kept between file calls
+  PinnedBuf ing_hb[2];
+  DevBuf<uint8_t> ing_draw, ing_scratch;
+  DevBuf<IngestState> ing_dst;
   // LIF table cache key
   bool lif_valid = false;
   LifParams lif_key{};
@@ -446,6 +471,8 @@ void nk_free(nk_counter *c) {
   c->span.release();
   c->rk_keys.release(); c->rk_idx.release(); c->rk_tmp.release(); c->rk_cand.release();
   c->rk_uniq.release();
+  c->ing_hb[0].release(); c->ing_hb[1].release(); c->ing_draw.release();
+  c->ing_scratch.release(); c->ing_dst.release();
   c->special.release(); c->stats.release(); c->lif_tbl.release(); c->topst.release();
   c->cand.release(); c->top_cur.release(); c->set_keys.release(); c->top_keys.release();
   c->top_keys_n.release(); c->radix_h.release(); c->set_mask_d.release();
@@ -1911,25 +1938,9 @@ static int ingest_file(nk_counter *c, const char *path, bool *fallback) {
   // thread fills one while the device copies and parses the other
   size_t chunk = ingest_chunk_bytes();
   size_t room = std::max<size_t>(chunk / 8, 1 << 16);
-  struct Pinned {
-    uint8_t *p = nullptr;
-    size_t n = 0;
-    ~Pinned() {
-      if (p) (void)hipHostFree(p);
-    }
-    int ensure(size_t want) {
-      if (want <= n) return NK_OK;
-      if (p) (void)hipHostFree(p);
-      p = nullptr;
-      n = 0;
-      if (hipHostMalloc((void **)&p, want) != hipSuccess) {
-        p = nullptr;
-        return fail(NK_E_OOM, "hipHostMalloc of %zu bytes failed", want);
-      }
-      n = want;
-      return NK_OK;
-    }
-  } hb[2];
+  // (kept by the handle: pinning ~150 MB of host memory per call cost more
+  // than reading a 100 MB file from the page cache)
+  PinnedBuf *hb = c->ing_hb;
   if ((rc = hb[0].ensure(room + chunk)) || (rc = hb[1].ensure(room + chunk))) return rc;
   int cur = 0;
   size_t start = room, have = src.read(hb[0].p + room, chunk);
@@ -1940,7 +1951,7 @@ static int ingest_file(nk_counter *c, const char *path, bool *fallback) {
     return fail(NK_E_PARSE, "unknown format: first byte is neither '>' nor '@'");
   std::future<size_t> next;
   auto prefetch = [&](int b) {
-    next = std::async(std::launch::async, [&src, &hb, b, room, chunk] {
+    next = std::async(std::launch::async, [&src, hb, b, room, chunk] {
       return src.read(hb[b].p + room, chunk);
     });
   };
@@ -1949,8 +1960,8 @@ static int ingest_file(nk_counter *c, const char *path, bool *fallback) {
   const uint64_t fsize = src.file_size();
   uint64_t cap_bases = (src.gz() ? 4 * fsize : fsize) + 64;
   if ((rc = c->in_bases.ensure(cap_bases + 16)) || (rc = c->in_offs.ensure(1025))) return rc;
-  DevBuf<uint8_t> draw, scratch;
-  DevBuf<IngestState> dst;
+  DevBuf<uint8_t> &draw = c->ing_draw, &scratch = c->ing_scratch;
+  DevBuf<IngestState> &dst = c->ing_dst;
   if ((rc = draw.ensure(chunk)) || (rc = scratch.ensure(ingest_scratch_bytes(chunk))) ||
       (rc = dst.ensure(1)))
     return rc;
