@@ -453,6 +453,8 @@ __device__ __forceinline__ uint32_t in_vgpr(uint32_t x) {
 #endif
 }
 
+constexpr uint32_t kSpanTail = 2048;  // last-dispatched workgroups that stamp the span's end
+
 // K16: k >= 16, so the low word of the window mask is all ones
 template <bool CANON, int MAXB, bool K16 = false>
 __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMod fm, PartArgs pa) {
@@ -474,7 +476,13 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
   const uint32_t B = pa.n_buckets;
   NK_STAMP(0);
   NK_STAMP(8);
-  if (pa.span && tid == 0) atomicMin(pa.span, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  // the launch's span (nk_count_spans): its first workgroups start it, its
+  // last-dispatched workgroups end it (workgroups run for about the same time
+  // and are dispatched in index order, so no earlier one ends last); stamping
+  // every workgroup (an end barrier + two global atomics each) cost the step
+  // ~5 us (profiles/r02_s15)
+  if (pa.span && tid == 0 && blockIdx.x < 8u)
+    atomicMin(pa.span, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   for (uint32_t b = tid; b <= B; b += kPartBlock) s_cnt[b] = 0;
   stage_tile<kPartTile, kPartBlock, !CANON, !CANON>(L, in, tile, k);  // syncs (INV: pack_kmer only)
   NK_STAMP(2);
@@ -678,7 +686,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
           atomicAdd(&pa.currents[((uint64_t)b << pa.bin_bits) | (w[i] & 0xFFFFu)], 1ULL);
     }
   }
-  if (pa.span) {  // this workgroup's last stores are issued: its end time
+  if (pa.span && blockIdx.x + kSpanTail >= gridDim.x) {  // its last stores are issued: end time
     __syncthreads();
     if (tid == 0) atomicMax(pa.span + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   }
