@@ -24,7 +24,7 @@ histograms -> [N>1: RCCL all-reduce of the currents] -> closed-form LIF ->
 exact top-20 -> unique-k-mer pass for the top-20 rows [N>1: all-gather of the
 top k-mer keys + merge] -> results in host memory.  Inputs are resident in HBM
 before the timed region; timed steps run with no event between kernels
-(stage_timing 2), K1a's duration comes from in-kernel s_memrealtime stamps.
+(stage_timing 3), K1a's duration comes from in-kernel s_memrealtime stamps.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload config2|config4]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
@@ -276,7 +276,10 @@ def main() -> int:
         torch.cuda.synchronize()
     # timed steps: no event between kernels (the count kernel's own duration
     # comes from its in-kernel stamps, nk_count_spans)
-    ctr.set_stage_timing(2)
+    # timed steps record no events at all (stage_timing 3; NK_BENCH_TIMED_LEVEL
+    # for A/B runs); K1a's duration comes from its in-kernel stamps
+    timed_level = int(os.environ.get("NK_BENCH_TIMED_LEVEL", "3"))
+    ctr.set_stage_timing(timed_level)
     # one more untimed step in the timed mode: the first step after the switch
     # measured ~0.18 ms slower on the host side (profiles/r02_s2/bench_default.log,
     # step_ms_host[0]) while its K1a span was normal
@@ -310,7 +313,7 @@ def main() -> int:
     torch.cuda.synchronize()
     ev_ms = [x for x in ctr.count_history(5) if x == x and x > 0]
     stages = ctr.last_timings()
-    ctr.set_stage_timing(2)
+    ctr.set_stage_timing(timed_level)
 
     if rank == 0:
         ms_step = dt / args.steps * 1e3

@@ -57,7 +57,9 @@ typedef struct nk_opts {
                             1: an event between every stage (each costs ~6 us
                             of GPU idle time on MI355X);
                             2: events at both ends of a call only (no event
-                            between two kernels; no count-kernel time) */
+                            between two kernels; no count-kernel time);
+                            3: no events (nk_last_timings reports nothing;
+                            nk_count_spans still times the count kernel) */
   uint32_t exact_counts; /* 1: build the exact k-mer count table on the device
                             (the reference's `counts` DashMap and the full
                             `kmer_per_neuron`, src/spiking_hash.rs:27,157-172)
@@ -307,7 +309,7 @@ int nk_last_timings(const nk_counter *c, const char **names, float *ms, int cap)
  * timed step's K1 duration after its timed loop.  Returns the number written.
  * (No reference counterpart: measurement only.) */
 int nk_count_history(const nk_counter *c, float *ms, int cap);
-/* Sets nk_opts.stage_timing (0, 1 or 2) for later calls on this handle, e.g. 2
+/* Sets nk_opts.stage_timing (0 .. 3) for later calls on this handle, e.g. 3
  * for timed benchmark steps and 0 for a separate count-kernel measurement.
  * (No reference counterpart: measurement only.) */
 int nk_set_stage_timing(nk_counter *c, uint32_t level);

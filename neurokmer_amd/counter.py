@@ -294,7 +294,7 @@ class SpikingKmerCounter:
 
     def set_stage_timing(self, level: int) -> None:
         """0: events around the count kernel (default); 1: every stage; 2: only
-        at both ends of a call (no event between kernels, no K1 time)."""
+        at both ends of a call (no event between kernels, no K1 time); 3: none."""
         _lib.check(self._L.nk_set_stage_timing(self._h, level))
 
     def count_history(self, n: int) -> list:

@@ -250,8 +250,9 @@ struct nk_counter {
 // (stage_timing 0: also around the count kernel; 1: every stage; 2: the ends
 // of a call only, so no event sits between two kernels)
 static bool full_timing(const nk_counter *c) { return c->opts.stage_timing == 1; }
-static bool count_timing(const nk_counter *c) { return c->opts.stage_timing != 2; }
+static bool count_timing(const nk_counter *c) { return c->opts.stage_timing < 2; }
 static hipError_t mark(nk_counter *c, int i, hipStream_t s) {
+  if (c->opts.stage_timing == 3) return hipSuccess;  // no events at all
   if (full_timing(c) || i == 0 || i == 6 || i == 7 || (count_timing(c) && (i == 1 || i == 2)))
     return hipEventRecord(c->ev[i], s);
   return hipSuccess;
@@ -1160,6 +1161,11 @@ static void collect_timings_now(nk_counter *c, bool with_count);
 // (the results are awaited on k_gather's completion word, not on the stream):
 // the timings are read when asked for.
 static void collect_timings(nk_counter *c, bool with_count) {
+  if (c->opts.stage_timing == 3) {  // nothing was recorded
+    c->timing_pending = 0;
+    c->n_stage = 0;
+    return;
+  }
   c->timing_pending = with_count ? 2 : 1;
   c->n_stage = full_timing(c) ? kStages : kStagesLight;
 }
@@ -2380,7 +2386,7 @@ int nk_diag_hash_ms(int device, uint64_t n_keys, uint64_t pool, int reps, float 
 
 int nk_set_stage_timing(nk_counter *c, uint32_t level) {
   if (!c) return fail(NK_E_INVALID, "null counter");
-  if (level > 2) return fail(NK_E_INVALID, "stage timing level must be 0, 1 or 2");
+  if (level > 3) return fail(NK_E_INVALID, "stage timing level must be 0, 1, 2 or 3");
   c->opts.stage_timing = level;
   return NK_OK;
 }
