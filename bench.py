@@ -147,7 +147,9 @@ def timed(fn, reps: int):
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    # the overlapped run's first two steps carry the pipeline's fill (~0.7 ms
+    # extra in all): 50 steps amortise it (profiles/r02_s22)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=("config2", "config4", "config5"), default="config2")
     ap.add_argument("--bases", type=int, default=BASES, help="config2: bases per rank")
@@ -165,6 +167,9 @@ def main() -> int:
     # rehearsal: the multi-rank step (wire all-reduce, key all-gather, merge) in
     # a 1-rank process group, to measure its overhead on a 1-GPU box
     ap.add_argument("--force-dist", action="store_true")
+    ap.add_argument("--inflight", type=int, default=None, choices=(1, 2),
+                    help="batches in flight (default: 2 on one GPU, 1 across ranks): 2 "
+                         "overlaps a batch's finish with the next batch's count")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -188,6 +193,12 @@ def main() -> int:
     dev_idx = local % max(ndev, 1)
     backend = args.dist_backend or ("gloo" if shared else "nccl")
     dist_on = world > 1 or args.force_dist
+    if args.inflight is None:
+        # across ranks the finish holds the collectives: beside the next
+        # batch's count their kernels wait for its workgroups, so the
+        # overlapped step measured slower (1-rank RCCL rehearsal, 0.698 vs
+        # 0.624 ms, profiles/r02_s21)
+        args.inflight = 1 if dist_on else 2
     if dist_on:
         torch.cuda.set_device(dev_idx)
         if backend == "nccl":
@@ -230,37 +241,77 @@ def main() -> int:
     d_offs = torch.from_numpy(offsets.view(np.int64)).to(dev)
     torch.cuda.synchronize()
 
-    ctr = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, True, device=dev_idx,
-                             kmer_width=args.kmer_width)
-    # one non-default stream for the whole run: the library's kernels, its
-    # events and the collectives all go on it (a NULL stream handle would mean
-    # the library's own stream)
-    run_stream = torch.cuda.Stream(device=dev)
+    # two handles: batch i+1's count is enqueued before batch i's finish (LIF,
+    # top-N, uniques, readback; N > 1: the collectives) is awaited.  Each
+    # handle counts on its own stream; finishes go on a high-priority stream
+    # (its own hardware queue: two same-priority torch streams were measured
+    # sharing one queue, which serialises them), so a batch's finish runs
+    # between the workgroups of the next batch's count.  The library orders a
+    # handle's calls across streams itself (pick_stream: the finish waits for
+    # the work of ITS handle's count stream only).  --inflight 1: one handle,
+    # one stream, one batch at a time.
+    ctrs = [SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, True, device=dev_idx,
+                               kmer_width=args.kmer_width) for _ in range(args.inflight)]
+    ctr = ctrs[0]
+    # non-default streams: a NULL stream handle would mean the library's own
+    count_streams = [torch.cuda.Stream(device=dev) for _ in range(args.inflight)]
+    run_stream = count_streams[0]
+    fin_stream = (torch.cuda.Stream(device=dev, priority=torch.cuda.Stream.priority_range()[1])
+                  if args.inflight > 1 else run_stream)
     torch.cuda.set_stream(run_stream)
     s_handle = run_stream.cuda_stream
 
-    def step():
-        ctr.reset(s_handle, blocking=False)
+    def start(j):
+        """Enqueue one batch's count on handle j (returns at once)."""
+        c, sh = ctrs[j], count_streams[j].cuda_stream
+        c.reset(sh, blocking=False)
+        c.accumulate_device(d_bases.data_ptr(), d_offs.data_ptr(), n_recs, bases.size, sh)
+
+    def finish(j, st):
+        """LIF + top-N + uniques of handle j's batch on stream st, results read
+        back (the one host wait).  N > 1: RCCL over xGMI -- the currents as
+        u32 while every rank's k-mers together stay below 2^31, LIF + top-N +
+        this shard's top k-mers into a fixed-size all-gather segment, the union
+        merged on the device."""
+        c = ctrs[j]
         if not dist_on:
-            ctr.process_parallel_device(d_bases.data_ptr(), d_offs.data_ptr(), n_recs, bases.size,
-                                        s_handle)
+            c.finalize(False, st.cuda_stream)
             return
-        ctr.accumulate_device(d_bases.data_ptr(), d_offs.data_ptr(), n_recs, bases.size, s_handle)
-        # RCCL over xGMI: the currents as u32 while every rank's k-mers together
-        # stay below 2^31, then LIF + top-N + this shard's top k-mers into a
-        # fixed-size all-gather segment, the union merged on the device: one
-        # host synchronisation per step
-        if args.workload == "config5":
-            nkdist.finalize_step_sliced(ctr, total_kmers=total_kmers)
-        else:
-            nkdist.finalize_step(ctr, total_kmers=total_kmers)
+        with torch.cuda.stream(st):
+            if args.workload == "config5":
+                nkdist.finalize_step_sliced(c, total_kmers=total_kmers)
+            else:
+                nkdist.finalize_step(c, total_kmers=total_kmers)
+
+    def run(n, inflight, marks=None):
+        """n complete steps (count + finish of one batch each), at most
+        `inflight` batches in flight; all n are finished on return."""
+        if n <= 0:
+            return
+        if inflight == 1:
+            for _ in range(n):
+                start(0)
+                finish(0, run_stream)
+                if marks is not None:
+                    marks.append(time.perf_counter())
+            return
+        start(0)
+        for i in range(n):
+            if i + 1 < n:
+                start((i + 1) % 2)
+            finish(i % 2, fin_stream)
+            if marks is not None:
+                marks.append(time.perf_counter())
+
+    def step():
+        run(1, 1)
 
     per = float("inf")  # fastest warmup step (the first one allocates)
     for _ in range(max(args.warmup, 1 if args.settle > 0 else 0)):
         t_w = time.perf_counter()
-        step()
+        run(args.inflight, args.inflight)  # every handle allocates
         torch.cuda.synchronize()
-        per = min(per, time.perf_counter() - t_w)
+        per = min(per, (time.perf_counter() - t_w) / args.inflight)
     # clock settle: the GPU reaches its sustained clock only after ~10-30 ms of
     # load, so untimed steps continue for about --settle seconds; every rank
     # runs the same number (the steps contain collectives)
@@ -271,40 +322,53 @@ def main() -> int:
             t = torch.tensor([settle], dtype=torch.int64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             settle = int(t.item())
-        for _ in range(settle):
-            step()
+        run(settle, args.inflight)
         torch.cuda.synchronize()
-    # timed steps: no event between kernels (the count kernel's own duration
-    # comes from its in-kernel stamps, nk_count_spans)
     # timed steps record no events at all (stage_timing 3; NK_BENCH_TIMED_LEVEL
     # for A/B runs); K1a's duration comes from its in-kernel stamps
     timed_level = int(os.environ.get("NK_BENCH_TIMED_LEVEL", "3"))
-    ctr.set_stage_timing(timed_level)
-    # one more untimed step in the timed mode: the first step after the switch
+    for c in ctrs:
+        c.set_stage_timing(timed_level)
+    # one more untimed round in the timed mode: the first step after the switch
     # measured ~0.18 ms slower on the host side (profiles/r02_s2/bench_default.log,
     # step_ms_host[0]) while its K1a span was normal
-    step()
+    run(args.inflight, args.inflight)
     torch.cuda.synchronize()
-    if dist_on:
-        dist.barrier()
-    torch.cuda.synchronize()
+
+    def timed(n, inflight, marks):
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t_a = time.perf_counter()
+        run(n, inflight, marks)
+        torch.cuda.synchronize()
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize()
+        d = time.perf_counter() - t_a
+        if dist_on:
+            t = torch.tensor([d], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            d = float(t.item())
+        return t_a, d
+
     marks = []
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        marks.append(time.perf_counter())  # host view: each step ends with its readback
-    torch.cuda.synchronize()
-    if dist_on:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    if dist_on:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    t0, dt = timed(args.steps, args.inflight, marks)
+    # both handles' last batches (same input) gave the same results
+    same_inflight = None
+    if args.inflight > 1:
+        same_inflight = (ctrs[0].top_abundant_neurons(20) == ctrs[1].top_abundant_neurons(20) and
+                         ctrs[0].energy.total_spikes() == ctrs[1].energy.total_spikes())
+    # the same K steps one batch at a time: the step latency, and K1a's
+    # duration without the other batch's finish beside it (the roofline)
+    marks1 = []
+    _, dt1 = timed(args.steps, 1, marks1) if args.inflight > 1 else (t0, dt)
 
     log(f"timed {args.steps} steps: {dt / args.steps * 1e3:.4f} ms/step")
-    spans = ctr.count_spans(args.steps)  # K1a of every timed step (in-kernel stamps)
+    # K1a of every step of the one-at-a-time run (in-kernel stamps), and of
+    # handle 1's steps in the overlapped run (the other batch's finish beside it)
+    spans = ctr.count_spans(args.steps)
+    spans2 = ctrs[1].count_spans(args.steps // 2) if args.inflight > 1 else []
     total_spikes = ctr.energy.total_spikes()
     # cross-check: K1a between hipEvents in 5 extra (untimed) steps
     ctr.set_stage_timing(0)
@@ -348,6 +412,9 @@ def main() -> int:
             "metric": METRIC, "value": round(value, 3), "unit": "Mk-mers/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "settle_steps": settle,
             "ms_per_step": round(ms_step, 4),
+            "inflight": args.inflight,
+            "ms_per_step_one_in_flight": round(dt1 / args.steps * 1e3, 4),
+            "inflight_handles_same_results": same_inflight,
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "u64",
             "data": ("synthetic (splitmix64 i.i.d. ACGT, seed 0x4E4B4D52" +
                      ("^rank, 64x200-bp planted repeats per MB)" if args.workload != "config4"
@@ -362,7 +429,7 @@ def main() -> int:
                          "unit": "GB/s", "frac": round(hbm_frac, 4),
                          "traffic": traffic, "traffic_source": pmc.get("source") if traffic else None,
                          "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(k1_ms, 4),
-                         "avg_launch_source": ("in-kernel s_memrealtime span over the timed steps"
+                         "avg_launch_source": ("in-kernel s_memrealtime span over the one-in-flight timed steps"
                                                if sp else "hipEvents"),
                          "launches_timed": len(sp),
                          "avg_launch_ms_events": round(float(np.mean(ev_ms)), 4) if ev_ms else None,
@@ -370,13 +437,15 @@ def main() -> int:
             "stage_ms_event_steps": {k2: round(v, 4) for k2, v in stages.items()},
             "step_ms_host": [round((b - a) * 1e3, 4) for a, b in zip([t0] + marks[:-1], marks)],
             "k1a_ms_steps": [round(x, 4) for x in spans],
+            "k1a_ms_steps_overlapped": [round(x, 4) for x in spans2],
             "total_spikes": total_spikes,
         }
         if world == 1 and args.workload == "config2" and args.kmer_width == 64:
             out.update(extras(args, ctr, bases, offsets, nk_rank, d_bases, d_offs, s_handle,
                               dev_idx, SpikingKmerCounter, synth))
         print(json.dumps(out), flush=True)
-    ctr.close()
+    for c in ctrs:
+        c.close()
     if dist_on:
         dist.destroy_process_group()
     return 0

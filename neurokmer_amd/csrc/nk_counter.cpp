@@ -193,6 +193,12 @@ struct nk_counter {
   DevBuf<unsigned long long> xp_ctr;
   DevBuf<uint8_t> x_tmp;
   DevBuf<unsigned long long> x_n;  // [0] keys of the last input, [1] distinct keys
+  // kmer_per_neuron by partition (table_kpn): fine / coarse bucket regions,
+  // K1b partials, and the overflow + slices == 1 target (all zero between uses)
+  DevBuf<uint16_t> xk_off;
+  DevBuf<uint32_t> xk_over, xk_wrec, xk_wover, xk_part;
+  DevBuf<unsigned long long> xk_fill, xk_wfill, xk_cur;
+  size_t xk_cur_zeroed = 0;
   bool exact_built = false;        // the sorted table holds the last process/accumulate input
   // process_sequence: delta counts on top of the sorted table, kmer_per_neuron
   DevBuf<unsigned long long> d_keys, d_meta;
@@ -233,6 +239,7 @@ struct nk_counter {
   int n_stage = 0;
   hipStream_t last_s = nullptr;  // stream of the previous enqueue (pick_stream)
   hipEvent_t order_ev = nullptr;
+  bool order_eager = false;  // order_ev marks the end of the last call (record_order)
   int timing_pending = 0;  // 0: stage_ms is current; 1/2: collect (without/with count) on demand
   // ev[1]/ev[2] (around the count kernel) rotate through a ring, one pair per
   // accumulate call, so every call's K1 time stays readable (nk_count_history)
@@ -266,15 +273,26 @@ static uint64_t cost_fixed(double cost) {  // Rust `(cost * 1000.0) as u64`
 }
 
 // The stream an entry point enqueues on (NULL: the handle's own stream).  When
-// it differs from the previous call's, it first waits for that stream's work:
+// it differs from the previous call's, it first waits for that call's work:
 // the calls of one handle stay ordered whatever streams the caller mixes.
+// The wait is on an event recorded when the switch happens -- or, after
+// nk_accumulate_device, on the one recorded at the end of that call
+// (order_eager): by the time of the switch the caller may have queued other
+// work behind it (another handle's count on a stream that shares the hardware
+// queue), which a marker recorded then would wait for as well.
 static hipStream_t pick_stream(nk_counter *c, void *s) {
   hipStream_t t = s ? (hipStream_t)s : c->own_stream;
   if (c->last_s && c->last_s != t && c->order_ev &&
-      hipEventRecord(c->order_ev, c->last_s) == hipSuccess)
+      (c->order_eager || hipEventRecord(c->order_ev, c->last_s) == hipSuccess))
     (void)hipStreamWaitEvent(t, c->order_ev, 0);
+  c->order_eager = false;
   c->last_s = t;
   return t;
+}
+
+// the end of this call's work, for the next call's pick_stream
+static void record_order(nk_counter *c, hipStream_t s) {
+  c->order_eager = c->order_ev && hipEventRecord(c->order_ev, s) == hipSuccess;
 }
 
 // Reset is lazy: the neuron state (spikes, v, r) and the currents are only
@@ -506,6 +524,83 @@ int nk_reset_async(nk_counter *c, void *stream) {
 // ---------------------------------------------------------------------------
 // accumulate: currents = histogram of H(kmer) % pool over this input
 // ---------------------------------------------------------------------------
+// kmer_per_neuron[i] = distinct keys of the table with H(key) % pool == i
+// (src/spiking_hash.rs:467-473), from the table's key array (*n_uniq keys of
+// wpk words, at most max_n).  The keys are hashed and partitioned exactly like
+// the count (k_part_keys, then k_split for pools past 16.7 M, k_bucket_hist
+// and one fold into kpn): no global atomic per key.  The per-key atomic kernel
+// (k_kpn) took 4.2 ms of an 11.4 ms table build at 113 M keys
+// (profiles/r02_s18); it remains only for pools past 2^31.
+static int table_kpn(nk_counter *c, const uint64_t *uniq, const unsigned long long *n_uniq,
+                     uint64_t max_n, int wpk, hipStream_t s) {
+  const uint64_t P = c->pool;
+  int rc;
+  if ((rc = c->kpn.ensure(std::max<uint64_t>(P, 1)))) return rc;
+  if (!P) return NK_OK;
+  const char *force = getenv("NK_KPN_ATOMIC");  // tests / A/B: the per-key atomic kernel
+  if (!max_n || P > (1ull << 31) || (force && atoi(force))) {
+    HIPCHK(hipMemsetAsync(c->kpn.p, 0, P * 4, s));
+    if (!max_n) return NK_OK;
+    HIPCHK(wpk == 2 ? exact_kpn128(uniq, n_uniq, max_n, P, c->kpn.p, s)
+                    : exact_kpn(uniq, n_uniq, max_n, P, c->kpn.p, s));
+    return NK_OK;
+  }
+  const uint64_t B0 = (P + kBinsPerBucket - 1) >> kBinBits;
+  const bool wide = B0 > (uint64_t)kMaxBuckets;
+  GenPartArgs ga{};
+  PartArgs pa{};
+  uint64_t B = B0, cap;
+  if (wide) {
+    int bits = kBinBits;
+    while (((P + (1ull << bits) - 1) >> bits) > (uint64_t)kWideMaxBuckets) ++bits;
+    const uint64_t C = (P + (1ull << bits) - 1) >> bits;
+    // distinct keys hash uniformly: 1.25x the fair share + a tile overflows
+    // only in theory (and stays exact: the excess is counted with atomics)
+    const uint64_t cap_c = (max_n / C * 5 / 4 + kPartTile + 63) & ~63ull;
+    if ((rc = c->xk_wrec.ensure(C * cap_c)) || (rc = c->xk_wfill.ensure(C)) ||
+        (rc = c->xk_wover.ensure(C)))
+      return rc;
+    ga = GenPartArgs{(uint32_t)C, bits, cap_c, c->xk_wrec.p, c->xk_wfill.p, c->xk_wover.p, nullptr};
+    B = C << (bits - kBinBits);
+    cap = max_n / B * 5 / 4 + 8 * ((cap_c + kPartTile - 1) / kPartTile) + 1024;
+    HIPCHK(hipMemsetAsync(c->xk_wfill.p, 0, C * 8, s));
+    HIPCHK(hipMemsetAsync(c->xk_wover.p, 0, C * 4, s));
+  } else {
+    cap = max_n / B * 5 / 4 + kPartTile;
+  }
+  cap = (cap + 63) & ~63ull;
+  const uint32_t slices = (uint32_t)std::max<uint64_t>(1, 256 / B);
+  // xk_cur is zero between calls (k_kpn_fold clears what it read) unless it was
+  // (re)allocated (its size grows) or a call failed half-way (xk_cur_zeroed is
+  // set again only once the fold is enqueued)
+  const size_t clean_n = c->xk_cur_zeroed;
+  c->xk_cur_zeroed = 0;
+  if ((rc = c->xk_off.ensure(B * cap)) || (rc = c->xk_fill.ensure(B)) || (rc = c->xk_over.ensure(B)) ||
+      (rc = c->xk_cur.ensure(P)) || (slices > 1 && (rc = c->xk_part.ensure(slices * P))))
+    return rc;
+  if (!clean_n || clean_n != c->xk_cur.n) HIPCHK(hipMemsetAsync(c->xk_cur.p, 0, c->xk_cur.n * 8, s));
+  HIPCHK(hipMemsetAsync(c->xk_fill.p, 0, B * 8, s));
+  HIPCHK(hipMemsetAsync(c->xk_over.p, 0, B * 4, s));
+  pa.n_buckets = (uint32_t)B;
+  pa.cap = cap;
+  pa.off = c->xk_off.p;
+  pa.fill = c->xk_fill.p;
+  pa.overflow = c->xk_over.p;
+  pa.currents = c->xk_cur.p;
+  pa.bin_bits = kBinBits;
+  if (wide) {
+    ga.currents = c->xk_cur.p;
+  } else {
+    ga = GenPartArgs{(uint32_t)B, kBinBits, cap, c->xk_off.p, c->xk_fill.p, c->xk_over.p, c->xk_cur.p};
+  }
+  HIPCHK(launch_part_keys(uniq, n_uniq, max_n, wpk, P, ga, wide ? 1 : 0, s));
+  if (wide) HIPCHK(launch_split(ga, pa, s));
+  HIPCHK(launch_bucket_hist(pa, P, slices, slices > 1 ? c->xk_part.p : nullptr, s));
+  HIPCHK(launch_kpn_fold(c->xk_part.p, slices > 1 ? slices : 0, P, c->xk_cur.p, c->kpn.p, s));
+  c->xk_cur_zeroed = c->xk_cur.n;
+  return NK_OK;
+}
+
 // The exact k-mer table of this input (opts.exact_counts; nk_exact.h).  One
 // host synchronisation (the key count sizes the sort).
 static int build_exact(nk_counter *c, const KmerInput &in0, hipStream_t s) {
@@ -533,16 +628,13 @@ static int build_exact(nk_counter *c, const KmerInput &in0, hipStream_t s) {
       (rc = c->x_cnt.ensure(nn)) ||
       (rc = c->x_tmp.ensure(c->w128 ? exact_temp_bytes128(nn, end_bit) : exact_temp_bytes(nn, end_bit))))
     return rc;
-  HIPCHK(hipMemsetAsync(c->kpn.p, 0, c->pool * 4, s));
-  if (c->w128) {
+  if (c->w128)
     HIPCHK(exact_sort_rle128(c->x_keys.p, c->x_sorted.p, n, end_bit, c->x_uniq.p, c->x_cnt.p,
                              c->x_n.p + 1, c->x_tmp.p, c->x_tmp.n, s));
-    HIPCHK(exact_kpn128(c->x_uniq.p, c->x_n.p + 1, n, c->pool, c->kpn.p, s));
-  } else {
+  else
     HIPCHK(exact_sort_rle(c->x_keys.p, c->x_sorted.p, n, end_bit, c->x_uniq.p, c->x_cnt.p,
                           c->x_n.p + 1, c->x_tmp.p, c->x_tmp.n, s));
-    HIPCHK(exact_kpn(c->x_uniq.p, c->x_n.p + 1, n, c->pool, c->kpn.p, s));
-  }
+  if ((rc = table_kpn(c, c->x_uniq.p, c->x_n.p + 1, n, w, s))) return rc;
   c->x_lazy = false;
   c->exact_built = true;
   c->kpn_valid = true;
@@ -807,16 +899,23 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
   return NK_OK;
 }
 
+// The split entry points (a finish usually follows on another stream: the
+// multi-GPU step, or batches in flight on two handles) mark their end for the
+// next call's pick_stream.
 int nk_accumulate_device(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_offs,
                          size_t n_recs, size_t n_bases, void *stream) {
   // the partials stay pending: nk_finalize's LIF (or nk_wire32) folds them,
   // nk_device_currents / nk_copy_currents fold them first
-  return accumulate(c, d_bases, d_offs, n_recs, n_bases, stream, true);
+  const int rc = accumulate(c, d_bases, d_offs, n_recs, n_bases, stream, true);
+  if (!rc) record_order(c, c->last_s);
+  return rc;
 }
 
 int nk_accumulate_device_from(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_offs,
                               size_t n_recs, size_t n_bases, size_t first_pos, void *stream) {
-  return accumulate(c, d_bases, d_offs, n_recs, n_bases, stream, true, first_pos);
+  const int rc = accumulate(c, d_bases, d_offs, n_recs, n_bases, stream, true, first_pos);
+  if (!rc) record_order(c, c->last_s);
+  return rc;
 }
 
 // ---------------------------------------------------------------------------
@@ -2268,10 +2367,7 @@ int nk_exact_adopt(nk_counter *c, const uint64_t *d_keys, const uint32_t *d_coun
     return rc;
   HIPCHK(exact_merge_pairs(d_keys, d_counts, n, end_bit, c->x_sorted.p, c->x_cs.p, c->x_uniq.p,
                            c->x_cnt.p, c->x_n.p + 1, c->x_tmp.p, c->x_tmp.n, s));
-  if (c->pool) {
-    HIPCHK(hipMemsetAsync(c->kpn.p, 0, c->pool * 4, s));
-    HIPCHK(exact_kpn(c->x_uniq.p, c->x_n.p + 1, n, c->pool, c->kpn.p, s));
-  }
+  if ((rc = table_kpn(c, c->x_uniq.p, c->x_n.p + 1, n, 1, s))) return rc;
   HIPCHK(hipStreamSynchronize(s));  // the caller may free the received buffers
   c->exact_built = true;
   c->kpn_valid = true;

@@ -19,23 +19,47 @@ constexpr int kXTile = kTile;     // 4096 positions per workgroup
 constexpr int kXBlock = kBlock;   // 256 threads
 constexpr int kXPer = kXTile / kXBlock;
 
-// exclusive scan over a 256-thread block, *total = sum
-__device__ __forceinline__ uint32_t scan256(uint32_t x, uint32_t *s_w, uint32_t *total) {
+constexpr int kXWaves = kXBlock / 64;
+static_assert(kXPer * kXWaves == 64, "one wave scans the per-(round, wave) counts");
+
+// A tile's valid keys compacted in position order (q = j * kXBlock + tid):
+// slot[j] = the key's index within the tile, *base = the tile's first index
+// in the global key array (one atomic per tile), *total = its key count.  The
+// keys are then staged in LDS and stored coalesced (each lane writing its own
+// run of keys touched 64 cache lines per store instruction: the extraction ran
+// at 1.8 TB/s, profiles/r02_s18).
+struct TileSlots {
+  uint32_t pre[kXPer * kXWaves];
+  uint32_t total;
+  unsigned long long base;
+};
+__device__ __forceinline__ void tile_slots(uint32_t ok, uint32_t (&slot)[kXPer], TileSlots &T,
+                                           unsigned long long *n_keys) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint32_t incl = x;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += y;
+  const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int j = 0; j < kXPer; ++j) {
+    const uint64_t m = __ballot((ok >> j) & 1u);
+    slot[j] = (uint32_t)__popcll(m & below);
+    if (lane == 0) T.pre[j * kXWaves + w] = (uint32_t)__popcll(m);
   }
-  if (lane == 63) s_w[w] = incl;
   __syncthreads();
-  uint32_t pre = 0, tot = 0;
-  for (int i = 0; i < kXBlock / 64; ++i) {
-    pre += i < w ? s_w[i] : 0u;
-    tot += s_w[i];
+  if (threadIdx.x < 64) {
+    const uint32_t c = T.pre[threadIdx.x];
+    uint32_t incl = c;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    T.pre[threadIdx.x] = incl - c;
+    if (threadIdx.x == 63) {
+      T.total = incl;
+      T.base = incl ? atomicAdd(n_keys, (unsigned long long)incl) : 0ull;
+    }
   }
-  *total = tot;
-  return pre + incl - x;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kXPer; ++j) slot[j] += T.pre[j * kXWaves + w];
 }
 
 // k <= 32: keys from the staged tile, exactly as the count kernels derive them
@@ -44,8 +68,8 @@ __global__ __launch_bounds__(kXBlock) void k_keys_tile(KmerInput in, int k,
                                                        uint64_t *__restrict__ keys,
                                                        unsigned long long *__restrict__ n_keys) {
   __shared__ TileLds<kXTile, !CANON> L;
-  __shared__ uint32_t s_w[kXBlock / 64];
-  __shared__ unsigned long long s_base;
+  __shared__ TileSlots T;
+  __shared__ uint64_t s_out[kXTile];
   const uint64_t tile = in.tile_base + blockIdx.x;
   const uint64_t T0 = tile * kXTile;
   stage_tile<kXTile, kXBlock, !CANON>(L, in, tile, k);
@@ -60,14 +84,13 @@ __global__ __launch_bounds__(kXBlock) void k_keys_tile(KmerInput in, int k,
     kv[j] = window_key<kXTile, !CANON, CANON>(L, q, k);
     ok |= 1u << j;
   }
-  uint32_t total;
-  const uint32_t pre = scan256((uint32_t)__popc(ok), s_w, &total);
-  if (threadIdx.x == 0) s_base = total ? atomicAdd(n_keys, (unsigned long long)total) : 0ull;
-  __syncthreads();
-  uint64_t at = s_base + pre;
+  uint32_t slot[kXPer];
+  tile_slots(ok, slot, T, n_keys);
 #pragma unroll
   for (int j = 0; j < kXPer; ++j)
-    if ((ok >> j) & 1u) keys[at++] = kv[j];
+    if ((ok >> j) & 1u) s_out[slot[j]] = kv[j];
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < T.total; i += kXBlock) keys[T.base + i] = s_out[i];
 }
 
 // k > 32 (NK_KMER_COMPAT): the reference's release-build keys, one window per
@@ -76,8 +99,8 @@ template <bool CANON>
 __global__ __launch_bounds__(kXBlock) void k_keys_compat(KmerInput in, int k,
                                                          uint64_t *__restrict__ keys,
                                                          unsigned long long *__restrict__ n_keys) {
-  __shared__ uint32_t s_w[kXBlock / 64];
-  __shared__ unsigned long long s_base;
+  __shared__ TileSlots T;
+  __shared__ uint64_t s_out[kXTile];
   const uint64_t T0 = (in.tile_base + blockIdx.x) * kXTile;
   uint64_t r = in.tile_rec[blockIdx.x];
   uint64_t kv[kXPer];
@@ -93,26 +116,26 @@ __global__ __launch_bounds__(kXBlock) void k_keys_compat(KmerInput in, int k,
     kv[j] = compat_key<CANON>(in.bases, s0, p, k);
     ok |= 1u << j;
   }
-  uint32_t total;
-  const uint32_t pre = scan256((uint32_t)__popc(ok), s_w, &total);
-  if (threadIdx.x == 0) s_base = total ? atomicAdd(n_keys, (unsigned long long)total) : 0ull;
-  __syncthreads();
-  uint64_t at = s_base + pre;
+  uint32_t slot[kXPer];
+  tile_slots(ok, slot, T, n_keys);
 #pragma unroll
   for (int j = 0; j < kXPer; ++j)
-    if ((ok >> j) & 1u) keys[at++] = kv[j];
+    if ((ok >> j) & 1u) s_out[slot[j]] = kv[j];
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < T.total; i += kXBlock) keys[T.base + i] = s_out[i];
 }
 
 // NK_KMER_128 (k <= 64): the 128-bit keys of the staged tile, exactly as the
-// 128-bit count kernels derive them (nk_tile.h window_key128)
+// 128-bit count kernels derive them (nk_tile.h window_key128); staged and
+// stored one 64-bit half at a time
 using u128 = unsigned __int128;
 template <bool CANON>
 __global__ __launch_bounds__(kXBlock) void k_keys_tile128(KmerInput in, int k,
-                                                          u128 *__restrict__ keys,
+                                                          uint64_t *__restrict__ keys2,
                                                           unsigned long long *__restrict__ n_keys) {
   __shared__ TileLds<kXTile, !CANON> L;
-  __shared__ uint32_t s_w[kXBlock / 64];
-  __shared__ unsigned long long s_base;
+  __shared__ TileSlots T;
+  __shared__ uint64_t s_out[kXTile];
   const uint64_t tile = in.tile_base + blockIdx.x;
   const uint64_t T0 = tile * kXTile;
   stage_tile<kXTile, kXBlock, !CANON>(L, in, tile, k);
@@ -123,16 +146,26 @@ __global__ __launch_bounds__(kXBlock) void k_keys_tile128(KmerInput in, int k,
     if (T0 + (uint64_t)q + (uint64_t)k > in.n_bases) continue;
     if (window_valid(L, T0, q, k, in.n_bases, in.pos_lo, in.pos_hi)) ok |= 1u << j;
   }
-  uint32_t total;
-  const uint32_t pre = scan256((uint32_t)__popc(ok), s_w, &total);
-  if (threadIdx.x == 0) s_base = total ? atomicAdd(n_keys, (unsigned long long)total) : 0ull;
-  __syncthreads();
-  uint64_t at = s_base + pre;
+  uint32_t slot[kXPer];
+  tile_slots(ok, slot, T, n_keys);
+  uint64_t hi[kXPer];
+#pragma unroll
   for (int j = 0; j < kXPer; ++j) {
+    hi[j] = 0;
     if (!((ok >> j) & 1u)) continue;
     const Key128 key = window_key128<kXTile, !CANON, CANON>(L, j * kXBlock + threadIdx.x, k);
-    keys[at++] = ((u128)key.hi << 64) | key.lo;
+    s_out[slot[j]] = key.lo;
+    hi[j] = key.hi;
   }
+  __syncthreads();
+  uint64_t *dst = keys2 + 2 * T.base;
+  for (uint32_t i = threadIdx.x; i < T.total; i += kXBlock) dst[2 * i] = s_out[i];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kXPer; ++j)
+    if ((ok >> j) & 1u) s_out[slot[j]] = hi[j];
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < T.total; i += kXBlock) dst[2 * i + 1] = s_out[i];
 }
 
 __global__ void k_kpn128(const u128 *__restrict__ uniq, const unsigned long long *__restrict__ n_uniq,
@@ -402,9 +435,29 @@ hipError_t exact_keys(const KmerInput &in, int k, int canonical, uint64_t *keys,
   return hipGetLastError();
 }
 
+// The u64 table sort: rocPRIM's onesweep radix sort.  NK_SORT_BITS (A/B
+// builds) replaces its default gfx950 config (8 bits per pass: 8 passes of
+// ~590 us over 115 M keys) with NK_SORT_BITS per pass, 512 x NK_SORT_IPT keys
+// per block.
+#ifndef NK_SORT_BITS
+#define NK_SORT_BITS 0
+#endif
+#ifndef NK_SORT_IPT
+#define NK_SORT_IPT 8
+#endif
+#if NK_SORT_BITS
+using KeySortCfg = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<512, NK_SORT_IPT>,
+                                        rocprim::kernel_config<512, NK_SORT_IPT>, NK_SORT_BITS,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+#else
+using KeySortCfg = rocprim::default_config;
+#endif
+
 size_t exact_temp_bytes(size_t n, int end_bit) {
   size_t a = 0, b = 0;
-  (void)rocprim::radix_sort_keys(nullptr, a, (const uint64_t *)nullptr, (uint64_t *)nullptr, n, 0,
+  (void)rocprim::radix_sort_keys<KeySortCfg>(nullptr, a, (const uint64_t *)nullptr, (uint64_t *)nullptr, n, 0,
                                  end_bit);
   (void)rocprim::run_length_encode(nullptr, b, (const uint64_t *)nullptr, n, (uint64_t *)nullptr,
                                    (uint32_t *)nullptr, (unsigned long long *)nullptr);
@@ -416,7 +469,7 @@ hipError_t exact_sort_rle(uint64_t *keys, uint64_t *keys_sorted, size_t n, int e
                           size_t tmp_bytes, hipStream_t s) {
   if (!n) return hipMemsetAsync(n_uniq, 0, sizeof(unsigned long long), s);
   size_t tb = tmp_bytes;
-  hipError_t e = rocprim::radix_sort_keys(tmp, tb, (const uint64_t *)keys, keys_sorted, n, 0,
+  hipError_t e = rocprim::radix_sort_keys<KeySortCfg>(tmp, tb, (const uint64_t *)keys, keys_sorted, n, 0,
                                           end_bit, s);
   if (e != hipSuccess) return e;
   tb = tmp_bytes;
@@ -600,10 +653,9 @@ hipError_t exact_keys128(const KmerInput &in, int k, int canonical, uint64_t *ke
                          unsigned long long *n_keys, hipStream_t s) {
   if (!in.n_tiles) return hipSuccess;
   if (k > 64) return hipErrorInvalidValue;
-  u128 *keys = reinterpret_cast<u128 *>(keys2);
   const dim3 g((unsigned)in.n_tiles), b(kXBlock);
-  if (canonical) hipLaunchKernelGGL(k_keys_tile128<true>, g, b, 0, s, in, k, keys, n_keys);
-  else hipLaunchKernelGGL(k_keys_tile128<false>, g, b, 0, s, in, k, keys, n_keys);
+  if (canonical) hipLaunchKernelGGL(k_keys_tile128<true>, g, b, 0, s, in, k, keys2, n_keys);
+  else hipLaunchKernelGGL(k_keys_tile128<false>, g, b, 0, s, in, k, keys2, n_keys);
   return hipGetLastError();
 }
 

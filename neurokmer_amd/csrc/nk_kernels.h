@@ -252,6 +252,13 @@ hipError_t launch_part_gen(const KmerInput &in, int k, int canonical, int km, ui
 hipError_t launch_uniq_gen(const KmerInput &in, int k, int canonical, int km, uint64_t pool,
                            const UniqArgs &u, hipStream_t s);
 hipError_t launch_split(const GenPartArgs &ga, const PartArgs &fine, hipStream_t s);
+// the exact table's kmer_per_neuron: a key array (wpk u64 words per key, *n_keys
+// of them on the device, at most max_n) hashed and partitioned like the count
+hipError_t launch_part_keys(const uint64_t *keys, const unsigned long long *n_keys, uint64_t max_n,
+                            int wpk, uint64_t pool, const GenPartArgs &ga, int wide, hipStream_t s);
+// kpn[i] = cur[i] + sum of `slices` partials (0: none); cur[i] = 0 after
+hipError_t launch_kpn_fold(const uint32_t *partials, uint32_t slices, uint64_t pool,
+                           unsigned long long *cur, uint32_t *kpn, hipStream_t s);
 hipError_t launch_bucket_hist(const PartArgs &pa, uint64_t pool, uint32_t slices,
                               uint32_t *partials, hipStream_t s);
 hipError_t launch_partials_add(const uint32_t *partials, uint32_t slices, uint64_t pool,

@@ -223,7 +223,91 @@ __global__ __launch_bounds__(kPartBlock) void k_split(GenPartArgs ga, PartArgs p
                               pa.currents);
 }
 
+// K1k: the exact table's distinct keys -> kmer_per_neuron, as a count of a key
+// array through the same partition + LDS histograms (a per-key global atomic,
+// k_kpn, runs at the memory side: 4.2 ms for 113 M keys, profiles/r02_s18).
+// Lane j of a tile takes keys T0 + j * kPartBlock + lane (coalesced loads; the
+// record order inside a bucket does not matter to a histogram).
+template <bool W128, bool WIDE>
+__global__ __launch_bounds__(kPartBlock) void k_part_keys(const uint64_t *__restrict__ keys,
+                                                          const unsigned long long *__restrict__ n_keys,
+                                                          FastMod fm, GenPartArgs ga) {
+  using S = GenShape<WIDE>;
+  __shared__ uint32_t s_cnt[S::kMaxB + 1];
+  __shared__ uint32_t s_start[S::kMaxB + 1];
+  __shared__ uint32_t s_base[S::kMaxB];
+  __shared__ uint32_t s_fit[S::kMaxB];
+  __shared__ __align__(16) typename S::Rec s_rec[S::kSlots];
+  __shared__ typename S::GMap s_gmap[S::kGroups];
+  const uint64_t n = *n_keys;
+  const uint64_t T0 = (uint64_t)blockIdx.x * kPartTile;
+  if (T0 >= n) return;  // uniform: the grid is sized for the key bound
+  const int tid = threadIdx.x;
+  const uint32_t nb = ga.n_buckets;
+  const int bb = ga.bin_bits;
+  const uint32_t omask = (uint32_t)((1ull << bb) - 1ull);
+  for (uint32_t b = tid; b <= nb; b += kPartBlock) s_cnt[b] = 0;
+  __syncthreads();
+  uint32_t E[kPer], O[kPer];
+#pragma unroll 4
+  for (int j = 0; j < kPer; ++j) {
+    const uint64_t i = T0 + (uint64_t)j * kPartBlock + (uint64_t)tid;
+    const bool ok = i < n;
+    uint64_t h = 0;
+    if (ok) h = W128 ? sip13_u128(keys[2 * i], keys[2 * i + 1]) : sip13_u64(keys[i]);
+    const uint32_t idx = (uint32_t)fastmod(h, fm);
+    const uint32_t b = ok ? (idx >> bb) : nb;
+    E[j] = (b << 16) | atomicAdd(&s_cnt[b], 1u);
+    O[j] = idx & omask;
+  }
+  sort_and_store<WIDE, kPer>(E, O, nb, s_cnt, s_start, s_base, s_fit, s_rec, s_gmap, ga.fill,
+                             ga.overflow, ga.cap, reinterpret_cast<typename S::Rec *>(ga.rec), 0,
+                             bb, ga.currents);
+}
+
+__global__ void k_kpn_fold(const uint32_t *__restrict__ partials, uint32_t slices, uint64_t pool,
+                           unsigned long long *__restrict__ cur, uint32_t *__restrict__ kpn) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < pool;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    unsigned long long s = cur[i];
+    if (s) cur[i] = 0;
+    for (uint32_t r = 0; r < slices; ++r) s += partials[(uint64_t)r * pool + i];
+    kpn[i] = (uint32_t)s;
+  }
+}
+
 // ---------------------------------------------------------------------------
+hipError_t launch_part_keys(const uint64_t *keys, const unsigned long long *n_keys, uint64_t max_n,
+                            int wpk, uint64_t pool, const GenPartArgs &ga, int wide, hipStream_t s) {
+  if (!max_n) return hipSuccess;
+  if (pool == 0 || pool > (1ull << 31) || (wpk != 1 && wpk != 2)) return hipErrorInvalidValue;
+  if (wide ? (ga.n_buckets > (uint32_t)kWideMaxBuckets || ga.bin_bits < kBinBits ||
+              ga.bin_bits - kBinBits > kMaxSplitBits)
+           : (ga.n_buckets > (uint32_t)kMaxBuckets || ga.bin_bits != kBinBits))
+    return hipErrorInvalidValue;
+  const uint64_t tiles = (max_n + kPartTile - 1) / kPartTile;
+  if (tiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  const FastMod fm = make_fastmod(pool);
+  const dim3 g((unsigned)tiles), b(kPartBlock);
+  if (wpk == 2) {
+    if (wide) hipLaunchKernelGGL((k_part_keys<true, true>), g, b, 0, s, keys, n_keys, fm, ga);
+    else hipLaunchKernelGGL((k_part_keys<true, false>), g, b, 0, s, keys, n_keys, fm, ga);
+  } else {
+    if (wide) hipLaunchKernelGGL((k_part_keys<false, true>), g, b, 0, s, keys, n_keys, fm, ga);
+    else hipLaunchKernelGGL((k_part_keys<false, false>), g, b, 0, s, keys, n_keys, fm, ga);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_kpn_fold(const uint32_t *partials, uint32_t slices, uint64_t pool,
+                           unsigned long long *cur, uint32_t *kpn, hipStream_t s) {
+  if (!pool) return hipSuccess;
+  unsigned g = (unsigned)((pool + 255) / 256);
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(k_kpn_fold, dim3(g), dim3(256), 0, s, partials, slices, pool, cur, kpn);
+  return hipGetLastError();
+}
+
 hipError_t launch_part_gen(const KmerInput &in, int k, int canonical, int km, uint64_t pool,
                            const GenPartArgs &ga, int wide, hipStream_t s) {
   if (!in.n_tiles) return hipSuccess;

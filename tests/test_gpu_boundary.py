@@ -128,3 +128,32 @@ def test_exact_table_128(k, canon, exact):
     for kk, c, p in zip(probe, cnt, pres):
         assert (int(c) if p else None) == r.get_count(kk), hex(kk)
     assert g.top_abundant_neurons(2000) == r.top_abundant_neurons(2000)
+
+
+@pytest.mark.parametrize("k,pool,canon,width", [(31, 20_000_003, True, 64), (40, 16_777_217, False, 64),
+                                                (63, 40_000_000, True, 128), (21, 3_001, True, 128)])
+def test_kmer_per_neuron_by_partition(k, pool, canon, width):
+    """kmer_per_neuron of the table: its distinct keys hashed and partitioned like
+    the count (narrow buckets, or coarse buckets + k_split past 16.7 M neurons),
+    against the oracle and against the per-key atomic kernel (NK_KPN_ATOMIC)."""
+    bases, offs = ragged_records(total=300_000, n_rate=0.005, mixed_case=True, seed=800 + k,
+                                 repeats_per_mb=20_000, motif_len=90)
+    g, r = _pair(k, pool, canon, width=width, exact=True)
+    g.process_parallel_arrays(bases, offs)
+    r.process_parallel_arrays(bases, offs)
+    kpn = g.kmer_per_neuron()
+    np.testing.assert_array_equal(kpn, r.kmer_per_neuron())
+    assert int(kpn.sum(dtype=np.int64)) == g.distinct_kmers() == r.distinct_kmers()
+    os.environ["NK_KPN_ATOMIC"] = "1"
+    try:
+        a = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, canon, kmer_width=width,
+                               exact_counts=True)
+        a.process_parallel_arrays(bases, offs)
+        np.testing.assert_array_equal(a.kmer_per_neuron(), kpn)
+    finally:
+        del os.environ["NK_KPN_ATOMIC"]
+    # a second input on the same handle: the partition's scratch is clean again
+    b2, o2 = synth.make_records(150_000, 5, seed=k)
+    g.process_parallel_arrays(b2, o2)
+    r.process_parallel_arrays(b2, o2)
+    np.testing.assert_array_equal(g.kmer_per_neuron(), r.kmer_per_neuron())
