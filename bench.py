@@ -167,7 +167,7 @@ def main() -> int:
     # rehearsal: the multi-rank step (wire all-reduce, key all-gather, merge) in
     # a 1-rank process group, to measure its overhead on a 1-GPU box
     ap.add_argument("--force-dist", action="store_true")
-    ap.add_argument("--inflight", type=int, default=None, choices=(1, 2),
+    ap.add_argument("--inflight", type=int, default=None, choices=(1, 2, 3),
                     help="batches in flight (default: 2 on one GPU, 1 across ranks): 2 "
                          "overlaps a batch's finish with the next batch's count")
     args = ap.parse_args()
@@ -295,11 +295,13 @@ def main() -> int:
                 if marks is not None:
                     marks.append(time.perf_counter())
             return
-        start(0)
+        m = inflight
+        for j in range(min(m - 1, n)):
+            start(j)
         for i in range(n):
-            if i + 1 < n:
-                start((i + 1) % 2)
-            finish(i % 2, fin_stream)
+            if i + m - 1 < n:
+                start((i + m - 1) % m)
+            finish(i % m, fin_stream)
             if marks is not None:
                 marks.append(time.perf_counter())
 
@@ -357,8 +359,9 @@ def main() -> int:
     # both handles' last batches (same input) gave the same results
     same_inflight = None
     if args.inflight > 1:
-        same_inflight = (ctrs[0].top_abundant_neurons(20) == ctrs[1].top_abundant_neurons(20) and
-                         ctrs[0].energy.total_spikes() == ctrs[1].energy.total_spikes())
+        same_inflight = all(c.top_abundant_neurons(20) == ctrs[0].top_abundant_neurons(20) and
+                            c.energy.total_spikes() == ctrs[0].energy.total_spikes()
+                            for c in ctrs[1:])
     # the same K steps one batch at a time: the step latency, and K1a's
     # duration without the other batch's finish beside it (the roofline)
     marks1 = []
@@ -368,7 +371,7 @@ def main() -> int:
     # K1a of every step of the one-at-a-time run (in-kernel stamps), and of
     # handle 1's steps in the overlapped run (the other batch's finish beside it)
     spans = ctr.count_spans(args.steps)
-    spans2 = ctrs[1].count_spans(args.steps // 2) if args.inflight > 1 else []
+    spans2 = ctrs[1].count_spans(args.steps // args.inflight) if args.inflight > 1 else []
     total_spikes = ctr.energy.total_spikes()
     # cross-check: K1a between hipEvents in 5 extra (untimed) steps
     ctr.set_stage_timing(0)
