@@ -121,7 +121,11 @@ int nk_process_file_parallel(nk_counter *c, const char *path);
  *   nk_finalize            — LIF + top-N (+ uniques of this shard's k-mers)
  * `streaming_semantics` = 1 applies process_file_streaming's LIF rule (zero
  * current neurons also step, src/spiking_hash.rs:544-659), 0 process_parallel's
- * (they are skipped, :189-191). */
+ * (they are skipped, :189-191).
+ * Calls of one handle stay ordered across streams: a call on another stream
+ * than the handle's previous one first waits for that call's work (after
+ * nk_accumulate_device: for exactly its work, recorded when it returns, so
+ * another handle's batch queued behind it is not waited for). */
 int nk_accumulate_device(nk_counter *c, const uint8_t *d_bases,
                          const uint64_t *d_rec_offsets, size_t n_recs,
                          size_t n_bases, void *stream);
