@@ -267,21 +267,26 @@ def main() -> int:
         c.reset(sh, blocking=False)
         c.accumulate_device(d_bases.data_ptr(), d_offs.data_ptr(), n_recs, bases.size, sh)
 
-    def finish(j, st):
+    def finish(j, st, between=None):
         """LIF + top-N + uniques of handle j's batch on stream st, results read
         back (the one host wait).  N > 1: RCCL over xGMI -- the currents as
         u32 while every rank's k-mers together stay below 2^31, LIF + top-N +
         this shard's top k-mers into a fixed-size all-gather segment, the union
-        merged on the device."""
+        merged on the device; `between` (the next batch's count) is enqueued
+        once the all-reduce is, so that count waits for the all-reduce only."""
         c = ctrs[j]
         if not dist_on:
+            if between is not None:
+                between()
             c.finalize(False, st.cuda_stream)
             return
         with torch.cuda.stream(st):
             if args.workload == "config5":
+                if between is not None:
+                    between()
                 nkdist.finalize_step_sliced(c, total_kmers=total_kmers)
             else:
-                nkdist.finalize_step(c, total_kmers=total_kmers)
+                nkdist.finalize_step(c, total_kmers=total_kmers, between=between)
 
     def run(n, inflight, marks=None):
         """n complete steps (count + finish of one batch each), at most
@@ -299,9 +304,8 @@ def main() -> int:
         for j in range(min(m - 1, n)):
             start(j)
         for i in range(n):
-            if i + m - 1 < n:
-                start((i + m - 1) % m)
-            finish(i % m, fin_stream)
+            nxt = (lambda h=(i + m - 1) % m: start(h)) if i + m - 1 < n else None
+            finish(i % m, fin_stream, nxt)
             if marks is not None:
                 marks.append(time.perf_counter())
 

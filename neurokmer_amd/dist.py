@@ -103,7 +103,7 @@ def allreduce_currents_(t, group=None, total_kmers=None) -> None:
 
 
 def finalize_step(ctr, group=None, total_kmers=None, cap: int = 4096,
-                  streaming: bool = False) -> None:
+                  streaming: bool = False, between=None) -> None:
     """After every rank's ctr.accumulate_device: the whole multi-GPU finish with
     ONE host synchronisation (include/neurokmer.h, nk_finalize_export):
 
@@ -118,18 +118,26 @@ def finalize_step(ctr, group=None, total_kmers=None, cap: int = 4096,
     If any rank could not export exactly (the segment headers carry the
     reasons, so every rank decides alike) all ranks redo the slow way:
     nk_finalize_redo + union_top_kmers.  With the exact k-mer table the
-    uniques come from kmer_per_neuron: plain finalize."""
+    uniques come from kmer_per_neuron: plain finalize.
+
+    between: called once the currents' all-reduce is enqueued, before the rest
+    (a caller keeping batches in flight enqueues the next batch's count there:
+    on another handle it starts when this all-reduce is done and runs beside
+    this batch's finish; bench.py --inflight 2)."""
     import torch
     import torch.distributed as dist
     if torch.cuda.current_stream().cuda_stream == 0:
         # the library reads a NULL stream as its own stream: run the step on a
         # real torch stream so the collectives and our kernels share one order
-        _on_side_stream(ctr, lambda: finalize_step(ctr, group, total_kmers, cap, streaming))
+        _on_side_stream(ctr, lambda: finalize_step(ctr, group, total_kmers, cap, streaming,
+                                                   between))
         return
     stream = torch.cuda.current_stream().cuda_stream
     if getattr(ctr, "exact_counts", False):  # (after exchange_exact_table)
         cur = _currents_view(ctr, torch.device("cuda", torch.cuda.current_device()))
         allreduce_currents_(cur, group=group, total_kmers=total_kmers)
+        if between is not None:
+            between()
         # the LIF must run after the all-reduce on the SAME stream: the
         # library's own stream would not wait for torch's collective
         ctr.finalize(streaming, stream)
@@ -150,6 +158,8 @@ def finalize_step(ctr, group=None, total_kmers=None, cap: int = 4096,
     else:
         cur = _currents_view(ctr, dev)
         allreduce_currents_(cur, group=group)
+    if between is not None:
+        between()
     wpk = 2 if getattr(ctr, "kmer_width", 64) == 128 else 1
     stride = 1 + wpk * cap
     key = ("seg", world, stride)
