@@ -253,7 +253,9 @@ def main() -> int:
     ctrs = [SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, True, device=dev_idx,
                                kmer_width=args.kmer_width) for _ in range(args.inflight)]
     ctr = ctrs[0]
-    # non-default streams: a NULL stream handle would mean the library's own
+    # non-default streams: a NULL stream handle would mean the library's own.
+    # (Count streams CU-masked to leave 8-32 CUs to the finishes slowed K1a by
+    # 13-90 %, profiles/r02_s26, r02_s27: not used.)
     count_streams = [torch.cuda.Stream(device=dev) for _ in range(args.inflight)]
     run_stream = count_streams[0]
     fin_stream = (torch.cuda.Stream(device=dev, priority=torch.cuda.Stream.priority_range()[1])
