@@ -263,11 +263,15 @@ def main() -> int:
     torch.cuda.set_stream(run_stream)
     s_handle = run_stream.cuda_stream
 
+    start_host_s = []  # host time of each start() (the enqueue of a count)
+
     def start(j):
         """Enqueue one batch's count on handle j (returns at once)."""
+        t_s = time.perf_counter()
         c, sh = ctrs[j], count_streams[j].cuda_stream
         c.reset(sh, blocking=False)
         c.accumulate_device(d_bases.data_ptr(), d_offs.data_ptr(), n_recs, bases.size, sh)
+        start_host_s.append(time.perf_counter() - t_s)
 
     def finish(j, st, between=None):
         """LIF + top-N + uniques of handle j's batch on stream st, results read
@@ -361,7 +365,11 @@ def main() -> int:
         return t_a, d
 
     marks = []
+    del start_host_s[:]
     t0, dt = timed(args.steps, args.inflight, marks)
+    start_ms = sorted(start_host_s)
+    start_ms = (round(start_ms[len(start_ms) // 2] * 1e3, 4), round(start_ms[-1] * 1e3, 4)) \
+        if start_ms else None
     # both handles' last batches (same input) gave the same results
     same_inflight = None
     if args.inflight > 1:
@@ -424,6 +432,7 @@ def main() -> int:
             "inflight": args.inflight,
             "ms_per_step_one_in_flight": round(dt1 / args.steps * 1e3, 4),
             "inflight_handles_same_results": same_inflight,
+            "start_host_ms_median_max": start_ms,
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "u64",
             "data": ("synthetic (splitmix64 i.i.d. ACGT, seed 0x4E4B4D52" +
                      ("^rank, 64x200-bp planted repeats per MB)" if args.workload != "config4"

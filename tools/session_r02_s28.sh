@@ -14,5 +14,7 @@ timeout -k 10 600 python -u bench.py > gpurun_out/s28/bench_default.log 2>&1 || 
 tail -1 gpurun_out/s28/bench_default.log | cut -c1-300
 timeout -k 10 300 python -u bench.py --inflight 1 --no-cpu-baseline --no-extras > gpurun_out/s28/bench_one_in_flight.log 2>&1 || exit $?
 tail -1 gpurun_out/s28/bench_one_in_flight.log | cut -c1-300
+timeout -k 10 300 python -u bench.py --inflight 3 --no-cpu-baseline --no-extras > gpurun_out/s28/bench_inflight3.log 2>&1 || exit $?
+for f in bench_default bench_one_in_flight bench_inflight3; do python3 -c "import json; d=json.loads(open('gpurun_out/s28/$f.log').read().strip().splitlines()[-1]); print('$f', d['value'], d['ms_per_step'], d.get('ms_per_step_one_in_flight'), d.get('start_host_ms_median_max'))"; done
 cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/s28/trace -o run -- python3 $R/bench.py --no-cpu-baseline --no-extras > $R/gpurun_out/s28/trace.log 2>&1 || exit $?
 echo done
