@@ -168,7 +168,8 @@ def main() -> int:
     # a 1-rank process group, to measure its overhead on a 1-GPU box
     ap.add_argument("--force-dist", action="store_true")
     ap.add_argument("--inflight", type=int, default=None, choices=(1, 2, 3),
-                    help="batches in flight (default: 2 on one GPU, 1 across ranks): 2 "
+                    help="batches in flight (default: 2 on one GPU, 1 across ranks and for "
+                         "config5): 2 "
                          "overlaps a batch's finish with the next batch's count")
     args = ap.parse_args()
 
@@ -198,7 +199,9 @@ def main() -> int:
         # batch's count their kernels wait for its workgroups, so the
         # overlapped step measured slower (1-rank RCCL rehearsal, 0.698 vs
         # 0.624 ms, profiles/r02_s21)
-        args.inflight = 1 if dist_on else 2
+        # config 5 (P = 256 M): its finish is a 256 M-neuron LIF + top-N pass
+        # that gains nothing beside a count (5.15 vs 5.02-5.07 ms, r02_s29)
+        args.inflight = 1 if dist_on or args.workload == "config5" else 2
     if dist_on:
         torch.cuda.set_device(dev_idx)
         if backend == "nccl":
