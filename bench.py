@@ -259,7 +259,13 @@ def main() -> int:
     # non-default streams: a NULL stream handle would mean the library's own.
     # (Count streams CU-masked to leave 8-32 CUs to the finishes slowed K1a by
     # 13-90 %, profiles/r02_s26, r02_s27: not used.)
-    count_streams = [torch.cuda.Stream(device=dev) for _ in range(args.inflight)]
+    # NK_BENCH_SHARED_COUNT_STREAM=1: all handles count on one stream (one
+    # hardware queue: counts queue back to back; the library orders each
+    # handle's finish on the end of its own count)
+    if os.environ.get("NK_BENCH_SHARED_COUNT_STREAM") == "1":
+        count_streams = [torch.cuda.Stream(device=dev)] * args.inflight
+    else:
+        count_streams = [torch.cuda.Stream(device=dev) for _ in range(args.inflight)]
     run_stream = count_streams[0]
     fin_stream = (torch.cuda.Stream(device=dev, priority=torch.cuda.Stream.priority_range()[1])
                   if args.inflight > 1 else run_stream)
