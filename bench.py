@@ -168,8 +168,8 @@ def main() -> int:
     # a 1-rank process group, to measure its overhead on a 1-GPU box
     ap.add_argument("--force-dist", action="store_true")
     ap.add_argument("--inflight", type=int, default=None, choices=(1, 2, 3),
-                    help="batches in flight (default: 2 on one GPU, 1 across ranks and for "
-                         "config5): 2 "
+                    help="batches in flight (default: 3 on one GPU, 1 across ranks and for "
+                         "config5): > 1 "
                          "overlaps a batch's finish with the next batch's count")
     args = ap.parse_args()
 
@@ -201,7 +201,7 @@ def main() -> int:
         # 0.624 ms, profiles/r02_s21)
         # config 5 (P = 256 M): its finish is a 256 M-neuron LIF + top-N pass
         # that gains nothing beside a count (5.15 vs 5.02-5.07 ms, r02_s29)
-        args.inflight = 1 if dist_on or args.workload == "config5" else 2
+        args.inflight = 1 if dist_on or args.workload == "config5" else 3
     if dist_on:
         torch.cuda.set_device(dev_idx)
         if backend == "nccl":
@@ -244,28 +244,30 @@ def main() -> int:
     d_offs = torch.from_numpy(offsets.view(np.int64)).to(dev)
     torch.cuda.synchronize()
 
-    # two handles: batch i+1's count is enqueued before batch i's finish (LIF,
-    # top-N, uniques, readback; N > 1: the collectives) is awaited.  Each
-    # handle counts on its own stream; finishes go on a high-priority stream
-    # (its own hardware queue: two same-priority torch streams were measured
-    # sharing one queue, which serialises them), so a batch's finish runs
-    # between the workgroups of the next batch's count.  The library orders a
-    # handle's calls across streams itself (pick_stream: the finish waits for
-    # the work of ITS handle's count stream only).  --inflight 1: one handle,
-    # one stream, one batch at a time.
+    # m handles (--inflight m): the counts of batches i+1 .. i+m-1 are enqueued
+    # before batch i's finish (LIF, top-N, uniques, readback; N > 1: the
+    # collectives) is awaited.  Finishes go on a high-priority stream (its own
+    # hardware queue: two same-priority torch streams were measured sharing
+    # one queue, which serialises them), so a batch's finish runs beside the
+    # next batch's count.  The library orders a handle's calls across streams
+    # itself (pick_stream: the finish waits for the end of ITS handle's count
+    # only).  --inflight 1: one handle, one stream, one batch at a time.
     ctrs = [SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, True, device=dev_idx,
                                kmer_width=args.kmer_width) for _ in range(args.inflight)]
     ctr = ctrs[0]
     # non-default streams: a NULL stream handle would mean the library's own.
     # (Count streams CU-masked to leave 8-32 CUs to the finishes slowed K1a by
     # 13-90 %, profiles/r02_s26, r02_s27: not used.)
-    # NK_BENCH_SHARED_COUNT_STREAM=1: all handles count on one stream (one
-    # hardware queue: counts queue back to back; the library orders each
-    # handle's finish on the end of its own count)
-    if os.environ.get("NK_BENCH_SHARED_COUNT_STREAM") == "1":
-        count_streams = [torch.cuda.Stream(device=dev)] * args.inflight
-    else:
+    # All handles count on ONE stream: one hardware queue, so the counts queue
+    # back to back and the count queue never idles while a finish is awaited
+    # (the library orders each handle's finish on the end of its own count).
+    # A stream per handle measured slower with 3 in flight: the third count's
+    # queue was not served until the finish queue went idle (0.529-0.537 vs
+    # 0.507-0.514 ms, profiles/r02_s31; NK_BENCH_COUNT_STREAM_PER_HANDLE=1).
+    if os.environ.get("NK_BENCH_COUNT_STREAM_PER_HANDLE") == "1":
         count_streams = [torch.cuda.Stream(device=dev) for _ in range(args.inflight)]
+    else:
+        count_streams = [torch.cuda.Stream(device=dev)] * args.inflight
     run_stream = count_streams[0]
     fin_stream = (torch.cuda.Stream(device=dev, priority=torch.cuda.Stream.priority_range()[1])
                   if args.inflight > 1 else run_stream)
