@@ -167,7 +167,7 @@ def main() -> int:
     # rehearsal: the multi-rank step (wire all-reduce, key all-gather, merge) in
     # a 1-rank process group, to measure its overhead on a 1-GPU box
     ap.add_argument("--force-dist", action="store_true")
-    ap.add_argument("--inflight", type=int, default=None, choices=(1, 2, 3),
+    ap.add_argument("--inflight", type=int, default=None, choices=(1, 2, 3, 4),
                     help="batches in flight (default: 3 on one GPU, 1 across ranks and for "
                          "config5): > 1 "
                          "overlaps a batch's finish with the next batch's count")
