@@ -23,6 +23,11 @@
 #include "nk_reader.h"
 #include "nk_kernels.h"
 
+// K1b workgroups per batch (one 128 KiB-LDS workgroup per CU: one round on 256 CUs)
+#ifndef NK_K1B_WGS
+#define NK_K1B_WGS 256
+#endif
+
 using namespace nk;
 
 namespace {
@@ -569,7 +574,7 @@ static int table_kpn(nk_counter *c, const uint64_t *uniq, const unsigned long lo
     cap = max_n / B * 5 / 4 + kPartTile;
   }
   cap = (cap + 63) & ~63ull;
-  const uint32_t slices = (uint32_t)std::max<uint64_t>(1, 256 / B);
+  const uint32_t slices = (uint32_t)std::max<uint64_t>(1, NK_K1B_WGS / B);
   // xk_cur is zero between calls (k_kpn_fold clears what it read) unless it was
   // (re)allocated (its size grows) or a call failed half-way (xk_cur_zeroed is
   // set again only once the fold is enqueued)
@@ -757,7 +762,7 @@ static int plan_count(nk_counter *c, uint64_t est_bases, uint64_t slack, uint64_
   }
   cap = (cap + 63) & ~63ull;
   // one round of 1-per-CU workgroups (128 KiB LDS each) on 256 CUs
-  cp.slices = (uint32_t)std::max<uint64_t>(1, 256 / B);
+  cp.slices = (uint32_t)std::max<uint64_t>(1, NK_K1B_WGS / B);
   if ((rc = c->p_off.ensure(B * cap)) || (rc = c->p_fill.ensure(B)) || (rc = c->p_over.ensure(B)) ||
       ((cp.path == CountPath::Part || cp.slices > 1) && (rc = c->partials.ensure(cp.slices * P))))
     return rc;
