@@ -47,6 +47,7 @@ Rank 0 at N=1 adds (config2):
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import socket
@@ -157,6 +158,8 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip end_to_end and the exact_counts step (rank 0, N=1)")
+    ap.add_argument("--no-parity-ranks", action="store_true",
+                    help="N > 1: skip the check of the N-rank result against one GPU")
     ap.add_argument("--settle", type=float, default=0.25,
                     help="seconds of untimed steps after the warmup (GPU clock settle)")
     # side measurements only (the metric is k=31, pool 2M)
@@ -167,6 +170,10 @@ def main() -> int:
     # rehearsal: the multi-rank step (wire all-reduce, key all-gather, merge) in
     # a 1-rank process group, to measure its overhead on a 1-GPU box
     ap.add_argument("--force-dist", action="store_true")
+    # N > 1 over RCCL: the finish runs inside the library (nk_finalize_dist, its
+    # own communicator) unless --dist-python drives it from Python with torch's
+    # collectives between the library calls (the round-2 protocol, for A/B)
+    ap.add_argument("--dist-python", action="store_true")
     ap.add_argument("--inflight", type=int, default=None, choices=(1, 2, 3, 4),
                     help="batches in flight (default: 3 on one GPU, 1 across ranks and for "
                          "config5): > 1 "
@@ -203,6 +210,12 @@ def main() -> int:
         # that gains nothing beside a count (5.15 vs 5.02-5.07 ms, r02_s29)
         args.inflight = 1 if dist_on or args.workload == "config5" else 3
     if dist_on:
+        if "RANK" not in os.environ:  # --force-dist without a launcher: a 1-rank group
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
+                                  MASTER_ADDR="127.0.0.1",
+                                  MASTER_PORT=str(sk.getsockname()[1]))
         torch.cuda.set_device(dev_idx)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
@@ -213,6 +226,8 @@ def main() -> int:
     from neurokmer_amd import SpikingKmerCounter, synth
     from neurokmer_amd import dist as nkdist
     from neurokmer_amd.counter import diag_hash_ms
+    comm = nkdist.Comm(device=dev_idx) if dist_on and backend == "nccl" and not args.dist_python \
+        else None
 
     # ---- this rank's input (resident in HBM) -------------------------------
     if args.workload in ("config2", "config5"):
@@ -301,9 +316,9 @@ def main() -> int:
             if args.workload == "config5":
                 if between is not None:
                     between()
-                nkdist.finalize_step_sliced(c, total_kmers=total_kmers)
+                nkdist.finalize_step_sliced(c, total_kmers=total_kmers, comm=comm)
             else:
-                nkdist.finalize_step(c, total_kmers=total_kmers, between=between)
+                nkdist.finalize_step(c, total_kmers=total_kmers, between=between, comm=comm)
 
     def run(n, inflight, marks=None):
         """n complete steps (count + finish of one batch each), at most
@@ -406,6 +421,13 @@ def main() -> int:
     ev_ms = [x for x in ctr.count_history(5) if x == x and x > 0]
     stages = ctr.last_timings()
     ctr.set_stage_timing(timed_level)
+    # N > 1: the N-rank result against one GPU counting every rank's shard
+    pr = None
+    if world > 1 and not args.no_parity_ranks:
+        log("parity_ranks: the union of every rank's input on rank 0's GPU")
+        pr = parity_ranks(args, ctr, world, rank, dev_idx, nkdist, SpikingKmerCounter, synth,
+                          total_kmers)
+        dist.barrier()
 
     if rank == 0:
         ms_step = dt / args.steps * 1e3
@@ -452,7 +474,10 @@ def main() -> int:
                        "pool_size": pool, "bases_rank0": int(bases.size), "records_rank0": n_recs,
                        "kmers_rank0": nk_rank, "kmers_total": total_kmers,
                        "parallelism": f"dp{world}" + (f" (rehearsal: {world} ranks on {ndev} GPU, "
-                                                      f"{backend})" if shared else "")},
+                                                      f"{backend})" if shared else ""),
+                       "collectives": ("in-library RCCL (nk_finalize_dist)" if comm is not None
+                                       else (f"torch.distributed {backend} from Python" if dist_on
+                                             else None))},
             "roofline": {"bound": bound, "kernel": "k_part<canonical> (K1a)",
                          "achieved": round(achieved / 1e9, 2), "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": round(hbm_frac, 4),
@@ -469,15 +494,84 @@ def main() -> int:
             "k1a_ms_steps_overlapped": [round(x, 4) for x in spans2],
             "total_spikes": total_spikes,
         }
+        if pr is not None:
+            out["parity_ranks"] = pr
         if world == 1 and args.workload == "config2" and args.kmer_width == 64:
             out.update(extras(args, ctr, bases, offsets, nk_rank, d_bases, d_offs, s_handle,
                               dev_idx, SpikingKmerCounter, synth))
         print(json.dumps(out), flush=True)
     for c in ctrs:
         c.close()
+    if comm is not None:
+        comm.close()
     if dist_on:
         dist.destroy_process_group()
     return 0
+
+
+def parity_ranks(args, ctr, world, rank, dev_idx, nkdist, Counter, synth, total_kmers):
+    """N > 1 (collective; the result on rank 0): rank 0 regenerates EVERY rank's
+    input, counts their union in ONE process call on its own GPU, and compares
+    the N-rank step's final state with it bit for bit.  The reference sums the
+    per-record currents (src/spiking_hash.rs:145-154), so one call over all
+    records is the N-rank answer (bit-identical currents at 1,
+    2, 4 and 8 GPUs).  Pool-sliced state (config5) is gathered first."""
+    import torch
+    st = nkdist.gather_state(ctr) if args.workload == "config5" else None
+    if rank != 0:
+        return None
+    k, pool = args.k, args.pool
+    t0 = time.perf_counter()
+    if args.workload == "config4":
+        T = args.total_bases
+        n_rec = max(1, -(-T // REC_LEN4))
+        offs = np.minimum(np.arange(n_rec + 1, dtype=np.int64) * REC_LEN4, T).astype(np.uint64)
+        bases = synth.random_bases(T, seed=synth.SEED, start=0)
+    else:
+        parts, offl, at = [], [np.zeros(1, np.uint64)], 0
+        for r in range(world):
+            b, o = synth.make_records(args.bases, RECS, seed=synth.SEED ^ (r * 0x9E37),
+                                      repeats_per_mb=64, motif_len=200)
+            parts.append(b)
+            offl.append(o[1:] + np.uint64(at))
+            at += b.size
+        bases, offs = np.concatenate(parts), np.concatenate(offl)
+        del parts
+    gen_s = time.perf_counter() - t0
+    dev = torch.device("cuda", dev_idx)
+    d_b = torch.from_numpy(np.concatenate([bases, np.zeros(16, np.uint8)])).to(dev)
+    d_o = torch.from_numpy(offs.view(np.int64)).to(dev)
+    torch.cuda.synchronize()
+    g = Counter(k, 1.0, 0.95, 2, 1.0, pool, True, device=dev_idx, kmer_width=args.kmer_width)
+    g.process_parallel_device(d_b.data_ptr(), d_o.data_ptr(), offs.size - 1, bases.size)
+    if st is None:
+        st = {"currents": ctr.currents(), "spike_counts": ctr.spike_counts(),
+              "voltages": ctr.voltages(), "refractory": ctr.refractory()}
+    one = {"currents": g.currents(), "spike_counts": g.spike_counts(),
+           "voltages": g.voltages(), "refractory": g.refractory()}
+    top_n, top_1 = ctr.top_abundant_neurons(20), g.top_abundant_neurons(20)
+    # every step starts from a reset pool: the spike counts are the last step's
+    spikes_n, spikes_1 = int(st["spike_counts"].sum(dtype=np.uint64)), g.energy.total_spikes()
+    out = {"method": (f"rank 0 regenerated all {world} ranks' inputs ({bases.size:,} bases, "
+                      f"{offs.size - 1} records) and ran ONE process_parallel over them on its GPU; "
+                      "compared with the N-rank step's final state"),
+           "currents": bool(np.array_equal(st["currents"], one["currents"])),
+           "spike_counts": bool(np.array_equal(st["spike_counts"], one["spike_counts"])),
+           "voltages_bitwise": bool(np.array_equal(st["voltages"].view(np.uint32),
+                                                   one["voltages"].view(np.uint32))),
+           "refractory": bool(np.array_equal(st["refractory"], one["refractory"])),
+           "top20_with_uniques": top_n == top_1,
+           "total_spikes": [spikes_n, spikes_1],
+           "sum_currents": [int(st["currents"].sum(dtype=np.uint64)), int(total_kmers)],
+           "currents_sha1": hashlib.sha1(st["currents"].tobytes()).hexdigest()[:16],
+           "seconds": round(time.perf_counter() - t0, 2), "generate_s": round(gen_s, 2)}
+    out["all_equal"] = bool(out["currents"] and out["spike_counts"] and out["voltages_bitwise"]
+                            and out["refractory"] and out["top20_with_uniques"]
+                            and spikes_n == spikes_1
+                            and out["sum_currents"][0] == out["sum_currents"][1])
+    g.close()
+    del d_b, d_o
+    return out
 
 
 def extras(args, ctr, bases, offsets, nk, d_bases, d_offs, s_handle, dev_idx, Counter, synth):

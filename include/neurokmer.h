@@ -176,12 +176,45 @@ int nk_finalize_redo(nk_counter *c, void *stream);
  *   <caller: the union of the shards' keys — nk_top_kmers_padded /
  *                         nk_merge_top_kmers_padded, as after nk_finalize>
  * Afterwards v / refractory / spike counts / currents are authoritative on
- * [lo, hi) only (the other ranks own the rest).  Replaces the reference's
+ * [lo, hi) only (the other ranks own the rest): until nk_reset, the calls that
+ * run the LIF or read the whole pool (nk_finalize, nk_finalize_export, the
+ * process calls, nk_process_sequence, nk_simulate_spikes_auto and rows past
+ * top_n in nk_top_abundant_neurons) return NK_E_UNSUPPORTED; further
+ * accumulate + nk_finalize_slice steps are allowed.  Replaces the reference's
  * single-process pool (src/spiking_hash.rs:49-53,97,186-200). */
 int nk_finalize_slice(nk_counter *c, int streaming_semantics, const void *d_slice, int slice_bits,
                       size_t lo, size_t hi, uint64_t *d_seg, size_t seg_rows, void *stream);
 int nk_adopt_slices(nk_counter *c, const uint64_t *d_all, size_t world, size_t stride,
                     void *stream);
+/* ---- multi-GPU step with the collectives inside the library ---------------
+ * One communicator per rank (RCCL over xGMI; one process per GPU): rank 0
+ * makes an id, the caller broadcasts it (e.g. torch.distributed), every rank
+ * builds its communicator from it.  Replaces the reference's single-process
+ * rayon reduce of the currents (src/spiking_hash.rs:145-154) across GPUs. */
+#define NK_COMM_ID_BYTES 128
+typedef struct nk_comm nk_comm;
+int nk_comm_unique_id(uint8_t id[NK_COMM_ID_BYTES]);
+nk_comm *nk_comm_new(const uint8_t id[NK_COMM_ID_BYTES], int world, int rank, int device);
+void nk_comm_free(nk_comm *m);
+/* After nk_accumulate_device(_from) on every rank: the whole multi-GPU finish
+ * enqueued on `stream` with no host code between the steps (the same protocol
+ * as nk_wire32 .. nk_merge_export above, the all-reduce and all-gather issued
+ * by the library):
+ *   u32 wire + all-reduce (u64 currents when total_kmers >= 2^31), LIF + top-N
+ *   + this shard's top k-mers into a segment of `cap` keys, all-gather of the
+ *   segments, their union -> uniques column, one host wait; a redo (full set,
+ *   overflowed bucket, truncated segment: every rank sees the same headers)
+ *   takes the blocking exchange, still inside.
+ * total_kmers: an upper bound of all ranks' k-mers together (the same on
+ * every rank).  With an adopted multi-GPU exact table (nk_exact_adopt) the
+ * currents are all-reduced as u64 and the uniques come from kmer_per_neuron. */
+int nk_finalize_dist(nk_counter *c, nk_comm *m, int streaming_semantics, uint64_t total_kmers,
+                     size_t cap, void *stream);
+/* The pool-sliced finish (nk_finalize_slice / nk_adopt_slices) with its
+ * reduce-scatter, all-gather and the top k-mer union inside the library. */
+int nk_finalize_sliced_dist(nk_counter *c, nk_comm *m, int streaming_semantics,
+                            uint64_t total_kmers, size_t cap, void *stream);
+
 /* nk_accumulate_device counting only the windows that start at or after
  * first_pos (bases before it are context: a shard cut inside a record of a
  * k > 32 NK_KMER_COMPAT input keeps a 32-base warm-up, after which the
@@ -251,8 +284,22 @@ int nk_get_counts128(nk_counter *c, const uint64_t *kmers2, size_t n, uint32_t *
 /* Number of distinct k-mers in the table (the reference's counts.len()). */
 long nk_distinct_kmers(nk_counter *c);
 /* The full `kmer_per_neuron` (src/spiking_hash.rs:28,167-172,262-267): out[i]
- * for every neuron i < pool (n must equal pool_size).  Needs exact_counts. */
+ * for every neuron i < pool (n must equal pool_size).  The table: see
+ * nk_opts.exact_counts (built with every call, or on demand from the last
+ * input the handle holds). */
 int nk_copy_kmer_per_neuron(nk_counter *c, uint32_t *out, size_t n);
+
+/* SpikingKmerCounter::simulate_spikes_auto(&mut self) — src/spiking_hash.rs:
+ * 697-714.  On x86-64 with AVX2 (the reference's target and an MI355X node's
+ * host) that is simulate_spikes_simd (:544-659): `steps` LifNeuron updates of
+ * EVERY neuron (zero currents included) from the currents the counter holds
+ * (the last process call's; zero after process_sequence), spikes added to the
+ * neurons' counts and the energy tracker; steps == 0 does nothing.  The top
+ * rows are re-selected; their uniques column is kmer_per_neuron when the handle
+ * holds the table, else the distinct k-mers of the last input (device input
+ * passed by pointer must still be resident, as for nk_finalize).
+ * NK_E_UNSUPPORTED after nk_finalize_slice (sharded state) until nk_reset. */
+int nk_simulate_spikes_auto(nk_counter *c);
 
 /* Multi-GPU exact table (hash partition + all-to-all), after
  * an accumulate/process call with exact_counts on every rank (one process per

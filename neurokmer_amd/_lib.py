@@ -45,7 +45,8 @@ EXPORTS = (
     "nk_willshaw_stored", "nk_assoc_new", "nk_assoc_free", "nk_assoc_pattern_size",
     "nk_assoc_store_kmers", "nk_assoc_find_similar",
     "nk_exact_owner", "nk_exact_partition", "nk_exact_adopt", "nk_device_kmer_per_neuron",
-    "nk_set_stage_timing", "nk_diag_hash_ms", "nk_count_spans",
+    "nk_set_stage_timing", "nk_diag_hash_ms", "nk_count_spans", "nk_simulate_spikes_auto",
+    "nk_comm_unique_id", "nk_comm_new", "nk_comm_free", "nk_finalize_dist", "nk_finalize_sliced_dist",
     "nk_last_error",
     "nk_version",
 )
@@ -155,6 +156,12 @@ def load(share_torch: bool = True):
         "nk_finalize_export": (C.c_int, [vp, C.c_int, vp, vp, sz, vp]),
         "nk_merge_export": (C.c_int, [vp, vp, sz, sz, sz, P(C.c_int), vp]),
         "nk_finalize_redo": (C.c_int, [vp, vp]),
+        "nk_simulate_spikes_auto": (C.c_int, [vp]),
+        "nk_comm_unique_id": (C.c_int, [vp]),
+        "nk_comm_new": (vp, [vp, C.c_int, C.c_int, C.c_int]),
+        "nk_comm_free": (None, [vp]),
+        "nk_finalize_dist": (C.c_int, [vp, vp, C.c_int, u64, sz, vp]),
+        "nk_finalize_sliced_dist": (C.c_int, [vp, vp, C.c_int, u64, sz, vp]),
         "nk_last_error": (C.c_char_p, []),
         "nk_version": (C.c_char_p, []),
     }

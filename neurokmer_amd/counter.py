@@ -227,6 +227,12 @@ class SpikingKmerCounter:
         check(self._L.nk_process_sequence(self._h, buf.ctypes.data if buf.size else None,
                                           buf.size))
 
+    def simulate_spikes_auto(self) -> None:
+        """src/spiking_hash.rs:697-714 (AVX2 branch, :544-659): `steps` LIF
+        updates of every neuron from the held currents; spikes and energy add
+        to the totals."""
+        check(self._L.nk_simulate_spikes_auto(self._h))
+
     def get_counts(self, kmers) -> tuple:
         """Batched get_count: -> (counts u32[n], present bool[n])."""
         q = np.ascontiguousarray(kmers, dtype=np.uint64)

@@ -100,13 +100,16 @@ __device__ int kmer_bits(uint64_t kmer, uint32_t n, uint32_t *bits) {
   return m;
 }
 
-// store: W[a] |= bit b for every pair of the listed bits
+// store: W[a] |= bit b for every pair of the listed bits (grid-stride: a dense
+// pattern of n = 2^20 bits has 2^40 pairs, more than a 32-bit grid holds)
 __global__ void k_ws_store_bits(uint32_t *__restrict__ W, uint32_t words,
                                 const uint32_t *__restrict__ idx, uint32_t m) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (uint64_t)m * m) return;
-  const uint32_t a = idx[t / m], b = idx[t % m];
-  atomicOr(&W[(uint64_t)a * words + (b >> 5)], 1u << (b & 31));
+  const uint64_t pairs = (uint64_t)m * m;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < pairs;
+       t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t a = idx[t / m], b = idx[t % m];
+    atomicOr(&W[(uint64_t)a * words + (b >> 5)], 1u << (b & 31));
+  }
 }
 
 // store_kmer of a batch: each thread one k-mer's pattern pairs
@@ -287,7 +290,8 @@ int nk_willshaw_store(nk_willshaw *w, const uint8_t *pattern, size_t len) {
   if (!on.empty()) {
     AS_CHK(hipMemcpyAsync(w->idx, on.data(), on.size() * 4, hipMemcpyHostToDevice, w->s));
     const uint64_t pairs = (uint64_t)on.size() * on.size();
-    hipLaunchKernelGGL(k_ws_store_bits, dim3(grid_of(pairs, 256)), dim3(256), 0, w->s, w->W,
+    const unsigned grid = (unsigned)std::min<uint64_t>((pairs + 255) / 256, 1u << 20);
+    hipLaunchKernelGGL(k_ws_store_bits, dim3(grid), dim3(256), 0, w->s, w->W,
                        w->words, w->idx, (uint32_t)on.size());
     AS_CHK(hipGetLastError());
     AS_CHK(hipStreamSynchronize(w->s));  // `on` is host memory the copy reads

@@ -218,6 +218,10 @@ struct nk_counter {
   // process_sequence) from that input, while it is still resident
   bool x_lazy = false;              // the table is the last input's, not built yet
   bool slice_ready = false;         // nk_finalize_slice ran; nk_adopt_slices next
+  // since nk_finalize_slice the neuron state is authoritative on this rank's
+  // slice only: whole-pool readers and LIF passes are refused until nk_reset
+  bool sliced = false;
+  uint64_t max_sc = 0;              // largest spike count of the pool (last LIF readback)
   bool input_owned = false;         // last_in is the handle's own copy (host/file entry points)
   // top_abundant_neurons(n) past the rows the last call selected
   DevBuf<uint64_t> rk_keys;         // [2P]: keys | sorted keys
@@ -319,6 +323,19 @@ static int zero_state_on(nk_counter *c, hipStream_t) {
   c->d_bound = 0;
   c->kpn_valid = false;
   c->x_lazy = false;
+  c->sliced = false;
+  c->max_sc = 0;
+  return NK_OK;
+}
+
+// LIF passes and readers of the whole pool need the whole pool's state on this
+// handle: not after the pool-sliced finish (nk_finalize_slice), which leaves a
+// rank authoritative on its slice only, until nk_reset
+static int whole_pool(nk_counter *c) {
+  if (c->sliced)
+    return fail(NK_E_UNSUPPORTED,
+                "the neuron state is sharded across ranks since nk_finalize_slice (this rank "
+                "holds its slice only): nk_reset first, or gather the state");
   return NK_OK;
 }
 
@@ -379,6 +396,25 @@ static int copy_out(nk_counter *c, const DevBuf<T> &b, T *out, size_t n) {
 
 // error text for the other translation units of the library (nk_assoc.hip)
 int nk_fail_msg(int code, const char *msg) { return fail(code, "%s", msg); }
+
+// nk_internal.h: what the multi-GPU driver (nk_dist.cpp) reads of a handle
+namespace nk {
+uint64_t counter_rows(const nk_counter *c) { return std::min<uint64_t>(c->opts.top_n, c->pool); }
+int counter_key_words(const nk_counter *c) { return c->w128 ? 2 : 1; }
+bool counter_kpn_global(const nk_counter *c) {
+  return c->opts.exact_counts && c->exact_built && c->kpn_global;
+}
+uint64_t *counter_currents_on(nk_counter *c, hipStream_t stream) {
+  if (c->cur_in_wire) {
+    fail(NK_E_INVALID, "the currents are in the wire vector until nk_finalize_export");
+    return nullptr;
+  }
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  if (materialize(c, true, s) || fold_pending(c, s)) return nullptr;
+  return c->cur.p;
+}
+}  // namespace nk
 
 extern "C" {
 
@@ -705,6 +741,23 @@ static bool atomic_forced() {
   return e && atoi(e) != 0;
 }
 
+// Positions counted per partition launch.  An input up to this size keeps its
+// records (4-5 B per k-mer) for the uniques scan; a larger one is counted in
+// batches of this many positions whose records are histogrammed and dropped
+// batch by batch (the arena is O(batch), not O(input): a config-4 shard of
+// 12.5 Gbases needs ~11 GB instead of ~62 GB) and the top rows' uniques come
+// from a rescan of the input.  NK_COUNT_CHUNK (tests) sets it, rounded to
+// whole partition tiles.
+#ifndef NK_COUNT_CHUNK_DEFAULT
+#define NK_COUNT_CHUNK_DEFAULT (1ull << 31)
+#endif
+static uint64_t count_chunk() {
+  const char *e = getenv("NK_COUNT_CHUNK");
+  uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
+  if (!v) v = NK_COUNT_CHUNK_DEFAULT;
+  return std::max<uint64_t>(kPartTile, v / kPartTile * kPartTile);
+}
+
 // Sizes the buffers for a batch of about est_bases bases (slack: extra
 // records per bucket region; max_segs: Part's descriptors per bucket) and
 // lists the arrays to zero before the first batch.
@@ -811,6 +864,23 @@ static hipError_t gen_count(nk_counter *c, const CountPlan &cp, const KmerInput 
   return launch_split(cp.ga, cp.pa, s);
 }
 
+// One batch whose records are not kept (Gen/Wide always; Part past
+// count_chunk()): count, histogram into the currents, empty the regions for
+// the next batch.
+static hipError_t batch_count(nk_counter *c, const CountPlan &cp, const KmerInput &in, hipStream_t s) {
+  hipError_t e = cp.path == CountPath::Part
+                     ? launch_part(in, (int)c->k, c->canonical, c->pool, cp.pa, s)
+                     : gen_count(c, cp, in, s);
+  if (e == hipSuccess) e = gen_hist(c, cp, false, s);
+  if (e != hipSuccess) return e;
+  ZeroList z{};
+  z.ptr[z.n] = cp.pa.fill; z.bytes[z.n++] = (uint64_t)cp.pa.n_buckets * 8;
+  if (cp.path == CountPath::Wide) {
+    z.ptr[z.n] = cp.ga.fill; z.bytes[z.n++] = (uint64_t)cp.ga.n_buckets * 8;
+  }
+  return launch_zero(z, s);
+}
+
 // defer_partials: leave K1c (currents += partials) to the LIF kernel of the
 // same process call instead of a separate pass
 static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_offs,
@@ -839,13 +909,56 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
   z.ptr[z.n] = c->cur.p; z.bytes[z.n++] = c->pool * 8;
   CountPlan cp;
   // bucket regions: 1.25x the fair share + one tile of slack (overflow is
-  // still exact: the excess is counted with direct atomics)
-  int rc = plan_count(c, n_bases, kPartTile, n_tiles_for(n_bases, kPartTile), cp, z);
+  // still exact: the excess is counted with direct atomics); past
+  // count_chunk() positions the regions hold one batch at a time
+  const uint64_t chunk = count_chunk();
+  const uint64_t est = std::min<uint64_t>(n_bases, chunk);
+  int rc = plan_count(c, est, kPartTile, n_tiles_for(est, kPartTile), cp, z);
   if (rc) return rc;
   in.n_tiles = n_tiles_for(n_bases, cp.tile);
-  if ((rc = c->tile_rec.ensure(std::max<uint64_t>(in.n_tiles, 1)))) return rc;
+  const bool batched = cp.path != CountPath::Atomic && n_bases > chunk;
+  const uint64_t batch_tiles = chunk / kPartTile;  // cp.tile == kPartTile on the partitioned paths
+  if ((rc = c->tile_rec.ensure(std::max<uint64_t>(batched ? batch_tiles : in.n_tiles, 1)))) return rc;
   in.tile_rec = c->tile_rec.p;
   const bool counted = cp.path != CountPath::Atomic && in.n_tiles > 0;
+  if (count_timing(c)) {  // level 2 records no count-kernel events
+    const int slot = (int)(c->cnt_calls++ % nk_counter::kCountRing);
+    c->ev[1] = c->cnt_ev[slot][0];
+    c->ev[2] = c->cnt_ev[slot][1];
+  }
+  if (batched) {
+    // prep (the zero list) with the first batch's tile index, then batch by
+    // batch; the records are dropped, so the uniques pass rescans the input
+    if (defer_partials) {
+      z.ptr[z.n] = c->hist.p;  z.bytes[z.n++] = kHistBins * kHistCopies * 4;
+      z.ptr[z.n] = c->stats.p; z.bytes[z.n++] = 16;
+      c->lif_zeroed = true;
+    }
+    HIPCHK(mark(c, 0, s));
+    for (uint64_t t0 = 0; t0 < in.n_tiles; t0 += batch_tiles) {
+      KmerInput bi = in;
+      bi.tile_base = t0;
+      bi.n_tiles = std::min<uint64_t>(batch_tiles, in.n_tiles - t0);
+      if (t0 == 0) {
+        HIPCHK(launch_prep(bi, cp.tile, c->tile_rec.p, z, s));
+        HIPCHK(mark(c, 1, s));
+      } else {
+        HIPCHK(launch_tile_rec(bi, cp.tile, c->tile_rec.p, s));
+      }
+      HIPCHK(batch_count(c, cp, bi, s));
+    }
+    HIPCHK(mark(c, 2, s));
+    c->cur_fresh = false;
+    c->part_used = false;
+    c->gen_km = cp.path == CountPath::Part ? -1 : cp.km;
+    c->pend_slices = 0;
+    HIPCHK(mark(c, 3, s));
+    c->last_in = in;
+    c->have_input = true;
+    c->top_valid = false;
+    c->input_owned = d_bases == c->in_bases.p;
+    return table_for_input(c, in, s);
+  }
   c->part_used = counted && cp.path == CountPath::Part;
   c->gen_km = (cp.path == CountPath::Gen || cp.path == CountPath::Wide) ? cp.km : -1;
   if (cp.path == CountPath::Part && c->set_dirty && !c->w128 && z.n < kZeroMax) {
@@ -860,11 +973,6 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
     z.ptr[z.n] = c->hist.p;  z.bytes[z.n++] = kHistBins * kHistCopies * 4;
     z.ptr[z.n] = c->stats.p; z.bytes[z.n++] = 16;
     c->lif_zeroed = true;
-  }
-  if (count_timing(c)) {  // level 2 records no count-kernel events
-    const int slot = (int)(c->cnt_calls++ % nk_counter::kCountRing);
-    c->ev[1] = c->cnt_ev[slot][0];
-    c->ev[2] = c->cnt_ev[slot][1];
   }
   unsigned long long *span = nullptr;
   if (c->part_used) {
@@ -1157,7 +1265,8 @@ static bool top_fused(const nk_counter *c, uint64_t want) {
 
 static int lif_top_uniques(nk_counter *c, int streaming, bool use_kpn, hipStream_t s,
                            const uint32_t *wire = nullptr) {
-  int rc;
+  int rc = whole_pool(c);
+  if (rc) return rc;
   c->top_keys_ready = false;
   const uint64_t want = std::min<uint64_t>(c->opts.top_n, c->pool);
   const bool uniq = want && c->have_input && c->last_in.n_tiles;
@@ -1214,6 +1323,7 @@ static int settle_top(nk_counter *c, uint64_t want, bool uniq, bool use_kpn, boo
   if (account) {
     c->total_spikes += h->stats[0];
     c->total_energy += h->stats[0] * cost_fixed(c->cost);
+    c->max_sc = h->stats[1];
   }
   if (want && h->st.refine) {  // spike counts >= 4095: exact radix refine, redo
     TopState st = h->st;
@@ -1316,8 +1426,44 @@ int nk_finalize(nk_counter *c, int streaming, void *stream) {
   return NK_OK;
 }
 
+// SpikingKmerCounter::simulate_spikes_auto (src/spiking_hash.rs:697-714).  On
+// x86-64 with AVX2 (the reference's target, and the host of an MI355X node) it
+// is simulate_spikes_simd (:544-659): `steps` LifNeuron updates of EVERY neuron,
+// zero currents included, from the currents the counter holds (neuron_currents:
+// the last process call's, :175/:464; zero after process_sequence, :271); the
+// spikes go to the neurons' counts and the energy tracker; steps == 0 returns
+// before touching anything (:549-551).  The same closed-form LIF kernel as a
+// process call with the streaming rule, then the top rows again: their uniques
+// column is kmer_per_neuron when the handle holds the table (exact_counts,
+// process_sequence), else the distinct k-mers of the last input (which must
+// still be resident, as for nk_finalize), else 0 (no input since new/reset).
+int nk_simulate_spikes_auto(nk_counter *c) {
+  if (!c) return fail(NK_E_INVALID, "null counter");
+  int rc = whole_pool(c);
+  if (rc) return rc;
+  if (c->cur_in_wire)
+    return fail(NK_E_INVALID, "the currents are in the wire vector until nk_finalize_export");
+  if (c->steps == 0 || c->pool == 0) return NK_OK;
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick_stream(c, nullptr);
+  HIPCHK(mark(c, 7, s));
+  if (c->kpn_valid) {
+    const uint64_t want = std::min<uint64_t>(c->opts.top_n, c->pool);
+    const bool fused = top_fused(c, want);
+    if ((rc = enqueue_lif(c, 1, fused ? (uint32_t)want : 0u, false, s))) return rc;
+    HIPCHK(mark(c, 4, s));
+    if ((rc = finish_top(c, want, fused, want != 0, true, s))) return rc;
+  } else if ((rc = lif_top_uniques(c, 1, false, s))) {
+    return rc;
+  }
+  c->top_valid = true;
+  collect_timings(c, false);
+  return NK_OK;
+}
+
 static int process_device(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_offs,
                           size_t n_recs, size_t n_bases, void *stream, int streaming) {
+  if (int rc0 = whole_pool(c)) return rc0;
   int rc = accumulate(c, d_bases, d_offs, n_recs, n_bases, stream, true);
   if (rc) {
     c->pend_slices = 0;
@@ -1386,7 +1532,8 @@ static int process_file(nk_counter *c, const char *path, int streaming) {
   if (!c) return fail(NK_E_INVALID, "null counter");
   if (!path) return fail(NK_E_INVALID, "null path");
   bool fallback = c->pool == 0;  // pool 0: the host path checks for k-mers (% 0)
-  int rc;
+  int rc = whole_pool(c);
+  if (rc) return rc;
   if (!fallback) {
     rc = ingest_file(c, path, &fallback);
     if (rc) return rc;
@@ -1588,6 +1735,7 @@ int nk_finalize_export(nk_counter *c, int streaming, const uint32_t *d_wire, uin
   if (c->cur_in_wire != (d_wire != nullptr))
     return fail(NK_E_INVALID, d_wire ? "d_wire without nk_wire32" : "the currents are in the wire vector: pass it");
   if (cap > (1ull << 40)) return fail(NK_E_INVALID, "cap too large");
+  if (int rc0 = whole_pool(c)) return rc0;
   const bool use_kpn = c->opts.exact_counts && c->exact_built && c->kpn_global;
   if (use_kpn)
     return fail(NK_E_UNSUPPORTED, "exact table: the uniques come from kmer_per_neuron (nk_finalize)");
@@ -1661,6 +1809,7 @@ int nk_merge_export(nk_counter *c, const uint64_t *d_buf, size_t world, size_t s
   if (!c->export_blocking) {  // the blocking export already counted its spikes
     c->total_spikes += h->stats[0];
     c->total_energy += h->stats[0] * cost_fixed(c->cost);
+    c->max_sc = h->stats[1];
   }
   c->top.resize(want);
   for (uint32_t i = 0; i < want; ++i) {
@@ -1737,6 +1886,7 @@ int nk_finalize_slice(nk_counter *c, int streaming, const void *d_slice, int sli
                             c->hist.p, c->stats.p, TopFuse{}, s));
   }
   c->state_fresh = false;
+  c->sliced = true;  // only [lo, hi) of v / r / spike counts / currents is this rank's now
   if (m) {
     HIPCHK(launch_topn_threshold(c->hist.p, m, n, c->topst.p, s));
     if ((rc = enqueue_select(c, m, s, c->sc.p + lo, n, c->cur.p + lo))) return rc;
@@ -1832,37 +1982,55 @@ int nk_adopt_slices(nk_counter *c, const uint64_t *d_all, size_t world, size_t s
 
 static int table_ready(nk_counter *c, hipStream_t *s);
 
-// Rows past the ones the last call selected: the whole pool ranked on the
-// device (stable radix sort, ties by index, src/spiking_hash.rs:661-673) and
-// the uniques column from kmer_per_neuron (built on demand from the last input
-// without opts.exact_counts).
+// Rows past the ones the last call selected (src/spiking_hash.rs:661-673: the
+// stable sort, ties by index), the uniques column from kmer_per_neuron (built
+// on demand from the last input without opts.exact_counts).
+//   m <= kMaxTopN: the exact threshold by radix passes over the spike counts
+//     (as many 8-bit digits as the known largest count has) and the select
+//     kernels of the top-N path: O(P / 2048) scratch, no pool-sized sort.
+//   more rows: the whole pool ranked by a stable radix sort over the bits of
+//     the largest count (24 B of scratch per neuron).
 static long extended_top(nk_counter *c, size_t m, nk_top_row *out) {
   hipStream_t s;
   int rc = table_ready(c, &s);
   if (rc) return rc;
+  if ((rc = whole_pool(c))) return rc;
   const uint64_t P = c->pool;
-  if (P > 0xFFFFFFFFull) return fail(NK_E_UNSUPPORTED, "rows past top_n need pool_size < 2^32");
   if ((rc = materialize(c, false, s))) return rc;
-  if ((rc = c->rk_keys.ensure(2 * P)) || (rc = c->rk_idx.ensure(2 * P)) ||
-      (rc = c->rk_tmp.ensure(rank_rows_temp_bytes(P))) || (rc = c->rk_cand.ensure(m)) ||
-      (rc = c->rk_uniq.ensure(m)))
-    return rc;
-  HIPCHK(rank_rows(c->sc.p, P, ~0ull, c->rk_keys.p, c->rk_keys.p + P, c->rk_idx.p, c->rk_idx.p + P,
-                   c->rk_tmp.p, c->rk_tmp.n, s));
-  std::vector<uint64_t> key(m);
-  std::vector<uint32_t> idx(m), uq(m, 0);
-  HIPCHK(hipMemcpyAsync(key.data(), c->rk_keys.p + P, m * 8, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(idx.data(), c->rk_idx.p + P, m * 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
+  if ((rc = c->rk_cand.ensure(m)) || (rc = c->rk_uniq.ensure(m))) return rc;
+  std::vector<TopCand> tc(m);
+  if (m <= (size_t)kMaxTopN) {
+    // the rows land in c->cand / c->top_cur: their first top_n rows are the
+    // call's own rows (same exact order), which the multi-GPU helpers read
+    TopState st{};
+    if ((rc = refine_threshold(c, m, c->max_sc, st, s))) return rc;
+    HIPCHK(hipMemcpyAsync(c->topst.p, &st, sizeof st, hipMemcpyHostToDevice, s));
+    if ((rc = enqueue_select(c, m, s))) return rc;
+    HIPCHK(hipMemcpyAsync(tc.data(), c->cand.p, m * sizeof(TopCand), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));  // st is host memory the copy reads
+  } else {
+    if (P > 0xFFFFFFFFull)
+      return fail(NK_E_UNSUPPORTED, "more than %d rows past top_n need pool_size < 2^32", kMaxTopN);
+    if ((rc = c->rk_keys.ensure(2 * P)) || (rc = c->rk_idx.ensure(2 * P)) ||
+        (rc = c->rk_tmp.ensure(rank_rows_temp_bytes(P))))
+      return rc;
+    HIPCHK(rank_rows(c->sc.p, P, c->max_sc, c->rk_keys.p, c->rk_keys.p + P, c->rk_idx.p,
+                     c->rk_idx.p + P, c->rk_tmp.p, c->rk_tmp.n, s));
+    std::vector<uint64_t> key(m);
+    std::vector<uint32_t> idx(m);
+    HIPCHK(hipMemcpyAsync(key.data(), c->rk_keys.p + P, m * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(idx.data(), c->rk_idx.p + P, m * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (size_t i = 0; i < m; ++i) tc[i] = TopCand{idx[i], c->max_sc - key[i]};
+  }
+  std::vector<uint32_t> uq(m, 0);
   if (c->kpn_valid) {
-    std::vector<TopCand> tc(m);
-    for (size_t i = 0; i < m; ++i) tc[i] = TopCand{idx[i], ~key[i]};
     HIPCHK(hipMemcpyAsync(c->rk_cand.p, tc.data(), m * sizeof(TopCand), hipMemcpyHostToDevice, s));
     HIPCHK(exact_top_uniques(c->rk_cand.p, (uint32_t)m, c->kpn.p, c->rk_uniq.p, s));
     HIPCHK(hipMemcpyAsync(uq.data(), c->rk_uniq.p, m * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
   }
-  for (size_t i = 0; i < m; ++i) out[i] = nk_top_row{idx[i], ~key[i], uq[i], 0};
+  for (size_t i = 0; i < m; ++i) out[i] = nk_top_row{tc[i].idx, tc[i].sc, uq[i], 0};
   return (long)m;
 }
 
@@ -1941,18 +2109,21 @@ static int need_exact(nk_counter *c) {
 // ---------------------------------------------------------------------------
 struct StreamAcc {
   CountPlan cp;
+  bool keep = false;  // Part keeps every record until acc_end (the uniques scan reads them)
 };
 
 // zero the accumulators and size the partition arena: Part keeps every
-// record until acc_end (~est_bases bases), Gen/Wide histogram each batch
-// (<= batch_bases bases) as it is counted
+// record until acc_end (~est_bases bases, up to count_chunk()); Gen/Wide, and
+// Part past count_chunk(), histogram each batch (<= batch_bases bases) as it
+// is counted and drop its records (the uniques pass then rescans the input)
 static int acc_begin(nk_counter *c, uint64_t est_bases, uint64_t batch_bases, StreamAcc &sa,
                      hipStream_t s) {
   int rc;
   ZeroList z{};
   z.ptr[z.n] = c->cur.p; z.bytes[z.n++] = c->pool * 8;
   const uint64_t B = (c->pool + kBinsPerBucket - 1) >> kBinBits;
-  const bool part_like = !c->w128 && c->k <= 32 && B <= (uint64_t)kMaxBuckets && !wide_bits_forced();
+  const bool part_like = !c->w128 && c->k <= 32 && B <= (uint64_t)kMaxBuckets &&
+                         !wide_bits_forced() && est_bases <= count_chunk();
   const uint64_t est = part_like ? est_bases : std::min(est_bases, batch_bases);
   // segments per bucket: one per tile per launch; chunk-straddling tiles add a few
   const uint64_t max_segs = n_tiles_for(std::max<uint64_t>(est, 1), kPartTile) + 4096;
@@ -1962,7 +2133,8 @@ static int acc_begin(nk_counter *c, uint64_t est_bases, uint64_t batch_bases, St
   c->lif_zeroed = true;
   if (c->pool) HIPCHK(launch_zero(z, s));
   c->cur_fresh = false;
-  c->part_used = sa.cp.path == CountPath::Part;
+  sa.keep = sa.cp.path == CountPath::Part && part_like;
+  c->part_used = sa.keep;
   c->gen_km = (sa.cp.path == CountPath::Gen || sa.cp.path == CountPath::Wide) ? sa.cp.km : -1;
   return NK_OK;
 }
@@ -1983,20 +2155,15 @@ static int acc_batch(nk_counter *c, StreamAcc &sa, const KmerInput &whole, uint6
   HIPCHK(launch_tile_rec(in, cp.tile, c->tile_rec.p, s));
   switch (cp.path) {
     case CountPath::Part:
-      HIPCHK(launch_part(in, (int)c->k, c->canonical, c->pool, cp.pa, s));
-      break;
-    case CountPath::Gen:
-    case CountPath::Wide: {
-      HIPCHK(gen_count(c, cp, in, s));
-      HIPCHK(gen_hist(c, cp, false, s));
-      ZeroList z{};  // empty the regions for the next batch
-      z.ptr[z.n] = cp.pa.fill; z.bytes[z.n++] = (uint64_t)cp.pa.n_buckets * 8;
-      if (cp.path == CountPath::Wide) {
-        z.ptr[z.n] = cp.ga.fill; z.bytes[z.n++] = (uint64_t)cp.ga.n_buckets * 8;
+      if (sa.keep) {
+        HIPCHK(launch_part(in, (int)c->k, c->canonical, c->pool, cp.pa, s));
+        break;
       }
-      HIPCHK(launch_zero(z, s));
+      [[fallthrough]];
+    case CountPath::Gen:
+    case CountPath::Wide:
+      HIPCHK(batch_count(c, cp, in, s));
       break;
-    }
     case CountPath::Atomic:
       if (c->w128)
         HIPCHK(launch_count128(in, (int)c->k, c->canonical, c->pool, c->cur.p, s));
@@ -2011,7 +2178,7 @@ static int acc_batch(nk_counter *c, StreamAcc &sa, const KmerInput &whole, uint6
 // bookkeeping of a finished input
 static int acc_end(nk_counter *c, StreamAcc &sa, const KmerInput &whole, hipStream_t s) {
   int rc;
-  if (sa.cp.path == CountPath::Part) {
+  if (sa.keep) {
     HIPCHK(launch_bucket_hist(sa.cp.pa, c->pool, sa.cp.slices, c->partials.p, s));
     c->pend_slices = sa.cp.slices;
     c->last_pa = sa.cp.pa;
@@ -2173,6 +2340,7 @@ int nk_process_sequence(nk_counter *c, const uint8_t *seq, size_t len) {
   if (c->w128)
     return fail(NK_E_UNSUPPORTED, "process_sequence takes the reference's u64 keys (NK_KMER_COMPAT)");
   if (len && !seq) return fail(NK_E_INVALID, "null sequence");
+  if (int rc0 = whole_pool(c)) return rc0;
   if (len < c->k) return NK_OK;  // :205-207: no k-mers, no LIF step
   if (c->pool == 0)
     return fail(NK_E_INVALID, "pool_size 0 with k-mers present (the reference panics on % 0)");

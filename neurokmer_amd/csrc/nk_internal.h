@@ -1,0 +1,23 @@
+// nk_internal.h — what other translation units of libneurokmer.so read of a
+// counter handle (internal; not ABI).  Implemented in nk_counter.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "neurokmer.h"
+
+// nk_last_error() text for this thread; returns code
+int nk_fail_msg(int code, const char *msg);
+
+namespace nk {
+// min(opts.top_n, pool_size): the rows every finish selects
+uint64_t counter_rows(const nk_counter *c);
+// u64 words per k-mer key (2 for NK_KMER_128)
+int counter_key_words(const nk_counter *c);
+// the uniques column comes from an adopted global kmer_per_neuron (multi-GPU
+// exact table): the finish is a plain nk_finalize after the currents' all-reduce
+bool counter_kpn_global(const nk_counter *c);
+// the u64 currents complete on stream s (lazily-zero currents materialised,
+// pending K1b partials folded, no host wait); null on error
+uint64_t *counter_currents_on(nk_counter *c, hipStream_t s);
+}  // namespace nk

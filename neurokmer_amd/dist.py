@@ -102,8 +102,65 @@ def allreduce_currents_(t, group=None, total_kmers=None) -> None:
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
 
 
+class Comm:
+    """The library's own communicator for this rank (RCCL over xGMI;
+    include/neurokmer.h nk_comm_*): rank 0 of `group` makes the id, the group
+    broadcasts it, every rank builds its communicator (collective).  With one,
+    finalize_step / finalize_step_sliced run the whole finish inside the
+    library (nk_finalize_dist / nk_finalize_sliced_dist): the collectives are
+    enqueued between the library's kernels with no Python in between."""
+
+    def __init__(self, group=None, device: int | None = None):
+        import ctypes as C
+
+        import torch
+        import torch.distributed as dist
+        from . import _lib
+        self._L = _lib.load()
+        self._h = None
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.device = torch.cuda.current_device() if device is None else device
+        idb = (C.c_uint8 * 128)()
+        if self.rank == 0:
+            _lib.check(self._L.nk_comm_unique_id(idb))
+        obj = [bytes(idb)]
+        src = 0 if group is None else dist.get_global_rank(group, 0)
+        dist.broadcast_object_list(obj, src=src, group=group)
+        idb = (C.c_uint8 * 128).from_buffer_copy(obj[0])
+        h = self._L.nk_comm_new(idb, self.world, self.rank, self.device)
+        if not h:
+            raise _lib.NeuroKmerError(_lib.NK_E_DEVICE, _lib.last_error())
+        self._h = h
+
+    def close(self):
+        if self._h:
+            self._L.nk_comm_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_U64_MAX = (1 << 64) - 1
+
+
+def _comm_finish(ctr, comm, fn, total_kmers, cap, streaming):
+    import torch
+    from ._lib import check
+    stream = torch.cuda.current_stream().cuda_stream
+    if stream == 0:
+        _on_side_stream(ctr, lambda: _comm_finish(ctr, comm, fn, total_kmers, cap, streaming))
+        return
+    tk = _U64_MAX if total_kmers is None or total_kmers < 0 else int(total_kmers)
+    check(getattr(comm._L, fn)(ctr._h, comm._h, 1 if streaming else 0, tk, cap, stream))
+
+
 def finalize_step(ctr, group=None, total_kmers=None, cap: int = 4096,
-                  streaming: bool = False, between=None) -> None:
+                  streaming: bool = False, between=None, comm: "Comm | None" = None) -> None:
     """After every rank's ctr.accumulate_device: the whole multi-GPU finish with
     ONE host synchronisation (include/neurokmer.h, nk_finalize_export):
 
@@ -123,9 +180,18 @@ def finalize_step(ctr, group=None, total_kmers=None, cap: int = 4096,
     between: called once the currents' all-reduce is enqueued, before the rest
     (a caller keeping batches in flight enqueues the next batch's count there:
     on another handle it starts when this all-reduce is done and runs beside
-    this batch's finish; bench.py --inflight 2)."""
+    this batch's finish; bench.py --inflight 2).
+
+    comm: the library's communicator (Comm): the same protocol, all of it
+    enqueued by one library call (nk_finalize_dist); `between` then runs
+    before it."""
     import torch
     import torch.distributed as dist
+    if comm is not None:
+        if between is not None:
+            between()
+        _comm_finish(ctr, comm, "nk_finalize_dist", total_kmers, cap, streaming)
+        return
     if torch.cuda.current_stream().cuda_stream == 0:
         # the library reads a NULL stream as its own stream: run the step on a
         # real torch stream so the collectives and our kernels share one order
@@ -183,7 +249,7 @@ def slice_bounds(pool: int, world: int, rank: int) -> Tuple[int, int, int]:
 
 
 def finalize_step_sliced(ctr, group=None, total_kmers=None, cap: int = 4096,
-                         streaming: bool = False) -> None:
+                         streaming: bool = False, comm: "Comm | None" = None) -> None:
     """After every rank's accumulate: the finish for very large pools
     (SURVEY.md §5/§8e, config 5).  Instead of all-reducing the whole currents
     vector and running the LIF of the whole pool on every rank:
@@ -197,9 +263,13 @@ def finalize_step_sliced(ctr, group=None, total_kmers=None, cap: int = 4096,
       union of the shards' top keys                            (union_top_kmers)
 
     Afterwards a rank's neuron state is authoritative on its slice only
-    (gather_state assembles the whole pool)."""
+    (gather_state assembles the whole pool).  comm: all of it inside the
+    library (nk_finalize_sliced_dist)."""
     import torch
     import torch.distributed as dist
+    if comm is not None:
+        _comm_finish(ctr, comm, "nk_finalize_sliced_dist", total_kmers, cap, streaming)
+        return
     if torch.cuda.current_stream().cuda_stream == 0:
         _on_side_stream(ctr, lambda: finalize_step_sliced(ctr, group, total_kmers, cap, streaming))
         return

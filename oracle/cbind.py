@@ -52,6 +52,8 @@ def lib():
             f.argtypes = [C.c_void_p, u8p, u64p, C.c_size_t, C.c_int]
         L.nko_process_sequence.restype = C.c_int
         L.nko_process_sequence.argtypes = [C.c_void_p, u8p, C.c_size_t]
+        L.nko_simulate_spikes_auto.restype = None
+        L.nko_simulate_spikes_auto.argtypes = [C.c_void_p]
         for fn, rt in (("nko_currents", u64p), ("nko_voltages", f32p), ("nko_refractory", u32p),
                        ("nko_spike_counts", u64p), ("nko_kmer_per_neuron", u32p)):
             f = getattr(L, fn)
@@ -176,6 +178,9 @@ class OracleCounter:
         buf = np.frombuffer(seq, dtype=np.uint8) if seq else np.zeros(1, np.uint8)
         if self._L.nko_process_sequence(self._h, _ptr(buf, C.c_uint8), len(seq)) != 0:
             raise RuntimeError("oracle rejected the input")
+
+    def simulate_spikes_auto(self):
+        self._L.nko_simulate_spikes_auto(self._h)
 
     def _arr(self, fn, dt):
         p = getattr(self._L, fn)(self._h)

@@ -594,12 +594,17 @@ int nko_process_parallel(nko_counter *c, const uint8_t *bases, const uint64_t *o
   return 0;
 }
 
-int nko_process_streaming(nko_counter *c, const uint8_t *bases, const uint64_t *offsets,
-                          size_t n_recs, int n_threads) {
-  if (accumulate(c, bases, offsets, n_recs, n_threads)) return -1;
-  /* simulate_spikes_simd (:544-659): every neuron, zero current included;
-   * steps == 0 returns before touching anything (:549-551). */
-  if (c->steps == 0) return 0;
+/* simulate_spikes_simd (src/spiking_hash.rs:544-659) — what
+ * simulate_spikes_auto (:697-714) runs on x86-64 with AVX2: `steps` updates of
+ * every neuron from neuron_currents (zero currents included), per 8-lane batch
+ * v' = active ? v*leak + c : v (two roundings), spike where active and
+ * v' >= thr (the blend puts f32::MAX in the threshold of refractory lanes; a
+ * refractory neuron's v is the 0 its spike left, so none spikes), r counted
+ * down / set to refractory exactly as LifNeuron::update (src/models.rs:34-51);
+ * total spikes and energy added once.  steps == 0 returns before touching
+ * anything (:549-551). */
+void nko_simulate_spikes_auto(nko_counter *c) {
+  if (c->steps == 0) return;
   uint64_t total = 0;
   lif_memo_t *memo = (lif_memo_t *)calloc((size_t)1 << LIF_MEMO_BITS, sizeof(lif_memo_t));
   for (size_t i = 0; i < c->pool; ++i) {
@@ -609,6 +614,12 @@ int nko_process_streaming(nko_counter *c, const uint8_t *bases, const uint64_t *
   }
   free(memo);
   add_spikes(c, total);
+}
+
+int nko_process_streaming(nko_counter *c, const uint8_t *bases, const uint64_t *offsets,
+                          size_t n_recs, int n_threads) {
+  if (accumulate(c, bases, offsets, n_recs, n_threads)) return -1;
+  nko_simulate_spikes_auto(c); /* :482 */
   return 0;
 }
 

@@ -75,6 +75,9 @@ int nko_process_parallel(nko_counter *c, const uint8_t *bases,
                          const uint64_t *offsets, size_t n_recs, int n_threads);
 int nko_process_streaming(nko_counter *c, const uint8_t *bases,
                           const uint64_t *offsets, size_t n_recs, int n_threads);
+/* simulate_spikes_auto (src/spiking_hash.rs:697-714 -> simulate_spikes_simd,
+ * :544-659): the streaming LIF rule over the held currents */
+void nko_simulate_spikes_auto(nko_counter *c);
 /* process_sequence (src/spiking_hash.rs:203-273): per-record single-step form */
 int nko_process_sequence(nko_counter *c, const uint8_t *seq, size_t len);
 

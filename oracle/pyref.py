@@ -271,6 +271,11 @@ class SpikingKmerCounter:
 
     def process_streaming(self, seqs):
         self._accumulate(seqs)
+        self.simulate_spikes_auto()  # src/spiking_hash.rs:482
+
+    def simulate_spikes_auto(self):
+        """:697-714 -> simulate_spikes_simd (:544-659): every neuron, zero
+        current included, from the held currents; steps == 0 returns first."""
         if self.steps == 0:
             return
         self._add_spikes(self._lif_all(skip_zero=False))

@@ -245,6 +245,95 @@ def test_config5_multi_gb_properties(width):
     g.close()
 
 
+# ---- bounded arena: inputs past count_chunk() are counted batch by batch ----------
+@pytest.mark.parametrize("k,pool,canon,width", [
+    (31, 2_000_000, True, 64),     # Part
+    (21, 100_003, False, 64),      # Part, pack_kmer keys
+    (40, 50_021, True, 64),        # Gen (compat k > 32)
+    (63, 20_000_003, True, 128),   # Wide, 128-bit keys
+])
+def test_batched_count_bit_exact(k, pool, canon, width):
+    """NK_COUNT_CHUNK forces the batched count (records histogrammed and dropped
+    per batch, uniques from a rescan) on a ~1.2 Mbase input: bit-exact vs the
+    oracle, for host input, device input + finalize, and two steps in a row."""
+    bases, offs = synth.make_records(1_200_000, 6, seed=140 + k, repeats_per_mb=4000,
+                                     motif_len=100, n_rate=0.002, mixed_case=True)
+    r = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, canon, width=width)
+    r.process_parallel_arrays(bases, offs, THREADS)
+    with env(NK_COUNT_CHUNK=200_000):  # 24 partition tiles per batch: 6 batches
+        g = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, canon, kmer_width=width)
+        g.process_parallel_arrays(bases, offs)
+        assert_same(g, r)
+        assert g.top_abundant_neurons(300) == r.top_abundant_neurons(300)  # held input
+        d_b = torch.from_numpy(np.concatenate([bases, np.zeros(16, np.uint8)])).cuda()
+        d_o = torch.from_numpy(offs.view(np.int64)).cuda()
+        torch.cuda.synchronize()
+        g.accumulate_device(d_b.data_ptr(), d_o.data_ptr(), offs.size - 1, bases.size)
+        g.finalize(False)
+        r.process_parallel_arrays(bases, offs, THREADS)
+        assert_same(g, r)
+    g.close()
+
+
+def test_batched_streaming_file(tmp_path):
+    """The file ingest's Part path past count_chunk(): each ingest batch is
+    histogrammed and dropped (FASTQ, pool 16 M, small ingest chunks)."""
+    bases, offs = synth.make_reads(20_000, 150, seed=150, repeats_per_mb=3000, motif_len=60,
+                                   n_rate=0.0005)
+    p = tmp_path / "b.fq"
+    _write_fastq_fast(str(p), bases, 150)
+    r = cbind.OracleCounter(31, 1.0, 0.95, 2, 1.0, C3_POOL, True)
+    r.process_streaming_arrays(bases, offs, THREADS)
+    with env(NK_COUNT_CHUNK=300_000, NK_INGEST_CHUNK=1_000_003):
+        g = SpikingKmerCounter(31, 1.0, 0.95, 2, 1.0, C3_POOL, True)
+        g.process_file_streaming(str(p))
+    assert_same(g, r)
+    g.close()
+
+
+def test_part_path_past_2_32_positions():
+    """k=31, pool 2M (the Part path) on 4.5 Gbases resident in HBM: past 2^32
+    positions and past count_chunk(), so the count runs in bounded batches.
+    The input is 5 copies of one 900 Mbase record: the currents must be exactly
+    5x one copy's (counted on the keep-records path), their sum N_k, the same on
+    a second run, and the top rows' uniques equal to one copy's kmer_per_neuron
+    (the same distinct keys)."""
+    n1, reps = 900_000_000, 5
+    one, _ = _device_random_records(n1, 1, seed=77)
+    d_b = torch.cat([one[:n1]] * reps + [torch.zeros(16, dtype=torch.uint8, device="cuda")])
+    n = n1 * reps
+    assert n > (1 << 32)
+    offs = np.arange(reps + 1, dtype=np.uint64) * np.uint64(n1)
+    d_o = torch.from_numpy(offs.view(np.int64)).cuda()
+    o1 = torch.from_numpy(np.array([0, n1], np.int64)).cuda()
+    torch.cuda.synchronize()
+    g1 = SpikingKmerCounter(31, 1.0, 0.95, 2, 1.0, POOL2, True, exact_counts=True)
+    g1.accumulate_device(one.data_ptr(), o1.data_ptr(), 1, n1)
+    single = torch.as_tensor(_CAI(g1.device_currents_ptr(), POOL2), device="cuda").clone()
+    torch.cuda.synchronize()
+    kpn1 = g1.kmer_per_neuron()
+    g = SpikingKmerCounter(31, 1.0, 0.95, 2, 1.0, POOL2, True)
+    g.accumulate_device(d_b.data_ptr(), d_o.data_ptr(), reps, n)
+    whole = torch.as_tensor(_CAI(g.device_currents_ptr(), POOL2), device="cuda").clone()
+    torch.cuda.synchronize()
+    assert int(whole.sum().item()) == n_kmers(offs, 31) == reps * (n1 - 30)
+    assert torch.equal(whole, single * reps)
+    g.accumulate_device(d_b.data_ptr(), d_o.data_ptr(), reps, n)
+    g.finalize(False)
+    assert torch.equal(torch.as_tensor(_CAI(g.device_currents_ptr(), POOL2), device="cuda"), whole)
+    top = g.top_abundant_neurons(20)
+    sc = g.spike_counts()
+    assert int(sc.sum()) == g.energy.total_spikes()
+    order = [int(i) for i in np.argsort(-sc.astype(np.int64), kind="stable")[:20]]
+    assert [t[0] for t in top] == order
+    assert [t[2] for t in top] == [int(kpn1[i]) for i in order]
+    g.close()
+    g1.close()
+
+
+POOL2 = 2_000_000
+
+
 # ---- golden fixtures through the HIP path ------------------------------------
 GOLDEN_E2E = sorted(glob.glob(os.path.join(GOLD, "e2e_*.json")))
 

@@ -139,6 +139,39 @@ def test_c_and_python_restatements_agree(seed):
     assert c.top_abundant_neurons(20) == p.top_abundant_neurons(20)
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_simulate_spikes_auto_restatements_agree(seed):
+    """simulate_spikes_auto (src/spiking_hash.rs:697-714 -> :544-659) after a
+    process call, repeated, with zero-current neurons stepping too; the C and
+    Python restatements agree bit for bit (steps 0 leaves everything alone)."""
+    rng = random.Random(100 + seed)
+    k = rng.choice([5, 17, 31, 40])
+    canon = rng.random() < 0.5
+    pool = rng.choice([7, 257, 3001])
+    thr, leak, refr = rng.choice([(1.0, 0.95, 2), (0.0, 0.9, 1), (0.02, 1.0, 0)])
+    bases, offs = synth.make_records(rng.randrange(500, 4000), rng.randrange(1, 5), seed=seed,
+                                     n_rate=0.01, repeats_per_mb=20000, motif_len=40)
+    seqs = synth.records_list(bases, offs)
+    p = pyref.SpikingKmerCounter(k, thr, leak, refr, 1.0, pool, canon)
+    c = cbind.OracleCounter(k, thr, leak, refr, 1.0, pool, canon)
+    for steps in (1000, 0, 37):
+        p.steps = steps
+        c.set_steps(steps)
+        if seed % 2:
+            p.process_parallel(seqs)
+            c.process_parallel(seqs, 2)
+        p.simulate_spikes_auto()
+        c.simulate_spikes_auto()
+        p.simulate_spikes_auto()
+        c.simulate_spikes_auto()
+        assert [int(x) for x in c.currents()] == p.currents
+        assert [int(x) for x in c.spike_counts()] == p.sc
+        assert [int(x) for x in c.voltages().view(np.uint32)] == [pyref.f32_bits(v) for v in p.v]
+        assert [int(x) for x in c.refractory()] == p.r
+        assert c.total_spikes == p.total_spikes
+        assert c.top_abundant_neurons(20) == p.top_abundant_neurons(20)
+
+
 # ---------------------------------------------------------------------------
 # CPU models of the device algorithms (neurokmer_amd/csrc/nk_device.h)
 # ---------------------------------------------------------------------------
