@@ -31,6 +31,7 @@ __device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) {
 }
 __device__ __forceinline__ uint64_t swap32(uint64_t x) { return (x << 32) | (x >> 32); }
 
+#define NK_SIP_V2(x) (x)  // (the held form of v2 between rounds)
 #define NK_SIPROUND                                                  \
   do {                                                               \
     v0 += v1; v1 = rotl64(v1, 13); v1 ^= v0; v0 = swap32(v0);        \
@@ -39,6 +40,25 @@ __device__ __forceinline__ uint64_t swap32(uint64_t x) { return (x << 32) | (x >
     v2 += v1; v1 = rotl64(v1, 17); v1 ^= v2; v2 = swap32(v2);        \
   } while (0)
 
+// The last SipRound fused with the output v0 ^ v1 ^ v2 ^ v3.  In that round
+// v3' = rotl(v3, 21) ^ v0' and the output xors v0' in again, so v0' (its swap,
+// its add) cancels and is never computed; v2' ^ swap32(v2') has equal halves:
+//   out = rotl(v1, 17) ^ v2' ^ swap32(v2') ^ rotl(v3, 21)   (v1, v3 mid-round)
+// (tests/test_oracle.py::test_sip13_last_round_model).  The compiler already
+// cancelled the output xors of the plain form; this drops the dead 64-bit add
+// of v0' (1 of 18 v_lshl_add_u64 per hash).
+__device__ __forceinline__ uint64_t sip_last_round_out(uint64_t v0, uint64_t v1, uint64_t v2,
+                                                       uint64_t v3) {
+  v0 += v1; v1 = rotl64(v1, 13); v1 ^= v0;
+  v2 += v3; v3 = rotl64(v3, 16); v3 ^= v2;
+  v3 = rotl64(v3, 21);
+  v2 += v1; v1 = rotl64(v1, 17);
+  const uint32_t x = (uint32_t)v2 ^ (uint32_t)(v2 >> 32);  // both halves of v2' ^ swap32(v2')
+  const uint32_t lo = (uint32_t)v1 ^ (uint32_t)v3 ^ x;
+  const uint32_t hi = (uint32_t)(v1 >> 32) ^ (uint32_t)(v3 >> 32) ^ x;
+  return ((uint64_t)hi << 32) | lo;
+}
+
 // SipHash-1-3 with key (0,0) of one u64 written as 8 LE bytes:
 // one compression round for the message block, one for the length block
 // (b = 8 << 56), three finalization rounds.  Constants of the first round
@@ -46,7 +66,7 @@ __device__ __forceinline__ uint64_t swap32(uint64_t x) { return (x << 32) | (x >
 __device__ __forceinline__ uint64_t sip13_u64(uint64_t m) {
   uint64_t v0 = 0x736f6d6570736575ULL;
   uint64_t v1 = 0x646f72616e646f6dULL;
-  uint64_t v2 = 0x6c7967656e657261ULL;
+  uint64_t v2 = NK_SIP_V2(0x6c7967656e657261ULL);
   uint64_t v3 = 0x7465646279746573ULL ^ m;
   NK_SIPROUND;
   v0 ^= m;
@@ -54,11 +74,15 @@ __device__ __forceinline__ uint64_t sip13_u64(uint64_t m) {
   v3 ^= b;
   NK_SIPROUND;
   v0 ^= b;
-  v2 ^= 0xffULL;
+  v2 ^= NK_SIP_V2(0xffULL);
   NK_SIPROUND;
   NK_SIPROUND;
+#if defined(NK_SIP_FULL_LAST)  // A/B only: the plain last round and output xor
   NK_SIPROUND;
   return v0 ^ v1 ^ v2 ^ v3;
+#else
+  return sip_last_round_out(v0, v1, NK_SIP_V2(v2), v3);
+#endif
 }
 
 // --kmer-width=128: SipHash-1-3 (key 0) over the 16 LE bytes of a u128 key:
@@ -67,7 +91,7 @@ __device__ __forceinline__ uint64_t sip13_u64(uint64_t m) {
 __device__ __forceinline__ uint64_t sip13_u128(uint64_t lo, uint64_t hi) {
   uint64_t v0 = 0x736f6d6570736575ULL;
   uint64_t v1 = 0x646f72616e646f6dULL;
-  uint64_t v2 = 0x6c7967656e657261ULL;
+  uint64_t v2 = NK_SIP_V2(0x6c7967656e657261ULL);
   uint64_t v3 = 0x7465646279746573ULL ^ lo;
   NK_SIPROUND;
   v0 ^= lo;
@@ -78,11 +102,15 @@ __device__ __forceinline__ uint64_t sip13_u128(uint64_t lo, uint64_t hi) {
   v3 ^= b;
   NK_SIPROUND;
   v0 ^= b;
-  v2 ^= 0xffULL;
+  v2 ^= NK_SIP_V2(0xffULL);
   NK_SIPROUND;
   NK_SIPROUND;
+#if defined(NK_SIP_FULL_LAST)  // A/B only: the plain last round and output xor
   NK_SIPROUND;
   return v0 ^ v1 ^ v2 ^ v3;
+#else
+  return sip_last_round_out(v0, v1, NK_SIP_V2(v2), v3);
+#endif
 }
 
 // Exact h % P for any P >= 1 given magic = floor((2^64-1)/P):

@@ -17,6 +17,7 @@
 //   K4 k_topn_*     exact top-N by (spikes desc, index asc).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <type_traits>
 
 #include "nk_device.h"
@@ -2131,22 +2132,33 @@ hipError_t launch_pad_keys(const uint64_t *src, const unsigned long long *n_src,
   return hipGetLastError();
 }
 
+// A/B experiments: NK_K1A_DYN_LDS=bytes of unused dynamic LDS per K1a
+// workgroup (fewer resident workgroups per CU leave room for other kernels)
+static size_t k1a_dyn_lds() {
+  static const size_t v = [] {
+    const char *e = getenv("NK_K1A_DYN_LDS");
+    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)0;
+  }();
+  return v;
+}
+
 hipError_t launch_part(const KmerInput &in, int k, int canonical, uint64_t pool,
                        const PartArgs &pa, hipStream_t s) {
   if (!in.n_tiles) return hipSuccess;
   FastMod fm = make_fastmod(pool);
   const dim3 g((unsigned)in.n_tiles), bl(kPartBlock);
+  const size_t dyn = k1a_dyn_lds();
   if (pa.n_buckets > (uint32_t)kMaxBuckets) return hipErrorInvalidValue;
   if (pa.n_buckets <= 256) {
-#if defined(NK_K1A_K16)
-    if (canonical && k >= 16) hipLaunchKernelGGL((k_part<true, 256, true>), g, bl, 0, s, in, k, fm, pa);
+#if !defined(NK_K1A_NO_K16)  // (A/B: the masked low word)
+    if (canonical && k >= 16) hipLaunchKernelGGL((k_part<true, 256, true>), g, bl, dyn, s, in, k, fm, pa);
     else
 #endif
-    if (canonical) hipLaunchKernelGGL((k_part<true, 256>), g, bl, 0, s, in, k, fm, pa);
-    else hipLaunchKernelGGL((k_part<false, 256>), g, bl, 0, s, in, k, fm, pa);
+    if (canonical) hipLaunchKernelGGL((k_part<true, 256>), g, bl, dyn, s, in, k, fm, pa);
+    else hipLaunchKernelGGL((k_part<false, 256>), g, bl, dyn, s, in, k, fm, pa);
   } else {
-    if (canonical) hipLaunchKernelGGL((k_part<true, kMaxBuckets>), g, bl, 0, s, in, k, fm, pa);
-    else hipLaunchKernelGGL((k_part<false, kMaxBuckets>), g, bl, 0, s, in, k, fm, pa);
+    if (canonical) hipLaunchKernelGGL((k_part<true, kMaxBuckets>), g, bl, dyn, s, in, k, fm, pa);
+    else hipLaunchKernelGGL((k_part<false, kMaxBuckets>), g, bl, dyn, s, in, k, fm, pa);
   }
   return hipGetLastError();
 }

@@ -178,6 +178,48 @@ def test_simulate_spikes_auto_restatements_agree(seed):
 f32 = pyref.f32
 
 
+def _sip_device_model(blocks):
+    """neurokmer_amd/csrc/nk_device.h's SipHash-1-3 (key 0): the message
+    blocks, then the length block, two finalisation rounds and the fused last
+    round, whose v0 cancels out of the output (sip_last_round_out)."""
+    M = pyref.M64
+    rot = pyref._rotl
+    v = [0x736f6d6570736575, 0x646f72616e646f6d, 0x6c7967656e657261, 0x7465646279746573]
+
+    def rnd():
+        v[0] = (v[0] + v[1]) & M; v[1] = rot(v[1], 13) ^ v[0]; v[0] = rot(v[0], 32)
+        v[2] = (v[2] + v[3]) & M; v[3] = rot(v[3], 16) ^ v[2]
+        v[0] = (v[0] + v[3]) & M; v[3] = rot(v[3], 21) ^ v[0]
+        v[2] = (v[2] + v[1]) & M; v[1] = rot(v[1], 17) ^ v[2]; v[2] = rot(v[2], 32)
+    for m in blocks + [(8 * len(blocks)) << 56]:
+        v[3] ^= m
+        rnd()
+        v[0] ^= m
+    v[2] ^= 0xFF
+    rnd()
+    rnd()
+    v0, v1, v2, v3 = v
+    v0 = (v0 + v1) & M; v1 = rot(v1, 13) ^ v0
+    v2 = (v2 + v3) & M; v3 = rot(v3, 16) ^ v2
+    v3 = rot(v3, 21)
+    v2 = (v2 + v1) & M; v1 = rot(v1, 17)
+    x = (v2 ^ (v2 >> 32)) & 0xFFFFFFFF
+    lo = (v1 ^ v3 ^ x) & 0xFFFFFFFF
+    hi = ((v1 >> 32) ^ (v3 >> 32) ^ x) & 0xFFFFFFFF
+    return (hi << 32) | lo
+
+
+def test_sip13_last_round_model():
+    """The device's fused last round equals full SipHash-1-3 (u64 and u128 keys)."""
+    rng = random.Random(13)
+    vals = [0, 1, M64 := (1 << 64) - 1, 1 << 63] + [rng.getrandbits(64) for _ in range(3000)]
+    for m in vals:
+        assert _sip_device_model([m]) == cbind.sip13_u64(m) == pyref.sip13_u64(m)
+    for _ in range(1000):
+        key = rng.getrandbits(126)
+        assert _sip_device_model([key & M64, key >> 64]) == cbind.sip13_u128(key)
+
+
 def lif_step(v, leak, c):
     return f32(f32(v * leak) + c)
 
