@@ -188,6 +188,11 @@ struct nk_counter {
   ResultHdr last_hdr{};
   bool lif_zeroed = false;   // hist/stats already zeroed by this call's prep kernel
   bool state_fresh = true;   // spikes/v/r are logically zero (lazy reset)
+  // the last LIF ran from the reset state, so v / r / spike counts are a
+  // function of each neuron's count (cur) and were not written: derived_lp
+  // and the closed-form table give them back (settle_state writes them out)
+  bool state_derived = false;
+  LifParams derived_lp{};
   bool cur_fresh = true;     // currents are logically zero (lazy reset)
   // exact k-mer table (opts.exact_counts, nk_exact.h)
   DevBuf<uint64_t> x_keys, x_sorted, x_uniq, x_q;
@@ -325,7 +330,32 @@ static int zero_state_on(nk_counter *c, hipStream_t) {
   c->x_lazy = false;
   c->sliced = false;
   c->max_sc = 0;
+  c->state_derived = false;
   return NK_OK;
+}
+
+// The derived state written out: before anything reads the v / refractory /
+// spike count arrays or changes the counts it is a function of.
+static int settle_state(nk_counter *c, hipStream_t s) {
+  if (!c->state_derived) return NK_OK;
+  c->state_derived = false;
+  HIPCHK(launch_lif_derive(c->cur.p, c->v.p, c->r.p, c->sc.p, c->pool, c->derived_lp, c->lif_tbl.p,
+                           kLifTable, s));
+  return NK_OK;
+}
+
+// spike counts of neurons [lo, ...) as the top-N passes read them
+static SpikeSrc spike_src(const nk_counter *c, uint64_t lo) {
+  SpikeSrc x{};
+  if (c->state_derived) {
+    x.cur = c->cur.p + lo;
+    x.tbl = c->lif_tbl.p;
+    x.tbl_n = kLifTable;
+    x.lp = c->derived_lp;
+  } else {
+    x.sc = c->sc.p + lo;
+  }
+  return x;
 }
 
 // LIF passes and readers of the whole pool need the whole pool's state on this
@@ -389,6 +419,7 @@ static int copy_out(nk_counter *c, const DevBuf<T> &b, T *out, size_t n) {
   int rc = materialize(c, is_cur, s);
   if (rc) return rc;
   if (is_cur && (rc = fold_pending(c, s))) return rc;
+  if (!is_cur && (rc = settle_state(c, s))) return rc;
   HIPCHK(hipStreamSynchronize(s));
   HIPCHK(hipMemcpy(out, b.p, n * sizeof(T), hipMemcpyDeviceToHost));
   return NK_OK;
@@ -411,7 +442,7 @@ uint64_t *counter_currents_on(nk_counter *c, hipStream_t stream) {
   }
   (void)hipSetDevice(c->device);
   hipStream_t s = pick_stream(c, stream);
-  if (materialize(c, true, s) || fold_pending(c, s)) return nullptr;
+  if (settle_state(c, s) || materialize(c, true, s) || fold_pending(c, s)) return nullptr;
   return c->cur.p;
 }
 }  // namespace nk
@@ -894,6 +925,8 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
     return fail(NK_E_INVALID, "pool_size 0 with k-mers present (the reference panics on % 0)");
   (void)hipSetDevice(c->device);
   hipStream_t s = pick_stream(c, stream);
+  // a derived state is a function of the counts this call replaces
+  if (int rc0 = settle_state(c, s)) return rc0;
   c->pend_slices = 0;  // this call zeroes the currents: earlier partials are void
   c->cur_in_wire = false;
   c->export_pending = c->redo_ready = false;
@@ -1037,11 +1070,9 @@ int nk_accumulate_device_from(nk_counter *c, const uint8_t *d_bases, const uint6
 // (sc, n): the spike counts ranked — the whole pool, or a rank's slice of it
 // (nk_finalize_slice); sc == nullptr means the handle's own pool
 static int refine_threshold(nk_counter *c, uint64_t want, uint64_t max_sc, TopState &st,
-                            hipStream_t s, const uint64_t *sc = nullptr, uint64_t n = 0) {
-  if (!sc) {
-    sc = c->sc.p;
-    n = c->pool;
-  }
+                            hipStream_t s, uint64_t lo = 0, uint64_t n = ~0ull) {
+  if (n == ~0ull) n = c->pool;
+  const SpikeSrc sc = spike_src(c, lo);
   int top_bit = 63;
   while (top_bit > 0 && !((max_sc >> top_bit) & 1)) --top_bit;
   int shift = (top_bit / 8) * 8;
@@ -1105,8 +1136,9 @@ static int lif_prepare(nk_counter *c, int streaming, LifParams &lp, hipStream_t 
 static int enqueue_lif(nk_counter *c, int streaming, uint32_t fuse_want, bool part,
                        hipStream_t s, const uint32_t *wire = nullptr) {
   LifParams lp;
-  int rc = lif_prepare(c, streaming, lp, s);
-  if (rc) return rc;
+  // (a LIF with no count since the last one: that one's derived state first)
+  int rc = settle_state(c, s);
+  if (rc || (rc = lif_prepare(c, streaming, lp, s))) return rc;
   TopFuse tf{};
   if (fuse_want) {
     const uint32_t nb = lif_blocks(c->pool);
@@ -1136,23 +1168,24 @@ static int enqueue_lif(nk_counter *c, int streaming, uint32_t fuse_want, bool pa
   // only overflowed buckets added into them, so only those buckets are read
   const uint32_t *over = (!wire && c->pend_slices && c->part_used) ? c->p_over.p : nullptr;
   HIPCHK(launch_lif_apply(c->cur.p, wire ? wire : c->partials.p, wire ? 1u : c->pend_slices,
-                          wire ? 1 : 0, over, (int)c->last_pa.bin_bits, c->state_fresh ? 1 : 0, c->v.p,
-                          c->r.p, c->sc.p, c->pool, lp, c->lif_tbl.p, kLifTable, c->hist.p,
-                          c->stats.p, tf, s));
+                          wire ? 1 : 0, over, (int)c->last_pa.bin_bits, c->state_fresh ? 1 : 0,
+                          /*derive=*/1, c->v.p, c->r.p, c->sc.p, c->pool, lp, c->lif_tbl.p, kLifTable,
+                          c->hist.p, c->stats.p, tf, s));
   c->pend_slices = 0;
+  if (c->pool && c->state_fresh) {  // from the reset state: v / r / spike counts derived
+    c->state_derived = true;
+    c->derived_lp = lp;
+  }
   if (c->pool) c->state_fresh = false;
   return NK_OK;
 }
 
-// (sc, n, cur): as refine_threshold; candidate indices are relative to sc
-static int enqueue_select(nk_counter *c, uint64_t want, hipStream_t s,
-                          const uint64_t *sc = nullptr, uint64_t n = 0,
-                          const uint64_t *cur = nullptr) {
-  if (!sc) {
-    sc = c->sc.p;
-    n = c->pool;
-    cur = c->cur.p;
-  }
+// (lo, n): as refine_threshold; candidate indices are relative to lo
+static int enqueue_select(nk_counter *c, uint64_t want, hipStream_t s, uint64_t lo = 0,
+                          uint64_t n = ~0ull) {
+  if (n == ~0ull) n = c->pool;
+  const SpikeSrc sc = spike_src(c, lo);
+  const uint64_t *cur = c->cur.p + lo;
   const unsigned nb = (unsigned)((n + 2047) / 2048);
   int rc;
   if ((rc = c->tie_cnt.ensure(nb))) return rc;
@@ -1718,8 +1751,8 @@ int nk_wire32(nk_counter *c, uint32_t *d_wire, void *stream) {
   if (c->cur_in_wire) return fail(NK_E_INVALID, "nk_wire32 twice without nk_finalize_export");
   (void)hipSetDevice(c->device);
   hipStream_t s = pick_stream(c, stream);
-  int rc = materialize(c, true, s);
-  if (rc) return rc;
+  int rc = settle_state(c, s);
+  if (rc || (rc = materialize(c, true, s))) return rc;
   // partitioned count with its partials pending: only overflowed buckets added into cur
   const uint32_t *over = (c->pend_slices && c->part_used) ? c->p_over.p : nullptr;
   HIPCHK(launch_wire32(c->cur.p, c->partials.p, c->pend_slices, over, (int)c->last_pa.bin_bits,
@@ -1868,8 +1901,8 @@ int nk_finalize_slice(nk_counter *c, int streaming, const void *d_slice, int sli
   const uint64_t n = hi - lo;
   const uint64_t m = std::min<uint64_t>(want, n);
   LifParams lp;
-  int rc = lif_prepare(c, streaming, lp, s);
-  if (rc) return rc;
+  int rc = settle_state(c, s);
+  if (rc || (rc = lif_prepare(c, streaming, lp, s))) return rc;
   // the reduced slice replaces this shard's currents and pending partials
   c->pend_slices = 0;
   c->cur_in_wire = false;
@@ -1882,14 +1915,18 @@ int nk_finalize_slice(nk_counter *c, int streaming, const void *d_slice, int sli
     const bool w32 = slice_bits == 32;
     HIPCHK(launch_lif_apply(c->cur.p + lo, w32 ? (const uint32_t *)d_slice : nullptr, w32 ? 1u : 0u,
                             w32 ? 1 : 0, nullptr, (int)c->last_pa.bin_bits, c->state_fresh ? 1 : 0,
-                            c->v.p + lo, c->r.p + lo, c->sc.p + lo, n, lp, c->lif_tbl.p, kLifTable,
-                            c->hist.p, c->stats.p, TopFuse{}, s));
+                            /*derive=*/1, c->v.p + lo, c->r.p + lo, c->sc.p + lo, n, lp, c->lif_tbl.p,
+                            kLifTable, c->hist.p, c->stats.p, TopFuse{}, s));
+  }
+  if (c->state_fresh) {  // derived on [lo, hi) (the rest of the pool is not this rank's)
+    c->state_derived = true;
+    c->derived_lp = lp;
   }
   c->state_fresh = false;
   c->sliced = true;  // only [lo, hi) of v / r / spike counts / currents is this rank's now
   if (m) {
     HIPCHK(launch_topn_threshold(c->hist.p, m, n, c->topst.p, s));
-    if ((rc = enqueue_select(c, m, s, c->sc.p + lo, n, c->cur.p + lo))) return rc;
+    if ((rc = enqueue_select(c, m, s, lo, n))) return rc;
   }
   if ((rc = enqueue_readback(c, (uint32_t)m, false, s))) return rc;
   if ((rc = wait_readback(c, s))) return rc;
@@ -1897,9 +1934,9 @@ int nk_finalize_slice(nk_counter *c, int streaming, const void *d_slice, int sli
   const uint64_t new_spikes = h->stats[0], max_sc = h->stats[1];
   if (m && h->st.refine) {  // spike counts >= 4095: exact radix refine over the slice
     TopState st = h->st;
-    if ((rc = refine_threshold(c, m, max_sc, st, s, c->sc.p + lo, n))) return rc;
+    if ((rc = refine_threshold(c, m, max_sc, st, s, lo, n))) return rc;
     HIPCHK(hipMemcpyAsync(c->topst.p, &st, sizeof st, hipMemcpyHostToDevice, s));
-    if ((rc = enqueue_select(c, m, s, c->sc.p + lo, n, c->cur.p + lo))) return rc;
+    if ((rc = enqueue_select(c, m, s, lo, n))) return rc;
   }
   std::vector<TopCand> rows(m);
   std::vector<uint64_t> rcur(m);
@@ -2012,7 +2049,7 @@ static long extended_top(nk_counter *c, size_t m, nk_top_row *out) {
     if (P > 0xFFFFFFFFull)
       return fail(NK_E_UNSUPPORTED, "more than %d rows past top_n need pool_size < 2^32", kMaxTopN);
     if ((rc = c->rk_keys.ensure(2 * P)) || (rc = c->rk_idx.ensure(2 * P)) ||
-        (rc = c->rk_tmp.ensure(rank_rows_temp_bytes(P))))
+        (rc = c->rk_tmp.ensure(rank_rows_temp_bytes(P))) || (rc = settle_state(c, s)))
       return rc;
     HIPCHK(rank_rows(c->sc.p, P, c->max_sc, c->rk_keys.p, c->rk_keys.p + P, c->rk_idx.p,
                      c->rk_idx.p + P, c->rk_tmp.p, c->rk_tmp.n, s));
@@ -2351,7 +2388,8 @@ int nk_process_sequence(nk_counter *c, const uint8_t *seq, size_t len) {
   if (rc) return rc;
   if (c->cur_in_wire)
     return fail(NK_E_INVALID, "the currents are in the wire vector until nk_finalize_export");
-  if ((rc = materialize(c, true, s)) || (rc = fold_pending(c, s))) return rc;
+  if ((rc = settle_state(c, s)) || (rc = materialize(c, true, s)) || (rc = fold_pending(c, s)))
+    return rc;
   if ((rc = c->in_bases.ensure(len + 16)) || (rc = c->in_offs.ensure(2)) ||
       (rc = c->x_n.ensure(2)) || (rc = c->kpn.ensure(c->pool)))
     return rc;
@@ -2596,10 +2634,13 @@ uint64_t *nk_device_currents(nk_counter *c) {
     fail(NK_E_INVALID, "the currents are in the wire vector until nk_finalize_export");
     return nullptr;
   }
-  if (c->cur_fresh || c->pend_slices) {  // lazily-reset currents / K1b partials pending
+  // lazily-reset currents / K1b partials pending / a derived state (the caller
+  // may change the counts it is a function of: written out first)
+  if (c->cur_fresh || c->pend_slices || c->state_derived) {
     (void)hipSetDevice(c->device);
     hipStream_t s = pick_stream(c, nullptr);
-    if (materialize(c, true, s) || fold_pending(c, s) || hipStreamSynchronize(s) != hipSuccess)
+    if (settle_state(c, s) || materialize(c, true, s) || fold_pending(c, s) ||
+        hipStreamSynchronize(s) != hipSuccess)
       return nullptr;
   } else if (c->last_s && c->last_s == c->own_stream) {
     // the last call ran on the handle's private stream, which the caller

@@ -32,6 +32,18 @@ struct LifEntry {  // closed-form result for a fresh neuron (v = 0, r = 0)
   uint32_t r;
 };
 
+// Where a top-N pass reads the spike counts: the materialised array, or --
+// after a LIF from the reset state, whose outcome is a function of each
+// neuron's count alone (the "derived" state: v / refractory / spike counts
+// are not written) -- from the counts through the closed form.
+struct SpikeSrc {
+  const uint64_t *sc;   // non-null: materialised spike counts
+  const uint64_t *cur;  // derived: the counts
+  const LifEntry *tbl;  // closed-form rows of fresh neurons (counts < tbl_n)
+  int tbl_n;
+  LifParams lp;         // of the LIF that produced the state
+};
+
 struct TopState {
   uint64_t T;          // spike count of the N-th row
   uint64_t n_above;    // rows with spikes > T (all selected)
@@ -179,19 +191,24 @@ uint64_t diag_hash_out_words(uint64_t n_keys);
 // partials/slices: when slices > 0, currents[i] += sum of the K1b partials
 // first (the fused K1c of a single-device process call) and is written back.
 // fresh: v/r/sc are taken as 0 (lazy reset) and every neuron is written.
+// derive (with fresh): v / r / spike counts are not written (the derived
+// state, SpikeSrc); launch_lif_derive materialises them from the counts.
 hipError_t launch_lif_apply(uint64_t *currents, const uint32_t *partials, uint32_t slices,
                             int cur_zero, const uint32_t *over, int over_bits,
-                            int fresh, float *v, uint32_t *r, uint64_t *sc, uint64_t pool, LifParams lp,
-                            const LifEntry *tbl, int tbl_n, uint32_t *hist, uint64_t *stats,
-                            const TopFuse &tf, hipStream_t s);
+                            int fresh, int derive, float *v, uint32_t *r, uint64_t *sc, uint64_t pool,
+                            LifParams lp, const LifEntry *tbl, int tbl_n, uint32_t *hist,
+                            uint64_t *stats, const TopFuse &tf, hipStream_t s);
+hipError_t launch_lif_derive(const uint64_t *currents, float *v, uint32_t *r, uint64_t *sc,
+                             uint64_t pool, LifParams lp, const LifEntry *tbl, int tbl_n,
+                             hipStream_t s);
 uint32_t lif_blocks(uint64_t pool);  // grid size of the LIF kernel
 hipError_t launch_topn_threshold(const uint32_t *hist, uint64_t n, uint64_t pool, TopState *st,
                                  hipStream_t s);
-hipError_t launch_radix_hist(const uint64_t *sc, uint64_t pool, int shift, uint64_t prefix,
+hipError_t launch_radix_hist(const SpikeSrc &sc, uint64_t pool, int shift, uint64_t prefix,
                              uint32_t *hist256, hipStream_t s);
-hipError_t launch_topn_count(const uint64_t *sc, uint64_t pool, TopState *st,
+hipError_t launch_topn_count(const SpikeSrc &sc, uint64_t pool, TopState *st,
                              uint32_t *tie_cnt, TopCand *cand, hipStream_t s);
-hipError_t launch_topn_emit(const uint64_t *sc, uint64_t pool, TopState *st,
+hipError_t launch_topn_emit(const SpikeSrc &sc, uint64_t pool, TopState *st,
                             const uint32_t *tie_cnt, TopCand *cand, hipStream_t s);
 hipError_t launch_topn_sort(TopCand *cand, uint32_t m, const uint64_t *currents,
                             uint64_t *top_cur, hipStream_t s);

@@ -1394,11 +1394,50 @@ __device__ void final_top(uint64_t pool, const uint64_t *currents, uint32_t nb,
   }
 }
 
+// Spikes of a neuron in the derived state: the LIF from (v, r) = (0, 0) of
+// its count (k_lif_apply's fresh branch).
+__device__ __forceinline__ uint64_t fresh_spikes(uint64_t cnt, const LifParams &lp,
+                                                 const LifEntry *tbl, int tbl_n, float &v,
+                                                 uint32_t &r) {
+  v = 0.0f;
+  r = 0u;
+  if ((lp.skip_zero && cnt == 0) || lp.steps == 0) return 0;
+  if (cnt < (uint64_t)tbl_n) {
+    const LifEntry e = tbl[cnt];
+    v = e.v;
+    r = e.r;
+    return e.spikes;
+  }
+  return lif_closed(lif_current(cnt, lp.steps), lp.steps, lp.thr, lp.leak, lp.refr, v, r);
+}
+
+__device__ __forceinline__ uint64_t spikes_at(const SpikeSrc &s, uint64_t i) {
+  if (s.sc) return s.sc[i];
+  float v;
+  uint32_t r;
+  return fresh_spikes(s.cur[i], s.lp, s.tbl, s.tbl_n, v, r);
+}
+
+// the derived state written out (materialised): v / r / spike counts
+__global__ void k_lif_derive(const uint64_t *__restrict__ cur, float *__restrict__ V,
+                             uint32_t *__restrict__ R, uint64_t *__restrict__ SC, uint64_t pool,
+                             LifParams lp, const LifEntry *__restrict__ tbl, int tbl_n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < pool;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    float v;
+    uint32_t r;
+    const uint64_t sp = fresh_spikes(cur[i], lp, tbl, tbl_n, v, r);
+    V[i] = v;
+    R[i] = r;
+    SC[i] = sp;
+  }
+}
+
 __global__ __launch_bounds__(kLifBlock) void k_lif_apply(uint64_t *__restrict__ currents,
                                                       const uint32_t *__restrict__ partials,
                                                       uint32_t slices, int cur_zero,
                                                       const uint32_t *__restrict__ over,
-                                                      int over_bits, int fresh,
+                                                      int over_bits, int fresh, int derive,
                                                       float *__restrict__ V,
                                                       uint32_t *__restrict__ R,
                                                       uint64_t *__restrict__ SC, uint64_t pool,
@@ -1470,12 +1509,14 @@ __global__ __launch_bounds__(kLifBlock) void k_lif_apply(uint64_t *__restrict__ 
       } else {
         sp = lif_closed(lif_current(cnt, lp.steps), lp.steps, lp.thr, lp.leak, lp.refr, v, r);
       }
-      V[i] = v;
-      R[i] = r;
       sc += sp;
-      SC[i] = sc;
+      if (!(fresh && derive)) {  // derived: a function of the count, not written
+        V[i] = v;
+        R[i] = r;
+        SC[i] = sc;
+      }
       my_sp += sp;
-    } else if (fresh) {
+    } else if (fresh && !derive) {
       V[i] = 0.0f;
       R[i] = 0u;
       SC[i] = 0;
@@ -1576,7 +1617,7 @@ __global__ __launch_bounds__(1024) void k_topn_threshold(const uint32_t *__restr
 
 // 256-bin histogram of digit (sc >> shift) & 255 over neurons whose higher bits
 // equal `prefix` (radix refine for spike counts >= 4095; rare path).
-__global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t *__restrict__ sc, uint64_t pool,
+__global__ __launch_bounds__(kBlock) void k_radix_hist(SpikeSrc sc, uint64_t pool,
                                                        int shift, uint64_t prefix,
                                                        uint32_t *__restrict__ h256) {
   __shared__ uint32_t sh[256];
@@ -1584,7 +1625,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t *__restric
   __syncthreads();
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < pool;
        i += (uint64_t)gridDim.x * kBlock) {
-    uint64_t v = sc[i];
+    uint64_t v = spikes_at(sc, i);
     uint64_t hi = (shift + 8 >= 64) ? 0 : (v >> (shift + 8));
     if (hi == prefix) atomicAdd(&sh[(v >> shift) & 255], 1u);
   }
@@ -1596,7 +1637,7 @@ constexpr int kTopChunk = kBlock * 8;  // neurons per block in count/emit
 
 // one pass over the spike counts: the rows above T are emitted (any order:
 // k_topn_sort orders them) and each block's ties (== T) counted
-__global__ __launch_bounds__(kBlock) void k_topn_count(const uint64_t *__restrict__ sc,
+__global__ __launch_bounds__(kBlock) void k_topn_count(SpikeSrc sc,
                                                        uint64_t pool, TopState *__restrict__ st,
                                                        uint32_t *__restrict__ tie_cnt,
                                                        TopCand *__restrict__ cand) {
@@ -1607,7 +1648,7 @@ __global__ __launch_bounds__(kBlock) void k_topn_count(const uint64_t *__restric
   for (int j = 0; j < 8; ++j) {
     const uint64_t i = base + (uint64_t)j * kBlock + threadIdx.x;
     if (i >= pool) break;
-    const uint64_t v = sc[i];
+    const uint64_t v = spikes_at(sc, i);
     if (v == T) ++c;
     if (v > T && T != ~0ULL) {
       const unsigned long long pos = atomicAdd((unsigned long long *)&st->emit_above, 1ull);
@@ -1657,7 +1698,7 @@ __global__ __launch_bounds__(1024) void k_tie_scan(uint32_t *__restrict__ cnt, u
 // the first `need` ties in index order (the rows above T were emitted by
 // k_topn_count): only blocks whose earlier ties fall short of `need` read
 // their spike counts
-__global__ __launch_bounds__(kBlock) void k_topn_emit(const uint64_t *__restrict__ sc,
+__global__ __launch_bounds__(kBlock) void k_topn_emit(SpikeSrc sc,
                                                       uint64_t pool, TopState *__restrict__ st,
                                                       const uint32_t *__restrict__ tie_cnt,
                                                       TopCand *__restrict__ cand) {
@@ -1672,7 +1713,7 @@ __global__ __launch_bounds__(kBlock) void k_topn_emit(const uint64_t *__restrict
   uint64_t v[8];
   for (int j = 0; j < 8; ++j) {
     uint64_t i = base + j;
-    v[j] = i < pool ? sc[i] : 0;
+    v[j] = i < pool ? spikes_at(sc, i) : 0;
     if (i < pool && v[j] == T) ++ties;
   }
   s_scan[threadIdx.x] = ties;
@@ -1969,15 +2010,26 @@ uint32_t lif_blocks(uint64_t pool) {
   return (uint32_t)((pool + per - 1) / per);
 }
 
+hipError_t launch_lif_derive(const uint64_t *currents, float *v, uint32_t *r, uint64_t *sc,
+                             uint64_t pool, LifParams lp, const LifEntry *tbl, int tbl_n,
+                             hipStream_t s) {
+  if (!pool) return hipSuccess;
+  unsigned g = (unsigned)((pool + 255) / 256);
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(k_lif_derive, dim3(g), dim3(256), 0, s, currents, v, r, sc, pool, lp, tbl, tbl_n);
+  return hipGetLastError();
+}
+
 hipError_t launch_lif_apply(uint64_t *currents, const uint32_t *partials, uint32_t slices,
-                            int cur_zero, const uint32_t *over, int over_bits, int fresh, float *v, uint32_t *r, uint64_t *sc, uint64_t pool, LifParams lp,
+                            int cur_zero, const uint32_t *over, int over_bits, int fresh, int derive,
+                            float *v, uint32_t *r, uint64_t *sc, uint64_t pool, LifParams lp,
                             const LifEntry *tbl, int tbl_n, uint32_t *hist, uint64_t *stats,
                             const TopFuse &tf, hipStream_t s) {
   if (!pool) return hipSuccess;
   const unsigned g = lif_blocks(pool);
   if (tf.want && (tf.want > kFuseMaxTopN || g > kFuseMaxBlocks || pool > (1ull << 24)))
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_lif_apply, dim3(g), dim3(kLifBlock), 0, s, currents, partials, slices, cur_zero, over, over_bits, fresh,
+  hipLaunchKernelGGL(k_lif_apply, dim3(g), dim3(kLifBlock), 0, s, currents, partials, slices, cur_zero, over, over_bits, fresh, derive,
                      v, r, sc, pool, lp, tbl, tbl_n, hist, (unsigned long long *)stats, tf);
   if (tf.want)
     hipLaunchKernelGGL(k_top_final, dim3(1), dim3(kLifBlock), 0, s, pool, currents, g, tf);
@@ -1990,7 +2042,7 @@ hipError_t launch_topn_threshold(const uint32_t *hist, uint64_t n, uint64_t pool
   return hipGetLastError();
 }
 
-hipError_t launch_radix_hist(const uint64_t *sc, uint64_t pool, int shift, uint64_t prefix,
+hipError_t launch_radix_hist(const SpikeSrc &sc, uint64_t pool, int shift, uint64_t prefix,
                              uint32_t *h256, hipStream_t s) {
   unsigned g = (unsigned)((pool + kBlock * 8 - 1) / (kBlock * 8));
   if (g > 2048) g = 2048;
@@ -2003,7 +2055,7 @@ static unsigned topn_blocks(uint64_t pool) {
   return (unsigned)((pool + kTopChunk - 1) / kTopChunk);
 }
 
-hipError_t launch_topn_count(const uint64_t *sc, uint64_t pool, TopState *st,
+hipError_t launch_topn_count(const SpikeSrc &sc, uint64_t pool, TopState *st,
                              uint32_t *tie_cnt, TopCand *cand, hipStream_t s) {
   if (!pool) return hipSuccess;
   hipLaunchKernelGGL(k_topn_count, dim3(topn_blocks(pool)), dim3(kBlock), 0, s, sc, pool, st,
@@ -2012,7 +2064,7 @@ hipError_t launch_topn_count(const uint64_t *sc, uint64_t pool, TopState *st,
   return hipGetLastError();
 }
 
-hipError_t launch_topn_emit(const uint64_t *sc, uint64_t pool, TopState *st,
+hipError_t launch_topn_emit(const SpikeSrc &sc, uint64_t pool, TopState *st,
                             const uint32_t *tie_cnt, TopCand *cand, hipStream_t s) {
   if (!pool) return hipSuccess;
   hipLaunchKernelGGL(k_topn_emit, dim3(topn_blocks(pool)), dim3(kBlock), 0, s, sc, pool, st,
