@@ -445,7 +445,8 @@ def main() -> int:
         # the limiter, measured in this run: the same GPU's rate for the hash
         # work alone (SipHash-1-3 + exact % pool of register-generated keys, no
         # memory traffic: nk_diag_hash_ms) against K1a's k-mer rate
-        floor_ms = diag_hash_ms(nk_rank, pool, dev_idx, reps=5) if args.kmer_width == 64 else None
+        floor_ms = diag_hash_ms(nk_rank, pool, dev_idx, reps=5, width=args.kmer_width) \
+            if pool < (1 << 30) else None
         valu = {"kmers_per_launch": nk_rank,
                 "k1a_gkmers_per_s": round(nk_rank / (k1_ms * 1e-3) / 1e9, 2)}
         if floor_ms:

@@ -377,6 +377,9 @@ int nk_count_spans(nk_counter *c, float *ms, int cap);
  * hash work with no memory traffic).  Measures the VALU floor of the count
  * kernel live on the device.  (No reference counterpart.) */
 int nk_diag_hash_ms(int device, uint64_t n_keys, uint64_t pool, int reps, float *ms);
+/* The same for width 128: SipHash-1-3 over 16-byte keys (NK_KMER_128, the
+ * config-5 count kernel's hash), or 64.  (No reference counterpart.) */
+int nk_diag_hash_ms_w(int device, uint64_t n_keys, uint64_t pool, int width, int reps, float *ms);
 
 /* ---- associative memory (src/associative.rs) -------------
  * WillshawNetwork — :12-62.  Binary weights of pattern_size^2 bits on the

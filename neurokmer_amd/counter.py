@@ -319,9 +319,10 @@ class SpikingKmerCounter:
         return [float(buf[i]) for i in range(m)]
 
 
-def diag_hash_ms(n_keys: int, pool: int, device: int = 0, reps: int = 5) -> float:
+def diag_hash_ms(n_keys: int, pool: int, device: int = 0, reps: int = 5, width: int = 64) -> float:
     """Best device time (ms) of SipHash-1-3 + exact % pool over n_keys keys
-    generated in registers: the count kernel's hash floor (nk_diag_hash_ms)."""
+    generated in registers (width 128: 16-byte keys): the count kernel's hash
+    floor (nk_diag_hash_ms_w)."""
     ms = C.c_float(0.0)
-    _lib.check(_lib.load().nk_diag_hash_ms(device, n_keys, pool, reps, C.byref(ms)))
+    _lib.check(_lib.load().nk_diag_hash_ms_w(device, n_keys, pool, width, reps, C.byref(ms)))
     return float(ms.value)

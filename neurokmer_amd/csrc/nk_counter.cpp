@@ -171,6 +171,9 @@ struct nk_counter {
   // wide partition (pool > 16.7 M or big-key modes past it): coarse buckets
   DevBuf<uint32_t> w_rec, w_over;
   DevBuf<unsigned long long> w_fill;
+  // overflow target of a write-through K1b (PartArgs::out), kept zero
+  DevBuf<unsigned long long> ovf;
+  size_t ovf_zeroed = 0;  // entries known zero
   uint32_t pend_slices = 0;  // K1b partials not yet folded into cur (fused into LIF)
   bool cur_in_wire = false;  // nk_wire32 moved the currents into the caller's wire vector
   // multi-GPU export (nk_finalize_export -> nk_merge_export -> [nk_finalize_redo])
@@ -193,6 +196,10 @@ struct nk_counter {
   // and the closed-form table give them back (settle_state writes them out)
   bool state_derived = false;
   LifParams derived_lp{};
+  // min(spike count, 255) per neuron, written by a LIF whose top-N is not fused
+  // (large pools): what the top-N passes read first (1 B instead of 8 per neuron)
+  DevBuf<uint8_t> sc8;
+  bool sc8_ok = false;
   bool cur_fresh = true;     // currents are logically zero (lazy reset)
   // exact k-mer table (opts.exact_counts, nk_exact.h)
   DevBuf<uint64_t> x_keys, x_sorted, x_uniq, x_q;
@@ -239,6 +246,16 @@ struct nk_counter {
   DevBuf<uint32_t> bcnt;
   bool part_used = false;
   int gen_km = -1;  // key mode of the last count when it ran k_part_gen (Gen/Wide), else -1
+  // Gen/Wide count of one batch: its k_part_gen records and segment
+  // descriptors are kept, so the uniques pass rescans only the tiles holding
+  // the top rows' records (k_uniq_tiles) instead of the whole input
+  bool gen_keep = false;
+  bool gen_wide = false;
+  GenPartArgs last_ga{};
+  DevBuf<uint32_t> u_tiles, u_nt;
+  DevBuf<uint32_t> u_mark;  // per tile: the last pass that listed it (zeroed when allocated)
+  size_t u_mark_zeroed = 0;
+  uint32_t u_epoch = 0;
   // input of the last accumulate (for the uniques pass)
   KmerInput last_in{};
   bool have_input = false;
@@ -331,6 +348,7 @@ static int zero_state_on(nk_counter *c, hipStream_t) {
   c->sliced = false;
   c->max_sc = 0;
   c->state_derived = false;
+  c->sc8_ok = false;
   return NK_OK;
 }
 
@@ -347,6 +365,7 @@ static int settle_state(nk_counter *c, hipStream_t s) {
 // spike counts of neurons [lo, ...) as the top-N passes read them
 static SpikeSrc spike_src(const nk_counter *c, uint64_t lo) {
   SpikeSrc x{};
+  if (c->sc8_ok) x.sc8 = c->sc8.p + lo;
   if (c->state_derived) {
     x.cur = c->cur.p + lo;
     x.tbl = c->lif_tbl.p;
@@ -377,6 +396,7 @@ static int materialize(nk_counter *c, bool currents, hipStream_t s) {
     c->cur_fresh = false;
   }
   if (!currents && c->state_fresh) {
+    c->sc8_ok = false;
     z.ptr[z.n] = c->sc.p; z.bytes[z.n++] = c->pool * 8;
     z.ptr[z.n] = c->v.p;  z.bytes[z.n++] = c->pool * 4;
     z.ptr[z.n] = c->r.p;  z.bytes[z.n++] = c->pool * 4;
@@ -793,7 +813,7 @@ static uint64_t count_chunk() {
 // records per bucket region; max_segs: Part's descriptors per bucket) and
 // lists the arrays to zero before the first batch.
 static int plan_count(nk_counter *c, uint64_t est_bases, uint64_t slack, uint64_t max_segs,
-                      CountPlan &cp, ZeroList &z) {
+                      CountPlan &cp, ZeroList &z, bool keep_gen = false) {
   cp = CountPlan{};
   const uint64_t P = c->pool;
   if (!P) return NK_OK;
@@ -867,6 +887,12 @@ static int plan_count(nk_counter *c, uint64_t est_bases, uint64_t slack, uint64_
   if (cp.path == CountPath::Gen)
     cp.ga = GenPartArgs{(uint32_t)B, kBinBits, cap, c->p_off.p, c->p_fill.p, c->p_over.p,
                         (unsigned long long *)c->cur.p};
+  if (keep_gen && (cp.path == CountPath::Gen || cp.path == CountPath::Wide)) {
+    // segment descriptors of k_part_gen's buckets (coarse ones when wide)
+    if ((rc = c->p_desc.ensure((uint64_t)cp.ga.n_buckets * max_segs))) return rc;
+    cp.ga.desc = c->p_desc.p;
+    cp.ga.max_segs = max_segs;
+  }
   z.ptr[z.n] = c->p_fill.p; z.bytes[z.n++] = B * 8;
   z.ptr[z.n] = c->p_over.p; z.bytes[z.n++] = B * 4;
   return NK_OK;
@@ -939,18 +965,38 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
   // one prep kernel: tile -> first record index, and every buffer the count
   // (and, for a process call, the LIF) accumulates into zeroed
   ZeroList z{};
-  z.ptr[z.n] = c->cur.p; z.bytes[z.n++] = c->pool * 8;
   CountPlan cp;
   // bucket regions: 1.25x the fair share + one tile of slack (overflow is
   // still exact: the excess is counted with direct atomics); past
   // count_chunk() positions the regions hold one batch at a time
   const uint64_t chunk = count_chunk();
   const uint64_t est = std::min<uint64_t>(n_bases, chunk);
-  int rc = plan_count(c, est, kPartTile, n_tiles_for(est, kPartTile), cp, z);
+  int rc = plan_count(c, est, kPartTile, n_tiles_for(est, kPartTile), cp, z,
+                     /*keep_gen=*/n_bases <= chunk);
   if (rc) return rc;
   in.n_tiles = n_tiles_for(n_bases, cp.tile);
   const bool batched = cp.path != CountPath::Atomic && n_bases > chunk;
   const uint64_t batch_tiles = chunk / kPartTile;  // cp.tile == kPartTile on the partitioned paths
+  // Gen/Wide with one K1b workgroup per bucket and one batch: K1b writes every
+  // bin of the currents (write-through), so they are neither zeroed nor read;
+  // region overflow goes to the kept-zero ovf array, which K1b folds back
+  const bool wt = !batched && (cp.path == CountPath::Gen || cp.path == CountPath::Wide) &&
+                  cp.slices == 1 && in.n_tiles > 0 && !getenv("NK_NO_WRITE_THROUGH");
+  if (wt) {
+    if (c->ovf.n < c->pool || c->ovf_zeroed < c->pool) {
+      if ((rc = c->ovf.ensure(c->pool))) return rc;
+      HIPCHK(hipMemsetAsync(c->ovf.p, 0, c->pool * 8, s));
+      c->ovf_zeroed = c->pool;
+    }
+    cp.pa.currents = cp.ga.currents = c->ovf.p;
+    cp.pa.out = (unsigned long long *)c->cur.p;
+    if (cp.path == CountPath::Wide) {
+      cp.pa.over_coarse = cp.ga.overflow;
+      cp.pa.coarse_shift = (uint32_t)(cp.ga.bin_bits - kBinBits);
+    }
+  } else {
+    z.ptr[z.n] = c->cur.p; z.bytes[z.n++] = c->pool * 8;
+  }
   if ((rc = c->tile_rec.ensure(std::max<uint64_t>(batched ? batch_tiles : in.n_tiles, 1)))) return rc;
   in.tile_rec = c->tile_rec.p;
   const bool counted = cp.path != CountPath::Atomic && in.n_tiles > 0;
@@ -983,6 +1029,7 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
     HIPCHK(mark(c, 2, s));
     c->cur_fresh = false;
     c->part_used = false;
+    c->gen_keep = false;
     c->gen_km = cp.path == CountPath::Part ? -1 : cp.km;
     c->pend_slices = 0;
     HIPCHK(mark(c, 3, s));
@@ -994,6 +1041,9 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
   }
   c->part_used = counted && cp.path == CountPath::Part;
   c->gen_km = (cp.path == CountPath::Gen || cp.path == CountPath::Wide) ? cp.km : -1;
+  c->gen_keep = counted && c->gen_km >= 0 && cp.ga.desc && !getenv("NK_NO_GEN_KEEP");
+  c->gen_wide = cp.path == CountPath::Wide;
+  c->last_ga = cp.ga;
   if (cp.path == CountPath::Part && c->set_dirty && !c->w128 && z.n < kZeroMax) {
     // the uniques set, empty for this input's scan (k_uniq_scan inserts as it goes)
     z.ptr[z.n] = c->set_keys.p; z.bytes[z.n] = c->set_dirty * 8; z.fill[z.n++] = 0xFF;
@@ -1151,9 +1201,12 @@ static int enqueue_lif(nk_counter *c, int streaming, uint32_t fuse_want, bool pa
     tf.st = c->topst.p;
     tf.cand = c->cand.p;
     tf.top_cur = c->top_cur.p;
-    tf.post = PostArgs{c->set_alloc, part ? c->p_over.p : nullptr, part ? 1 : 0, c->set_mask_d.p,
-                       c->tbuckets.p, c->post_flags.p, c->uniq.p, c->special.p, c->n_hits.p,
-                       c->last_pa.bin_bits};
+    // kept records (Part, or Gen/Wide): the top buckets and their overflow
+    const bool gk = part && !c->part_used;
+    tf.post = PostArgs{c->set_alloc, part ? (gk ? c->last_ga.overflow : c->p_over.p) : nullptr,
+                       part ? 1 : 0, c->set_mask_d.p, c->tbuckets.p, c->post_flags.p, c->uniq.p,
+                       c->special.p, c->n_hits.p,
+                       gk ? (uint32_t)c->last_ga.bin_bits : c->last_pa.bin_bits};
   }
   // steps == 0: the kernel leaves every neuron as it is (streaming returns early,
   // src/spiking_hash.rs:549-551; in-memory runs zero iterations)
@@ -1167,11 +1220,13 @@ static int enqueue_lif(nk_counter *c, int streaming, uint32_t fuse_want, bool pa
   // partitioned count with its partials pending: the prep zeroed the currents and
   // only overflowed buckets added into them, so only those buckets are read
   const uint32_t *over = (!wire && c->pend_slices && c->part_used) ? c->p_over.p : nullptr;
+  if (!fuse_want && (rc = c->sc8.ensure(c->pool))) return rc;
   HIPCHK(launch_lif_apply(c->cur.p, wire ? wire : c->partials.p, wire ? 1u : c->pend_slices,
                           wire ? 1 : 0, over, (int)c->last_pa.bin_bits, c->state_fresh ? 1 : 0,
                           /*derive=*/1, c->v.p, c->r.p, c->sc.p, c->pool, lp, c->lif_tbl.p, kLifTable,
-                          c->hist.p, c->stats.p, tf, s));
+                          c->hist.p, c->stats.p, tf, s, fuse_want ? nullptr : c->sc8.p));
   c->pend_slices = 0;
+  c->sc8_ok = !fuse_want;
   if (c->pool && c->state_fresh) {  // from the reset state: v / r / spike counts derived
     c->state_derived = true;
     c->derived_lp = lp;
@@ -1195,14 +1250,21 @@ static int enqueue_select(nk_counter *c, uint64_t want, hipStream_t s, uint64_t 
   return NK_OK;
 }
 
+#ifndef NK_U1_SLICE_BUDGET
+#define NK_U1_SLICE_BUDGET 1024  // scan workgroups per launch (A/B: 1024 with 4 loads in flight best)
+#endif
 static int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, bool post_done,
                            hipStream_t s) {
   const bool part = c->part_used && !rescan;
+  const bool genk = c->gen_keep && !rescan;  // kept Gen/Wide records: rescan the hit tiles only
   int rc;
   if ((rc = c->tbuckets.ensure(m))) return rc;
-  if (!post_done) HIPCHK(launch_top_post(c->cand.p, c->top_cur.p, m, c->set_alloc, part ? c->p_over.p : nullptr,
-                         part ? 1 : 0, c->set_mask_d.p, c->tbuckets.p, c->post_flags.p, c->uniq.p,
-                         c->special.p, c->n_hits.p, c->last_pa.bin_bits, s));
+  if (!post_done)
+    HIPCHK(launch_top_post(c->cand.p, c->top_cur.p, m, c->set_alloc,
+                           part ? c->p_over.p : genk ? c->last_ga.overflow : nullptr,
+                           (part || genk) ? 1 : 0, c->set_mask_d.p, c->tbuckets.p, c->post_flags.p,
+                           c->uniq.p, c->special.p, c->n_hits.p,
+                           genk ? (uint32_t)c->last_ga.bin_bits : c->last_pa.bin_bits, s));
   // the set must be empty up to the pass's mask: after the count's prep it is
   c->dirty_before = c->set_clean ? 0 : c->set_alloc;
   if (!part || !c->set_clean)
@@ -1224,9 +1286,6 @@ static int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, bool post_don
     u.xcap = c->xport_cap;
   }
   if (part) {
-#ifndef NK_U1_SLICE_BUDGET
-#define NK_U1_SLICE_BUDGET 1024  // scan workgroups per launch (A/B: 1024 with 4 loads in flight best)
-#endif
     const uint32_t slices = std::max<uint32_t>(1, NK_U1_SLICE_BUDGET / m);
     HIPCHK(launch_part_uniques(c->last_in, (int)c->k, c->canonical, c->last_pa, u, c->tbuckets.p,
                                c->post_flags.p + 2, m, slices, s));
@@ -1237,7 +1296,29 @@ static int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, bool post_don
     if ((rc = c->tile_rec.ensure(std::max<uint64_t>(in.n_tiles, 1)))) return rc;
     in.tile_rec = c->tile_rec.p;
     HIPCHK(launch_tile_rec(in, tile, c->tile_rec.p, s));
-    if (c->gen_km >= 0)
+    if (genk) {
+      // the tiles holding the top rows' records, then the rescan of those only;
+      // a full list sets post flag 1 (-> settle_top redoes a full rescan)
+      const uint32_t kTileList = [] {  // NK_UNIQ_TILE_LIST (tests): a small list overflows
+        const char *e = getenv("NK_UNIQ_TILE_LIST");
+        const unsigned long v = e ? strtoul(e, nullptr, 10) : 0;
+        return v ? (uint32_t)v : (1u << 20);
+      }();
+      if ((rc = c->u_tiles.ensure(kTileList)) || (rc = c->u_nt.ensure(1))) return rc;
+      if (c->u_mark.n < in.n_tiles || c->u_mark_zeroed < in.n_tiles || ++c->u_epoch == 0) {
+        if ((rc = c->u_mark.ensure(in.n_tiles))) return rc;
+        HIPCHK(hipMemsetAsync(c->u_mark.p, 0, c->u_mark.n * 4, s));
+        c->u_mark_zeroed = c->u_mark.n;
+        c->u_epoch = 1;
+      }
+      HIPCHK(hipMemsetAsync(c->u_nt.p, 0, 4, s));
+      const uint32_t slices = std::max<uint32_t>(1, NK_U1_SLICE_BUDGET / m);
+      HIPCHK(launch_uniq_tiles(c->last_ga, c->gen_wide ? 1 : 0, u, c->tbuckets.p, c->post_flags.p + 2,
+                               m, slices, c->u_tiles.p, c->u_nt.p, kTileList, c->post_flags.p + 1,
+                               c->u_mark.p, c->u_epoch, s));
+      HIPCHK(launch_uniq_gen(in, (int)c->k, c->canonical, c->gen_km, c->pool, u, s, c->u_tiles.p,
+                             c->u_nt.p, kTileList));
+    } else if (c->gen_km >= 0)
       HIPCHK(launch_uniq_gen(in, (int)c->k, c->canonical, c->gen_km, c->pool, u, s));
     else if (c->w128)
       HIPCHK(launch_uniques128(in, (int)c->k, c->canonical, c->pool, u, s));
@@ -1305,7 +1386,8 @@ static int lif_top_uniques(nk_counter *c, int streaming, bool use_kpn, hipStream
   const bool uniq = want && c->have_input && c->last_in.n_tiles;
   // top-N selection (and the uniques post step) inside the LIF kernel
   const bool fused = top_fused(c, want);
-  if ((rc = enqueue_lif(c, streaming, fused ? (uint32_t)want : 0u, uniq && c->part_used, s, wire)))
+  if ((rc = enqueue_lif(c, streaming, fused ? (uint32_t)want : 0u,
+                        uniq && (c->part_used || c->gen_keep), s, wire)))
     return rc;
   HIPCHK(mark(c, 4, s));
   return finish_top(c, want, fused, uniq, use_kpn, s);
@@ -1788,7 +1870,9 @@ int nk_finalize_export(nk_counter *c, int streaming, const uint32_t *d_wire, uin
   }
   const bool fused = top_fused(c, want);
   if (fused) {  // enqueue only: the host waits once, in nk_merge_export
-    if ((rc = enqueue_lif(c, streaming, (uint32_t)want, uniq && c->part_used, s, d_wire))) return rc;
+    if ((rc = enqueue_lif(c, streaming, (uint32_t)want, uniq && (c->part_used || c->gen_keep), s,
+                          d_wire)))
+      return rc;
     HIPCHK(mark(c, 4, s));
     HIPCHK(mark(c, 5, s));
     c->xport_dst = d_seg;  // the pass appends each new key to the segment
@@ -1909,6 +1993,7 @@ int nk_finalize_slice(nk_counter *c, int streaming, const void *d_slice, int sli
   c->cur_fresh = false;
   c->top_valid = false;
   c->top_keys_ready = false;
+  if ((rc = c->sc8.ensure(c->pool))) return rc;
   if (n) {
     if (slice_bits == 64)
       HIPCHK(hipMemcpyAsync(c->cur.p + lo, d_slice, n * 8, hipMemcpyDeviceToDevice, s));
@@ -1916,8 +2001,9 @@ int nk_finalize_slice(nk_counter *c, int streaming, const void *d_slice, int sli
     HIPCHK(launch_lif_apply(c->cur.p + lo, w32 ? (const uint32_t *)d_slice : nullptr, w32 ? 1u : 0u,
                             w32 ? 1 : 0, nullptr, (int)c->last_pa.bin_bits, c->state_fresh ? 1 : 0,
                             /*derive=*/1, c->v.p + lo, c->r.p + lo, c->sc.p + lo, n, lp, c->lif_tbl.p,
-                            kLifTable, c->hist.p, c->stats.p, TopFuse{}, s));
+                            kLifTable, c->hist.p, c->stats.p, TopFuse{}, s, c->sc8.p + lo));
   }
+  c->sc8_ok = true;  // on [lo, hi), the only range this rank's passes read
   if (c->state_fresh) {  // derived on [lo, hi) (the rest of the pool is not this rank's)
     c->state_derived = true;
     c->derived_lp = lp;
@@ -2172,6 +2258,7 @@ static int acc_begin(nk_counter *c, uint64_t est_bases, uint64_t batch_bases, St
   c->cur_fresh = false;
   sa.keep = sa.cp.path == CountPath::Part && part_like;
   c->part_used = sa.keep;
+  c->gen_keep = false;
   c->gen_km = (sa.cp.path == CountPath::Gen || sa.cp.path == CountPath::Wide) ? sa.cp.km : -1;
   return NK_OK;
 }
@@ -2428,6 +2515,7 @@ int nk_process_sequence(nk_counter *c, const uint8_t *seq, size_t len) {
   z.ptr[1] = c->stats.p; z.bytes[1] = 16;
   z.n = 2;
   HIPCHK(launch_zero(z, s));
+  c->sc8_ok = false;
   HIPCHK(seq_lif(c->pool, (unsigned long long *)c->cur.p, c->touched.p, c->kpn.p, c->v.p, c->r.p,
                  c->sc.p, c->thr, c->leak, c->refr, c->hist.p, c->stats.p, s));
   c->have_input = false;  // no uniques pass: the column comes from kmer_per_neuron
@@ -2664,8 +2752,12 @@ int nk_copy_refractory(nk_counter *c, uint32_t *out, size_t n) {
 }
 
 int nk_diag_hash_ms(int device, uint64_t n_keys, uint64_t pool, int reps, float *ms) {
-  if (!ms || !n_keys || !pool || pool >= (1ull << 30) || reps < 1)
-    return fail(NK_E_INVALID, "nk_diag_hash_ms: n_keys, pool in [1, 2^30), reps >= 1, ms");
+  return nk_diag_hash_ms_w(device, n_keys, pool, 64, reps, ms);
+}
+
+int nk_diag_hash_ms_w(int device, uint64_t n_keys, uint64_t pool, int width, int reps, float *ms) {
+  if (!ms || !n_keys || !pool || pool >= (1ull << 30) || reps < 1 || (width != 64 && width != 128))
+    return fail(NK_E_INVALID, "nk_diag_hash_ms: n_keys, pool in [1, 2^30), width 64|128, reps >= 1, ms");
   if (hipSetDevice(device) != hipSuccess) return fail(NK_E_NO_DEVICE, "hipSetDevice failed");
   uint32_t *out = nullptr;
   hipStream_t s = nullptr;
@@ -2679,7 +2771,7 @@ int nk_diag_hash_ms(int device, uint64_t n_keys, uint64_t pool, int reps, float 
   }
   for (int i = 0; rc == NK_OK && i < reps + 1; ++i) {  // + 1 untimed warm-up
     float t = 0.0f;
-    if (hipEventRecord(a, s) != hipSuccess || launch_diag_hash(n_keys, pool, out, s) != hipSuccess ||
+    if (hipEventRecord(a, s) != hipSuccess || launch_diag_hash(n_keys, pool, out, s, width) != hipSuccess ||
         hipEventRecord(b, s) != hipSuccess || hipEventSynchronize(b) != hipSuccess ||
         hipEventElapsedTime(&t, a, b) != hipSuccess)
       rc = fail(NK_E_DEVICE, "diag hash kernel failed");

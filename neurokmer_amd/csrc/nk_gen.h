@@ -69,9 +69,10 @@ struct RecCursor {  // KM 1: the record holding the lane's current position
 };
 
 template <int KM>
-__device__ __forceinline__ void rec_cursor_init(RecCursor &c, const KmerInput &in, uint64_t p0) {
+__device__ __forceinline__ void rec_cursor_init(RecCursor &c, const KmerInput &in, uint64_t p0,
+                                                uint64_t ti) {  // ti: tile - in.tile_base
   if (KM != 1 || !in.n_recs) return;
-  c.r = rec_of(in.offsets, in.n_recs, in.tile_rec[blockIdx.x], p0);
+  c.r = rec_of(in.offsets, in.n_recs, in.tile_rec[ti], p0);
   c.s0 = in.offsets[c.r];
   c.e0 = in.offsets[c.r + 1];
 }

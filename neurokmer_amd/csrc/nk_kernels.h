@@ -37,6 +37,7 @@ struct LifEntry {  // closed-form result for a fresh neuron (v = 0, r = 0)
 // neuron's count alone (the "derived" state: v / refractory / spike counts
 // are not written) -- from the counts through the closed form.
 struct SpikeSrc {
+  const uint8_t *sc8;   // non-null: min(spikes, 255) per neuron, read first
   const uint64_t *sc;   // non-null: materialised spike counts
   const uint64_t *cur;  // derived: the counts
   const LifEntry *tbl;  // closed-form rows of fresh neurons (counts < tbl_n)
@@ -133,6 +134,14 @@ struct PartArgs {
   // launch (s_memrealtime, 100 MHz), folded with atomicMin / atomicMax by one
   // lane per workgroup: the kernel's duration without an event in the stream
   unsigned long long *span = nullptr;
+  // K1b write-through (one slice per bucket, one batch): every bin of the
+  // bucket is written to out (no zeroed or read-modified currents); the
+  // overflow target `currents` is then a separate array kept zero -- a bucket
+  // whose region (or, wide, whose coarse bucket's region) overflowed folds
+  // its entries in and zeroes them again
+  unsigned long long *out = nullptr;
+  const uint32_t *over_coarse = nullptr;  // wide: coarse overflow flags
+  uint32_t coarse_shift = 0;              // fine bucket -> coarse bucket
 };
 
 // Generic partition (nk_wide.hip): any key mode; narrow (u16 offsets into
@@ -149,6 +158,11 @@ struct GenPartArgs {
   unsigned long long *fill;       // [bucket] records reserved
   uint32_t *overflow;             // [bucket] region overflowed (counted directly)
   unsigned long long *currents;   // overflow target
+  // kept records (k_part_gen only): per (bucket, segment) {tile, first record},
+  // the segment count in fill's bits 40..; the uniques pass finds the tiles
+  // that hold a top row's records and rescans only those (k_uniq_tiles)
+  uint2 *desc = nullptr;
+  uint64_t max_segs = 0;
 };
 
 // keys handed to the uniques merge: a flat list (world == 0) or the
@@ -186,18 +200,22 @@ hipError_t launch_uniques(const KmerInput &in, int k, int canonical, uint64_t po
                           const UniqArgs &u, hipStream_t s);
 hipError_t launch_lif_table(LifEntry *tbl, int n, LifParams lp, hipStream_t s);
 // diagnostic: SipHash-1-3 + % pool of n_keys register-generated keys
-hipError_t launch_diag_hash(uint64_t n_keys, uint64_t pool, uint32_t *out, hipStream_t s);
+hipError_t launch_diag_hash(uint64_t n_keys, uint64_t pool, uint32_t *out, hipStream_t s,
+                            int width = 64);
 uint64_t diag_hash_out_words(uint64_t n_keys);
 // partials/slices: when slices > 0, currents[i] += sum of the K1b partials
 // first (the fused K1c of a single-device process call) and is written back.
 // fresh: v/r/sc are taken as 0 (lazy reset) and every neuron is written.
 // derive (with fresh): v / r / spike counts are not written (the derived
 // state, SpikeSrc); launch_lif_derive materialises them from the counts.
+// sc8 (non-fused top-N only): min(spikes, 255) of every neuron, the compact
+// copy the top-N passes read (the global histogram's bin 0 is not counted).
 hipError_t launch_lif_apply(uint64_t *currents, const uint32_t *partials, uint32_t slices,
                             int cur_zero, const uint32_t *over, int over_bits,
                             int fresh, int derive, float *v, uint32_t *r, uint64_t *sc, uint64_t pool,
                             LifParams lp, const LifEntry *tbl, int tbl_n, uint32_t *hist,
-                            uint64_t *stats, const TopFuse &tf, hipStream_t s);
+                            uint64_t *stats, const TopFuse &tf, hipStream_t s,
+                            uint8_t *sc8 = nullptr);
 hipError_t launch_lif_derive(const uint64_t *currents, float *v, uint32_t *r, uint64_t *sc,
                              uint64_t pool, LifParams lp, const LifEntry *tbl, int tbl_n,
                              hipStream_t s);
@@ -265,9 +283,19 @@ hipError_t launch_part(const KmerInput &in, int k, int canonical, uint64_t pool,
 // key mode km: 0 k <= 32 u64, 1 k > 32 compat, 2 --kmer-width=128
 hipError_t launch_part_gen(const KmerInput &in, int k, int canonical, int km, uint64_t pool,
                            const GenPartArgs &ga, int wide, hipStream_t s);
-// uniques rescan over kPartTile tiles for the Gen/Wide count paths
+// uniques rescan over kPartTile tiles for the Gen/Wide count paths; with a
+// tile list (tiles, *n_list <= max_list) only those tiles
 hipError_t launch_uniq_gen(const KmerInput &in, int k, int canonical, int km, uint64_t pool,
-                           const UniqArgs &u, hipStream_t s);
+                           const UniqArgs &u, hipStream_t s, const uint32_t *tiles = nullptr,
+                           const uint32_t *n_list = nullptr, uint32_t max_list = 0);
+// the tiles holding the records of the top rows' neurons in the kept Gen/Wide
+// records (ga.desc): the top buckets (tbuckets, *n_tb), `slices` workgroups per
+// bucket -> tiles[*n_list++] (deduplicated per workgroup); past max_list the
+// list is incomplete and flag[0] is set (the caller rescans the input)
+hipError_t launch_uniq_tiles(const GenPartArgs &ga, int wide, const UniqArgs &u,
+                             const uint32_t *tbuckets, const uint32_t *n_tb, uint32_t max_tb,
+                             uint32_t slices, uint32_t *tiles, uint32_t *n_list, uint32_t max_list,
+                             uint32_t *flag, uint32_t *mark, uint32_t epoch, hipStream_t s);
 hipError_t launch_split(const GenPartArgs &ga, const PartArgs &fine, hipStream_t s);
 // the exact table's kmer_per_neuron: a key array (wpk u64 words per key, *n_keys
 // of them on the device, at most max_n) hashed and partitioned like the count

@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+
+#include <algorithm>
 #include <type_traits>
 
 #include "nk_device.h"
@@ -311,7 +313,10 @@ __global__ __launch_bounds__(kBlock) void k_kmers128(KmerInput in, int k, FastMo
 // into the uniques set.
 template <int KM, bool CANON>
 __global__ __launch_bounds__(kPartBlock) void k_uniq_gen(KmerInput in, int k, FastMod fm,
-                                                         UniqArgs u) {
+                                                         UniqArgs u, const uint32_t *__restrict__ tiles,
+                                                         const uint32_t *__restrict__ n_list) {
+  // with a tile list: workgroup i takes the i-th listed tile (uniform exit past it)
+  if (tiles && blockIdx.x >= *n_list) return;
   constexpr bool kRaw = !CANON;
   __shared__ TileLds<kPartTile, kRaw> L;
   __shared__ unsigned long long seen[KM == 2 ? 1 : kSeen];
@@ -320,12 +325,12 @@ __global__ __launch_bounds__(kPartBlock) void k_uniq_gen(KmerInput in, int k, Fa
   uint32_t *tbl_slot = reinterpret_cast<uint32_t *>(dyn + u.tbl_size);
   if (KM != 2) seen_init(seen);
   build_top_tbl(u, tbl_idx, tbl_slot);  // contains __syncthreads
-  const uint64_t tile = in.tile_base + blockIdx.x;
+  const uint64_t tile = tiles ? (uint64_t)tiles[blockIdx.x] : in.tile_base + blockIdx.x;
   const uint64_t T0 = tile * (uint64_t)kPartTile;
   stage_tile<kPartTile, kPartBlock, kRaw>(L, in, tile, k);
   const int q0 = threadIdx.x * kPer;
   RecCursor rc;
-  rec_cursor_init<KM>(rc, in, T0 + (uint64_t)q0);
+  rec_cursor_init<KM>(rc, in, T0 + (uint64_t)q0, tile - in.tile_base);  // (listed tile: not blockIdx)
   for (int j = 0; j < kPer; ++j) {
     const int q = q0 + j;
     if (!window_valid(L, T0, q, k, in.n_bases, in.pos_lo, in.pos_hi)) continue;
@@ -773,6 +778,22 @@ __global__ __launch_bounds__(kHistBlock) void k_bucket_hist(PartArgs pa, uint64_
   __syncthreads();
   const uint64_t nb0 = (uint64_t)b << BB;
   const uint64_t nbins = pool - nb0 < (uint64_t)kBins ? pool - nb0 : kBins;
+  if (!partials && pa.out) {  // write-through: every bin, the overflow target folded + re-zeroed
+    const bool ov = pa.overflow[b] || (pa.over_coarse && pa.over_coarse[b >> pa.coarse_shift]);
+    unsigned long long *o = pa.out + nb0, *ovf = pa.currents + nb0;
+    for (uint32_t t = threadIdx.x; t < nbins; t += kHistBlock) {
+      unsigned long long x = h[t];
+      if (ov) {
+        const unsigned long long e = ovf[t];
+        if (e) {
+          x += e;
+          ovf[t] = 0;
+        }
+      }
+      o[t] = x;
+    }
+    return;
+  }
   if (!partials) {
     unsigned long long *cur = pa.currents + nb0;
     for (uint32_t t = threadIdx.x; t < nbins; t += kHistBlock) {
@@ -1412,6 +1433,10 @@ __device__ __forceinline__ uint64_t fresh_spikes(uint64_t cnt, const LifParams &
 }
 
 __device__ __forceinline__ uint64_t spikes_at(const SpikeSrc &s, uint64_t i) {
+  if (s.sc8) {  // 1 B per neuron; 255 means "255 or more": the exact value below
+    const uint32_t v = s.sc8[i];
+    if (v < 255u) return v;
+  }
   if (s.sc) return s.sc[i];
   float v;
   uint32_t r;
@@ -1445,7 +1470,7 @@ __global__ __launch_bounds__(kLifBlock) void k_lif_apply(uint64_t *__restrict__ 
                                                       const LifEntry *__restrict__ tbl, int tbl_n,
                                                       uint32_t *__restrict__ hist,
                                                       unsigned long long *__restrict__ stats,
-                                                      TopFuse tf) {
+                                                      TopFuse tf, uint8_t *__restrict__ sc8) {
   __shared__ uint32_t sh[kHistBins];
   __shared__ unsigned long long s_sp[kLifWaves];
   __shared__ unsigned long long s_mx[kLifWaves];
@@ -1522,6 +1547,7 @@ __global__ __launch_bounds__(kLifBlock) void k_lif_apply(uint64_t *__restrict__ 
       SC[i] = 0;
     }
     scv[j] = sc;
+    if (sc8) sc8[i] = sc < 255 ? (uint8_t)sc : (uint8_t)255;  // the top-N passes' compact copy
     my_mx = sc > my_mx ? sc : my_mx;
     // neurons that never spiked (most of a large pool) are counted in a
     // register: same-address LDS atomics of a whole wave serialise
@@ -1542,13 +1568,16 @@ __global__ __launch_bounds__(kLifBlock) void k_lif_apply(uint64_t *__restrict__ 
     unsigned long long a = 0, m = 0;
     for (int w = 0; w < kLifWaves; ++w) { a += s_sp[w]; m = s_mx[w] > m ? s_mx[w] : m; }
     if (a) atomicAdd(&stats[0], a);
-    atomicMax(&stats[1], m);
+    if (m) atomicMax(&stats[1], m);
   }
   // 8 copies of the global histogram (blocks b, b+8, ... share one), summed by
-  // the threshold step: the hot spike-count bins see 8x fewer atomics each
+  // the threshold step: the hot spike-count bins see 8x fewer atomics each.
+  // Bin 0 (never-spiking neurons: nearly all of a large pool) is not counted:
+  // the threshold step takes it as the rest of the pool, so no block sends an
+  // atomic to that one hot address
   if (!tf.want) {  // the separate top-N kernels read the global histogram
     uint32_t *hc = hist + (size_t)(blockIdx.x & (kHistCopies - 1)) * kHistBins;
-    for (int i = threadIdx.x; i < kHistBins; i += kLifBlock)
+    for (int i = threadIdx.x + 1; i < kHistBins; i += kLifBlock)
       if (sh[i]) atomicAdd(&hc[i], sh[i]);
     return;
   }
@@ -1577,10 +1606,18 @@ __global__ __launch_bounds__(1024) void k_topn_threshold(const uint32_t *__restr
                                                          TopState *__restrict__ st) {
   __shared__ unsigned long long part[1024];
   const int t = threadIdx.x;
-  // thread t owns bins [4095-4t-3, 4095-4t] i.e. counting from the top
+  // thread t owns bins [4095-4t-3, 4095-4t] i.e. counting from the top.  Bin
+  // 0 is not counted by the LIF: it holds the rest of the pool's neurons
+  auto bin_count = [&](int bin) -> unsigned long long {
+    unsigned long long h = 0;
+    for (int c = 0; c < kHistCopies; ++c) h += hist[c * kHistBins + bin];
+    return h;
+  };
   unsigned long long loc = 0;
-  for (int j = 0; j < 4; ++j)
-    for (int c = 0; c < kHistCopies; ++c) loc += hist[c * kHistBins + kHistBins - 1 - (4 * t + j)];
+  for (int j = 0; j < 4; ++j) {
+    const int bin = kHistBins - 1 - (4 * t + j);
+    if (bin) loc += bin_count(bin);
+  }
   part[t] = loc;
   __syncthreads();
   // inclusive scan over threads (Hillis-Steele; 10 steps)
@@ -1596,13 +1633,14 @@ __global__ __launch_bounds__(1024) void k_topn_threshold(const uint32_t *__restr
     if (t == 0) { st->T = ~0ULL; st->n_above = 0; st->need = 0; st->emit_above = 0; st->refine = 0; }
     return;
   }
-  if (before < want && part[t] >= want) {
+  const unsigned long long spiking = part[1023];  // neurons in bins >= 1
+  // the thread whose bins reach `want` (t = 1023 also when only bin 0 can)
+  if (before < want && (part[t] >= want || (t == 1023 && spiking < want))) {
     unsigned long long cum = before;
     for (int j = 0; j < 4; ++j) {
       int bin = kHistBins - 1 - (4 * t + j);
-      unsigned long long h = 0;
-      for (int c = 0; c < kHistCopies; ++c) h += hist[c * kHistBins + bin];
-      if (cum + h >= want) {
+      const unsigned long long h = bin ? bin_count(bin) : (pool > spiking ? pool - spiking : 0ull);
+      if (cum + h >= want || bin == 0) {
         st->T = (uint64_t)bin;
         st->n_above = cum;
         st->need = want - cum;
@@ -2024,13 +2062,13 @@ hipError_t launch_lif_apply(uint64_t *currents, const uint32_t *partials, uint32
                             int cur_zero, const uint32_t *over, int over_bits, int fresh, int derive,
                             float *v, uint32_t *r, uint64_t *sc, uint64_t pool, LifParams lp,
                             const LifEntry *tbl, int tbl_n, uint32_t *hist, uint64_t *stats,
-                            const TopFuse &tf, hipStream_t s) {
+                            const TopFuse &tf, hipStream_t s, uint8_t *sc8) {
   if (!pool) return hipSuccess;
   const unsigned g = lif_blocks(pool);
   if (tf.want && (tf.want > kFuseMaxTopN || g > kFuseMaxBlocks || pool > (1ull << 24)))
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_lif_apply, dim3(g), dim3(kLifBlock), 0, s, currents, partials, slices, cur_zero, over, over_bits, fresh, derive,
-                     v, r, sc, pool, lp, tbl, tbl_n, hist, (unsigned long long *)stats, tf);
+                     v, r, sc, pool, lp, tbl, tbl_n, hist, (unsigned long long *)stats, tf, sc8);
   if (tf.want)
     hipLaunchKernelGGL(k_top_final, dim3(1), dim3(kLifBlock), 0, s, pool, currents, g, tf);
   return hipGetLastError();
@@ -2102,22 +2140,27 @@ static hipError_t launch_kmers128(const KmerInput &in, int k, int canonical, uin
   return hipGetLastError();
 }
 hipError_t launch_uniq_gen(const KmerInput &in, int k, int canonical, int km, uint64_t pool,
-                           const UniqArgs &u, hipStream_t s) {
+                           const UniqArgs &u, hipStream_t s, const uint32_t *tiles,
+                           const uint32_t *n_list, uint32_t max_list) {
   if (!in.n_tiles) return hipSuccess;
   if (km < 0 || km > 2 || k < 1 || k > 64 || (km == 0 && k > 32) || (km == 1 && k <= 32))
     return hipErrorInvalidValue;
   const FastMod fm = make_fastmod(pool);
-  const dim3 g((unsigned)in.n_tiles), b(kPartBlock);
+  const uint64_t nb = tiles ? std::min<uint64_t>(max_list, in.n_tiles) : in.n_tiles;
+  if (!nb) return hipSuccess;
+  const dim3 g((unsigned)nb), b(kPartBlock);
   const size_t dyn = tbl_bytes(u);
+#define NK_UG(KM_, C_) hipLaunchKernelGGL((k_uniq_gen<KM_, C_>), g, b, dyn, s, in, k, fm, u, tiles, n_list)
   if (canonical) {
-    if (km == 0) hipLaunchKernelGGL((k_uniq_gen<0, true>), g, b, dyn, s, in, k, fm, u);
-    else if (km == 1) hipLaunchKernelGGL((k_uniq_gen<1, true>), g, b, dyn, s, in, k, fm, u);
-    else hipLaunchKernelGGL((k_uniq_gen<2, true>), g, b, dyn, s, in, k, fm, u);
+    if (km == 0) NK_UG(0, true);
+    else if (km == 1) NK_UG(1, true);
+    else NK_UG(2, true);
   } else {
-    if (km == 0) hipLaunchKernelGGL((k_uniq_gen<0, false>), g, b, dyn, s, in, k, fm, u);
-    else if (km == 1) hipLaunchKernelGGL((k_uniq_gen<1, false>), g, b, dyn, s, in, k, fm, u);
-    else hipLaunchKernelGGL((k_uniq_gen<2, false>), g, b, dyn, s, in, k, fm, u);
+    if (km == 0) NK_UG(0, false);
+    else if (km == 1) NK_UG(1, false);
+    else NK_UG(2, false);
   }
+#undef NK_UG
   return hipGetLastError();
 }
 
@@ -2394,6 +2437,9 @@ namespace nk {
 // but one store per thread.  nk_diag_hash_ms times it: the VALU floor of K1a.
 // ---------------------------------------------------------------------------
 constexpr int kDiagPer = 64;
+// W128: SipHash-1-3 of 16-byte keys (--kmer-width=128, the config-5 count's
+// hash: K1g's floor), else of u64 keys (K1a's)
+template <bool W128>
 __global__ __launch_bounds__(256) void k_diag_hash(FastMod fm, uint64_t n_keys,
                                                    uint32_t *__restrict__ out) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2402,17 +2448,23 @@ __global__ __launch_bounds__(256) void k_diag_hash(FastMod fm, uint64_t n_keys,
   const uint64_t first = t * kDiagPer;
 #pragma unroll 16
   for (int i = 0; i < kDiagPer; ++i) {
-    if (first + (uint64_t)i < n_keys) acc ^= fastmod32(sip13_u64(key), fm);
+    if (first + (uint64_t)i < n_keys)
+      acc ^= fastmod32(W128 ? sip13_u128(key, key >> 17) : sip13_u64(key), fm);
     key += 0xD1B54A32D192ED03ull;
   }
   out[t] = acc;
 }
 
-hipError_t launch_diag_hash(uint64_t n_keys, uint64_t pool, uint32_t *out, hipStream_t s) {
+hipError_t launch_diag_hash(uint64_t n_keys, uint64_t pool, uint32_t *out, hipStream_t s,
+                            int width) {
   const uint64_t threads = (n_keys + kDiagPer - 1) / kDiagPer;
   const uint64_t blocks = (threads + 255) / 256;
-  hipLaunchKernelGGL(k_diag_hash, dim3((uint32_t)blocks), dim3(256), 0, s, make_fastmod(pool),
-                     n_keys, out);
+  if (width == 128)
+    hipLaunchKernelGGL(k_diag_hash<true>, dim3((uint32_t)blocks), dim3(256), 0, s,
+                       make_fastmod(pool), n_keys, out);
+  else
+    hipLaunchKernelGGL(k_diag_hash<false>, dim3((uint32_t)blocks), dim3(256), 0, s,
+                       make_fastmod(pool), n_keys, out);
   return hipGetLastError();
 }
 

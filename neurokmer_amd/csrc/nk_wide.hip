@@ -58,7 +58,9 @@ __device__ __forceinline__ void sort_and_store(const uint32_t (&E)[PER], const u
                                                uint32_t *__restrict__ overflow, uint64_t cap,
                                                typename GenShape<WIDE>::Rec *__restrict__ dst_rec,
                                                uint64_t bucket_base, int bin_bits,
-                                               unsigned long long *__restrict__ currents) {
+                                               unsigned long long *__restrict__ currents,
+                                               uint2 *__restrict__ desc = nullptr,
+                                               uint64_t max_segs = 0, uint32_t tile = 0) {
   using S = GenShape<WIDE>;
   using Rec = typename S::Rec;
   const int tid = threadIdx.x;
@@ -82,9 +84,18 @@ __device__ __forceinline__ void sort_and_store(const uint32_t (&E)[PER], const u
     const uint32_t c = (s_cnt[b] + 7u) & ~7u;
     uint32_t fit = 0, base = 0;
     if (c) {
-      const uint64_t eb = atomicAdd(&fill[bucket_base + b], (unsigned long long)c);
+      // kept records: one segment per (tile, bucket), counted in bits 40..
+      const unsigned long long ret =
+          atomicAdd(&fill[bucket_base + b], (unsigned long long)c | (desc ? (1ull << 40) : 0ull));
+      const uint64_t eb = ret & ((1ull << 40) - 1);
       fit = eb >= cap ? 0u : (uint32_t)(cap - eb < c ? cap - eb : c);
-      if (fit < c) overflow[bucket_base + b] = 1u;
+      bool over = fit < c;
+      if (desc) {
+        const uint64_t seg = ret >> 40;
+        if (seg < max_segs) desc[(bucket_base + b) * max_segs + seg] = make_uint2(tile, (uint32_t)eb);
+        else over = true;  // (the uniques of this bucket fall back to the rescan)
+      }
+      if (over) overflow[bucket_base + b] = 1u;
       base = (uint32_t)eb;
     }
     s_base[b] = base;
@@ -155,13 +166,14 @@ __global__ __launch_bounds__(kPartBlock) void k_part_gen(KmerInput in, int k, Fa
   const uint64_t T0 = tile * (uint64_t)kPartTile;
   const uint32_t nb = ga.n_buckets;
   const int bb = ga.bin_bits;
+  const bool small_pool = fm.p < (1ull << 30);  // the 32-bit modulo (nk_device.h) holds
   const uint32_t omask = (uint32_t)((1ull << bb) - 1ull);
   for (uint32_t b = tid; b <= nb; b += kPartBlock) s_cnt[b] = 0;
   stage_tile<kPartTile, kPartBlock, kRaw>(L, in, tile, k);  // syncs
 
   const int q0 = tid * kPer;
   RecCursor rc;
-  rec_cursor_init<KM>(rc, in, T0 + (uint64_t)q0);
+  rec_cursor_init<KM>(rc, in, T0 + (uint64_t)q0, blockIdx.x);
   uint32_t E[kPer], O[kPer];
 #pragma unroll 2
   for (int j = 0; j < kPer; ++j) {
@@ -169,14 +181,14 @@ __global__ __launch_bounds__(kPartBlock) void k_part_gen(KmerInput in, int k, Fa
     const bool ok = window_valid(L, T0, q, k, in.n_bases, in.pos_lo, in.pos_hi);
     uint64_t h = 0;
     if (ok) h = gen_hash<KM>(gen_key<KM, CANON>(L, in, q, T0 + (uint64_t)q, k, rc));
-    const uint32_t idx = (uint32_t)fastmod(h, fm);
+    const uint32_t idx = small_pool ? fastmod32(h, fm) : (uint32_t)fastmod(h, fm);
     const uint32_t b = ok ? (idx >> bb) : nb;
     E[j] = (b << 16) | atomicAdd(&s_cnt[b], 1u);
     O[j] = idx & omask;
   }
   sort_and_store<WIDE, kPer>(E, O, nb, s_cnt, s_start, s_base, s_fit, s_rec, s_gmap, ga.fill,
                              ga.overflow, ga.cap, reinterpret_cast<typename S::Rec *>(ga.rec), 0,
-                             bb, ga.currents);
+                             bb, ga.currents, ga.desc, ga.max_segs, (uint32_t)tile);
 }
 
 // K1s: one 8192-record tile of a coarse bucket (u32 offsets of 2^S bins) ->
@@ -191,7 +203,7 @@ __global__ __launch_bounds__(kPartBlock) void k_split(GenPartArgs ga, PartArgs p
   __shared__ S::GMap s_gmap[S::kGroups];
   const int tid = threadIdx.x;
   const uint32_t cb = blockIdx.y;
-  uint64_t n = ga.fill[cb];
+  uint64_t n = ga.fill[cb] & ((1ull << 40) - 1);  // (bits 40..: kept segments)
   if (n > ga.cap) n = ga.cap;
   const uint64_t t0 = (uint64_t)blockIdx.x * kPartTile;
   if (t0 >= n) return;  // uniform
@@ -223,6 +235,73 @@ __global__ __launch_bounds__(kPartBlock) void k_split(GenPartArgs ga, PartArgs p
                               pa.currents);
 }
 
+// U1g: the tiles that hold records of the top rows in the kept Gen/Wide
+// records.  One workgroup per (top bucket, slice): the bucket's records are
+// matched against its top offsets; a hit's segment (binary search of the
+// descriptors by first-record index) names its tile, which goes to the list
+// once per workgroup.  The uniques rescan then runs on the listed tiles only:
+// at config 5 (0.45 k-mers per neuron) a few tiles instead of all 14,000.
+constexpr int kTileSeen = 256;
+template <bool WIDE>
+__global__ __launch_bounds__(kHistBlock) void k_uniq_tiles(GenPartArgs ga, UniqArgs u,
+                                                           const uint32_t *__restrict__ tbuckets,
+                                                           const uint32_t *__restrict__ n_tb,
+                                                           uint32_t slices, uint32_t *__restrict__ tiles,
+                                                           uint32_t *__restrict__ n_list,
+                                                           uint32_t max_list, uint32_t *__restrict__ flag,
+                                                           uint32_t *__restrict__ mark, uint32_t epoch) {
+  using Rec = typename GenShape<WIDE>::Rec;
+  __shared__ uint32_t t_off[kMaxTopN];
+  __shared__ uint32_t s_seen[kTileSeen];
+  __shared__ uint32_t t_n, s_ns;
+  if (blockIdx.y >= *n_tb) return;  // uniform
+  const uint32_t b = tbuckets[blockIdx.y], r = blockIdx.x;
+  if (threadIdx.x == 0) { t_n = 0; s_ns = 0; }
+  // (a slot claimed but not yet written reads as the sentinel: never a false
+  // duplicate -- LDS left by earlier kernels holds small integers like tile ids)
+  for (int i = threadIdx.x; i < kTileSeen; i += kHistBlock) s_seen[i] = 0xFFFFFFFFu;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < u.n_top; i += kHistBlock) {
+    const uint64_t idx = u.top[i].idx;
+    if ((idx >> ga.bin_bits) == b)
+      t_off[atomicAdd(&t_n, 1u)] = (uint32_t)(idx & ((1ull << ga.bin_bits) - 1ull));
+  }
+  __syncthreads();
+  const uint32_t tn = t_n;
+  uint64_t n = ga.fill[b] & ((1ull << 40) - 1);
+  if (n > ga.cap) n = ga.cap;
+  uint64_t n_seg = ga.fill[b] >> 40;
+  if (n_seg > ga.max_segs) n_seg = ga.max_segs;
+  const uint64_t lo = n * r / slices, hi = n * (r + 1) / slices;
+  const Rec *src = reinterpret_cast<const Rec *>(ga.rec) + (uint64_t)b * ga.cap;
+  const uint2 *d = ga.desc + (uint64_t)b * ga.max_segs;
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += kHistBlock) {
+    const uint32_t off = (uint32_t)src[i];
+    bool hit = false;
+    for (uint32_t t = 0; t < tn; ++t) hit |= t_off[t] == off;  // (pads never match)
+    if (!hit) continue;
+    uint64_t a = 0, z = n_seg;  // last segment with first record <= i
+    while (z - a > 1) {
+      const uint64_t m = (a + z) >> 1;
+      if (d[m].y <= i) a = m;
+      else z = m;
+    }
+    const uint32_t tile = d[a].x;
+    bool dup = false;
+    const uint32_t ns = s_ns < (uint32_t)kTileSeen ? s_ns : (uint32_t)kTileSeen;
+    for (uint32_t j = 0; j < ns && !dup; ++j) dup = s_seen[j] == tile;
+    if (dup) continue;
+    const uint32_t at = atomicAdd(&s_ns, 1u);
+    if (at < (uint32_t)kTileSeen) s_seen[at] = tile;
+    // once per pass over all workgroups (the list holds at most n_tiles
+    // entries: the rescan's grid is sized for that)
+    if (atomicExch(&mark[tile], epoch) == epoch) continue;
+    const uint32_t g = atomicAdd(n_list, 1u);
+    if (g < max_list) tiles[g] = tile;
+    else atomicOr(flag, 1u);  // list full: the caller rescans everything
+  }
+}
+
 // K1k: the exact table's distinct keys -> kmer_per_neuron, as a count of a key
 // array through the same partition + LDS histograms (a per-key global atomic,
 // k_kpn, runs at the memory side: 4.2 ms for 113 M keys, profiles/r02_s18).
@@ -245,6 +324,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part_keys(const uint64_t *__rest
   const int tid = threadIdx.x;
   const uint32_t nb = ga.n_buckets;
   const int bb = ga.bin_bits;
+  const bool small_pool = fm.p < (1ull << 30);
   const uint32_t omask = (uint32_t)((1ull << bb) - 1ull);
   for (uint32_t b = tid; b <= nb; b += kPartBlock) s_cnt[b] = 0;
   __syncthreads();
@@ -255,7 +335,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part_keys(const uint64_t *__rest
     const bool ok = i < n;
     uint64_t h = 0;
     if (ok) h = W128 ? sip13_u128(keys[2 * i], keys[2 * i + 1]) : sip13_u64(keys[i]);
-    const uint32_t idx = (uint32_t)fastmod(h, fm);
+    const uint32_t idx = small_pool ? fastmod32(h, fm) : (uint32_t)fastmod(h, fm);
     const uint32_t b = ok ? (idx >> bb) : nb;
     E[j] = (b << 16) | atomicAdd(&s_cnt[b], 1u);
     O[j] = idx & omask;
@@ -336,6 +416,19 @@ hipError_t launch_part_gen(const KmerInput &in, int k, int canonical, int km, ui
   }
 #undef NK_GEN_W
 #undef NK_GEN
+  return hipGetLastError();
+}
+
+hipError_t launch_uniq_tiles(const GenPartArgs &ga, int wide, const UniqArgs &u,
+                             const uint32_t *tbuckets, const uint32_t *n_tb, uint32_t max_tb,
+                             uint32_t slices, uint32_t *tiles, uint32_t *n_list, uint32_t max_list,
+                             uint32_t *flag, uint32_t *mark, uint32_t epoch, hipStream_t s) {
+  if (!max_tb || !ga.desc) return hipSuccess;
+  const dim3 g(slices ? slices : 1, max_tb), b(kHistBlock);
+  if (wide) hipLaunchKernelGGL(k_uniq_tiles<true>, g, b, 0, s, ga, u, tbuckets, n_tb, slices ? slices : 1,
+                               tiles, n_list, max_list, flag, mark, epoch);
+  else hipLaunchKernelGGL(k_uniq_tiles<false>, g, b, 0, s, ga, u, tbuckets, n_tb, slices ? slices : 1,
+                          tiles, n_list, max_list, flag, mark, epoch);
   return hipGetLastError();
 }
 

@@ -334,6 +334,33 @@ def test_part_path_past_2_32_positions():
 POOL2 = 2_000_000
 
 
+@pytest.mark.parametrize("k,pool,canon,width,tile_list", [
+    (40, 2_000_003, True, 64, None),      # Gen: dense hits (57 k-mers per neuron)
+    (40, 2_000_003, True, 64, 3),         # ... list overflow -> the full rescan
+    (63, 40_000_003, True, 128, None),    # Wide, 128-bit keys
+    (33, 30_000_001, False, 64, 2),       # Wide, pack_kmer keys, list overflow
+    (63, C5_POOL, True, 64, None),        # config-5 pool, compat keys
+])
+def test_uniques_from_kept_records(k, pool, canon, width, tile_list):
+    """Gen/Wide counts keep k_part_gen's records and segment descriptors; the
+    top rows' uniques rescan only the tiles holding their records
+    (k_uniq_tiles), or everything when the tile list overflows
+    (NK_UNIQ_TILE_LIST): top-20 rows with uniques bit-exact vs the oracle."""
+    bases, offs = synth.make_records(1_500_000, 5, seed=170 + k, repeats_per_mb=3000,
+                                     motif_len=120, n_rate=0.002, mixed_case=True)
+    r = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, canon, width=width)
+    r.process_parallel_arrays(bases, offs, THREADS)
+    kv = {"NK_UNIQ_TILE_LIST": tile_list} if tile_list else {}
+    with env(**kv):
+        g = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, canon, kmer_width=width)
+        g.process_parallel_arrays(bases, offs)
+        assert_same(g, r)
+        g.process_parallel_arrays(bases, offs)  # state carries over
+    r.process_parallel_arrays(bases, offs, THREADS)
+    assert_same(g, r)
+    g.close()
+
+
 # ---- golden fixtures through the HIP path ------------------------------------
 GOLDEN_E2E = sorted(glob.glob(os.path.join(GOLD, "e2e_*.json")))
 
