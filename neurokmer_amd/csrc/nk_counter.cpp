@@ -196,6 +196,11 @@ struct nk_counter {
   // and the closed-form table give them back (settle_state writes them out)
   bool state_derived = false;
   LifParams derived_lp{};
+  // the last accumulate's write-through K1b also ran the LIF from the reset
+  // state with these parameters (sc8, hist, stats written): the next LIF of a
+  // finalize is skipped while nothing else touched the currents or the state
+  bool k1b_lif = false;
+  LifParams k1b_lp{};
   // min(spike count, 255) per neuron, written by a LIF whose top-N is not fused
   // (large pools): what the top-N passes read first (1 B instead of 8 per neuron)
   DevBuf<uint8_t> sc8;
@@ -254,6 +259,7 @@ struct nk_counter {
   GenPartArgs last_ga{};
   DevBuf<uint32_t> u_tiles, u_nt;
   DevBuf<uint32_t> u_mark;  // per tile: the last pass that listed it (zeroed when allocated)
+  DevBuf<uint32_t> u_lanes;  // per tile: lanes with a top row's record (lane-tagged records)
   size_t u_mark_zeroed = 0;
   uint32_t u_epoch = 0;
   // input of the last accumulate (for the uniques pass)
@@ -349,6 +355,7 @@ static int zero_state_on(nk_counter *c, hipStream_t) {
   c->max_sc = 0;
   c->state_derived = false;
   c->sc8_ok = false;
+  c->k1b_lif = false;
   return NK_OK;
 }
 
@@ -463,6 +470,7 @@ uint64_t *counter_currents_on(nk_counter *c, hipStream_t stream) {
   (void)hipSetDevice(c->device);
   hipStream_t s = pick_stream(c, stream);
   if (settle_state(c, s) || materialize(c, true, s) || fold_pending(c, s)) return nullptr;
+  c->k1b_lif = false;  // the caller may change the counts
   return c->cur.p;
 }
 }  // namespace nk
@@ -892,6 +900,8 @@ static int plan_count(nk_counter *c, uint64_t est_bases, uint64_t slack, uint64_
     if ((rc = c->p_desc.ensure((uint64_t)cp.ga.n_buckets * max_segs))) return rc;
     cp.ga.desc = c->p_desc.p;
     cp.ga.max_segs = max_segs;
+    cp.ga.lane_tag = (cp.path == CountPath::Wide && cp.ga.bin_bits <= kLaneTagMaxBits &&
+                      !getenv("NK_NO_LANE_TAG")) ? 1u : 0u;
   }
   z.ptr[z.n] = c->p_fill.p; z.bytes[z.n++] = B * 8;
   z.ptr[z.n] = c->p_over.p; z.bytes[z.n++] = B * 4;
@@ -940,6 +950,10 @@ static hipError_t batch_count(nk_counter *c, const CountPlan &cp, const KmerInpu
 
 // defer_partials: leave K1c (currents += partials) to the LIF kernel of the
 // same process call instead of a separate pass
+static bool top_fused(const nk_counter *c, uint64_t want);
+static LifParams lif_params(const nk_counter *c, int streaming);
+static int lif_table(nk_counter *c, const LifParams &lp, hipStream_t s);
+
 static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_offs,
                       size_t n_recs, size_t n_bases, void *stream, bool defer_partials,
                       uint64_t first_pos = 0) {
@@ -955,6 +969,7 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
   if (int rc0 = settle_state(c, s)) return rc0;
   c->pend_slices = 0;  // this call zeroes the currents: earlier partials are void
   c->cur_in_wire = false;
+  c->k1b_lif = false;
   c->export_pending = c->redo_ready = false;
   KmerInput in{};
   in.bases = d_bases;
@@ -990,6 +1005,23 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
     }
     cp.pa.currents = cp.ga.currents = c->ovf.p;
     cp.pa.out = (unsigned long long *)c->cur.p;
+    // from the reset state with the hist/stats zeroed by this prep (a split
+    // accumulate or a process call) and a finish that does not fuse its top-N
+    // into the LIF kernel: K1b runs the LIF too (a function of the counts)
+    const uint64_t want = std::min<uint64_t>(c->opts.top_n, c->pool);
+    if (defer_partials && c->state_fresh && !top_fused(c, want) && c->pool &&
+        !getenv("NK_NO_K1B_LIF")) {
+      const LifParams lp = lif_params(c, 0 /* skip_zero: the in-memory finish */);
+      if ((rc = lif_table(c, lp, s)) || (rc = c->sc8.ensure(c->pool))) return rc;
+      cp.pa.lif.sc8 = c->sc8.p;
+      cp.pa.lif.tbl = c->lif_tbl.p;
+      cp.pa.lif.tbl_n = kLifTable;
+      cp.pa.lif.lp = lp;
+      cp.pa.lif.hist = c->hist.p;
+      cp.pa.lif.stats = (unsigned long long *)c->stats.p;
+      c->k1b_lif = true;
+      c->k1b_lp = lp;
+    }
     if (cp.path == CountPath::Wide) {
       cp.pa.over_coarse = cp.ga.overflow;
       cp.pa.coarse_shift = (uint32_t)(cp.ga.bin_bits - kBinBits);
@@ -1055,7 +1087,7 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
   if (defer_partials) {  // the LIF of this process call accumulates into these
     z.ptr[z.n] = c->hist.p;  z.bytes[z.n++] = kHistBins * kHistCopies * 4;
     z.ptr[z.n] = c->stats.p; z.bytes[z.n++] = 16;
-    c->lif_zeroed = true;
+    c->lif_zeroed = !c->k1b_lif;  // (K1b adds into them: a LIF that runs after all re-zeroes)
   }
   unsigned long long *span = nullptr;
   if (c->part_used) {
@@ -1157,21 +1189,31 @@ static int refine_threshold(nk_counter *c, uint64_t want, uint64_t max_sc, TopSt
 // nk_wire32; the LIF reads them from it and writes the u64 currents
 // LIF parameters of a finalize, the closed-form table for them (cached), and
 // the spike histogram + stats zeroed unless this call's prep already did it
-static int lif_prepare(nk_counter *c, int streaming, LifParams &lp, hipStream_t s) {
+static LifParams lif_params(const nk_counter *c, int streaming) {
+  LifParams lp{};
   lp.steps = c->steps;
   lp.thr = c->thr;
   lp.leak = c->leak;
   lp.refr = c->refr;
   lp.skip_zero = streaming ? 0 : 1;  // process_parallel skips zero currents (:189-191)
-  int rc;
-  // closed-form results for fresh neurons with count < 65536, cached per params
+  return lp;
+}
+
+// closed-form results for fresh neurons with count < 65536, cached per params
+static int lif_table(nk_counter *c, const LifParams &lp, hipStream_t s) {
   if (!c->lif_valid || c->lif_key.steps != lp.steps || c->lif_key.refr != lp.refr ||
       memcmp(&c->lif_key.thr, &lp.thr, 4) || memcmp(&c->lif_key.leak, &lp.leak, 4)) {
-    if ((rc = c->lif_tbl.ensure(kLifTable))) return rc;
+    if (int rc = c->lif_tbl.ensure(kLifTable)) return rc;
     HIPCHK(launch_lif_table(c->lif_tbl.p, kLifTable, lp, s));
     c->lif_key = lp;
     c->lif_valid = true;
   }
+  return NK_OK;
+}
+
+static int lif_prepare(nk_counter *c, int streaming, LifParams &lp, hipStream_t s) {
+  lp = lif_params(c, streaming);
+  if (int rc = lif_table(c, lp, s)) return rc;
   if (!c->lif_zeroed) {
     ZeroList z{};
     z.ptr[0] = c->hist.p;  z.bytes[0] = kHistBins * kHistCopies * 4;
@@ -1183,12 +1225,39 @@ static int lif_prepare(nk_counter *c, int streaming, LifParams &lp, hipStream_t 
   return NK_OK;
 }
 
+// the LIF the write-through K1b already ran (K1bLif) holds for this finalize
+static bool k1b_lif_holds(const nk_counter *c, const LifParams &lp, uint32_t fuse_want,
+                          const uint32_t *wire) {
+  if (!c->k1b_lif || wire || fuse_want || !c->state_fresh || c->pend_slices || c->cur_fresh ||
+      c->cur_in_wire || !c->pool)
+    return false;
+  const LifParams &k = c->k1b_lp;
+  if (k.steps != lp.steps || k.refr != lp.refr || memcmp(&k.thr, &lp.thr, 4) ||
+      memcmp(&k.leak, &lp.leak, 4))
+    return false;
+  // skip_zero differs (a streaming finalize): the same outcome when a zero
+  // count cannot spike from the reset state (thr > 0: v stays 0)
+  return k.skip_zero == lp.skip_zero || lp.thr > 0.0f;
+}
+
 static int enqueue_lif(nk_counter *c, int streaming, uint32_t fuse_want, bool part,
                        hipStream_t s, const uint32_t *wire = nullptr) {
   LifParams lp;
   // (a LIF with no count since the last one: that one's derived state first)
   int rc = settle_state(c, s);
-  if (rc || (rc = lif_prepare(c, streaming, lp, s))) return rc;
+  if (rc) return rc;
+  const bool k1b = k1b_lif_holds(c, lif_params(c, streaming), fuse_want, wire) &&
+                   !getenv("NK_NO_K1B_LIF_USE");
+  c->k1b_lif = false;
+  if (k1b) {  // sc8, hist and stats are this LIF's: the state is derived
+    c->lif_zeroed = false;
+    c->sc8_ok = true;
+    c->state_derived = true;
+    c->derived_lp = lif_params(c, streaming);
+    c->state_fresh = false;
+    return NK_OK;
+  }
+  if ((rc = lif_prepare(c, streaming, lp, s))) return rc;
   TopFuse tf{};
   if (fuse_want) {
     const uint32_t nb = lif_blocks(c->pool);
@@ -1253,6 +1322,13 @@ static int enqueue_select(nk_counter *c, uint64_t want, hipStream_t s, uint64_t 
 #ifndef NK_U1_SLICE_BUDGET
 #define NK_U1_SLICE_BUDGET 1024  // scan workgroups per launch (A/B: 1024 with 4 loads in flight best)
 #endif
+// a positive integer from the environment (tests: force the rare branches)
+static uint32_t env_u32(const char *name, uint32_t dflt) {
+  const char *e = getenv(name);
+  const unsigned long v = e ? strtoul(e, nullptr, 10) : 0;
+  return v ? (uint32_t)v : dflt;
+}
+
 static int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, bool post_done,
                            hipStream_t s) {
   const bool part = c->part_used && !rescan;
@@ -1312,12 +1388,22 @@ static int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, bool post_don
         c->u_epoch = 1;
       }
       HIPCHK(hipMemsetAsync(c->u_nt.p, 0, 4, s));
+      const bool tagged = c->last_ga.lane_tag != 0;
+      if (tagged) {
+        if ((rc = c->u_lanes.ensure(in.n_tiles * kLaneWords))) return rc;
+        HIPCHK(hipMemsetAsync(c->u_lanes.p, 0, in.n_tiles * kLaneWords * 4, s));
+      }
       const uint32_t slices = std::max<uint32_t>(1, NK_U1_SLICE_BUDGET / m);
       HIPCHK(launch_uniq_tiles(c->last_ga, c->gen_wide ? 1 : 0, u, c->tbuckets.p, c->post_flags.p + 2,
                                m, slices, c->u_tiles.p, c->u_nt.p, kTileList, c->post_flags.p + 1,
-                               c->u_mark.p, c->u_epoch, s));
-      HIPCHK(launch_uniq_gen(in, (int)c->k, c->canonical, c->gen_km, c->pool, u, s, c->u_tiles.p,
-                             c->u_nt.p, kTileList));
+                               c->u_mark.p, c->u_epoch, tagged ? c->u_lanes.p : nullptr,
+                               env_u32("NK_UNIQ_HIT_QUEUE", ~0u), s));
+      if (tagged)  // the list holds lanes: their windows, keyed from global memory
+        HIPCHK(launch_uniq_lanes(in, (int)c->k, c->canonical, c->gen_km, c->pool, u, c->u_tiles.p,
+                                 c->u_nt.p, kTileList, s));
+      else
+        HIPCHK(launch_uniq_gen(in, (int)c->k, c->canonical, c->gen_km, c->pool, u, s, c->u_tiles.p,
+                               c->u_nt.p, kTileList));
     } else if (c->gen_km >= 0)
       HIPCHK(launch_uniq_gen(in, (int)c->k, c->canonical, c->gen_km, c->pool, u, s));
     else if (c->w128)
@@ -1832,6 +1918,7 @@ int nk_wire32(nk_counter *c, uint32_t *d_wire, void *stream) {
   if (!c || (!d_wire && c->pool)) return fail(NK_E_INVALID, "null argument");
   if (c->cur_in_wire) return fail(NK_E_INVALID, "nk_wire32 twice without nk_finalize_export");
   (void)hipSetDevice(c->device);
+  c->k1b_lif = false;  // the LIF reads the (all-reduced) wire
   hipStream_t s = pick_stream(c, stream);
   int rc = settle_state(c, s);
   if (rc || (rc = materialize(c, true, s))) return rc;
@@ -1976,6 +2063,7 @@ int nk_finalize_slice(nk_counter *c, int streaming, const void *d_slice, int sli
   if (lo > hi || hi > c->pool) return fail(NK_E_INVALID, "slice [%zu, %zu) outside the pool", lo, hi);
   if (slice_bits != 32 && slice_bits != 64) return fail(NK_E_INVALID, "slice_bits must be 32 or 64");
   if (hi > lo && !d_slice) return fail(NK_E_INVALID, "null slice");
+  c->k1b_lif = false;  // the slice's LIF runs on the reduced slice
   const uint64_t want = std::min<uint64_t>(c->opts.top_n, c->pool);
   if (seg_rows < want) return fail(NK_E_INVALID, "seg_rows (%zu) < top_n rows (%llu)", seg_rows,
                                    (unsigned long long)want);
@@ -2254,6 +2342,7 @@ static int acc_begin(nk_counter *c, uint64_t est_bases, uint64_t batch_bases, St
   z.ptr[z.n] = c->hist.p;  z.bytes[z.n++] = kHistBins * kHistCopies * 4;
   z.ptr[z.n] = c->stats.p; z.bytes[z.n++] = 16;
   c->lif_zeroed = true;
+  c->k1b_lif = false;
   if (c->pool) HIPCHK(launch_zero(z, s));
   c->cur_fresh = false;
   sa.keep = sa.cp.path == CountPath::Part && part_like;
@@ -2466,6 +2555,7 @@ int nk_process_sequence(nk_counter *c, const uint8_t *seq, size_t len) {
   if (len && !seq) return fail(NK_E_INVALID, "null sequence");
   if (int rc0 = whole_pool(c)) return rc0;
   if (len < c->k) return NK_OK;  // :205-207: no k-mers, no LIF step
+  c->k1b_lif = false;
   if (c->pool == 0)
     return fail(NK_E_INVALID, "pool_size 0 with k-mers present (the reference panics on % 0)");
   hipStream_t s;
@@ -2724,6 +2814,7 @@ uint64_t *nk_device_currents(nk_counter *c) {
   }
   // lazily-reset currents / K1b partials pending / a derived state (the caller
   // may change the counts it is a function of: written out first)
+  c->k1b_lif = false;
   if (c->cur_fresh || c->pend_slices || c->state_derived) {
     (void)hipSetDevice(c->device);
     hipStream_t s = pick_stream(c, nullptr);

@@ -119,6 +119,18 @@ struct KmerInput {
   uint64_t pos_hi = ~0ull;
 };
 
+// The LIF from the reset state fused into a write-through K1b (its outcome is
+// a function of each neuron's count): the u8 spike mirror, the spike
+// histogram (bin 0 not counted) and the totals, as k_lif_apply writes them
+struct K1bLif {
+  uint8_t *sc8 = nullptr;  // non-null: on
+  const LifEntry *tbl = nullptr;
+  int tbl_n = 0;
+  LifParams lp{};
+  uint32_t *hist = nullptr;             // [kHistCopies][kHistBins]
+  unsigned long long *stats = nullptr;  // [0] total spikes [1] max spikes
+};
+
 struct PartArgs {
   uint32_t n_buckets;
   uint64_t cap;                   // records per bucket region
@@ -142,6 +154,7 @@ struct PartArgs {
   unsigned long long *out = nullptr;
   const uint32_t *over_coarse = nullptr;  // wide: coarse overflow flags
   uint32_t coarse_shift = 0;              // fine bucket -> coarse bucket
+  K1bLif lif;                             // write-through only
 };
 
 // Generic partition (nk_wide.hip): any key mode; narrow (u16 offsets into
@@ -163,7 +176,13 @@ struct GenPartArgs {
   // that hold a top row's records and rescans only those (k_uniq_tiles)
   uint2 *desc = nullptr;
   uint64_t max_segs = 0;
+  // wide + kept, bin_bits <= kLaneTagMaxBits: each record also carries its
+  // k_part_gen lane (bits bin_bits .. bin_bits + 8), so the uniques rescan
+  // hashes only the lanes that produced a top row's records
+  uint32_t lane_tag = 0;
 };
+constexpr int kLaneTagMaxBits = 22;  // + 9 lane bits < 32: never the pad (all ones)
+constexpr int kLaneWords = 16;       // 512 lanes of a k_part_gen tile, one bit each
 
 // keys handed to the uniques merge: a flat list (world == 0) or the
 // fixed-stride segments [n_r, keys...] of an all-gather buffer
@@ -285,6 +304,10 @@ hipError_t launch_part_gen(const KmerInput &in, int k, int canonical, int km, ui
                            const GenPartArgs &ga, int wide, hipStream_t s);
 // uniques rescan over kPartTile tiles for the Gen/Wide count paths; with a
 // tile list (tiles, *n_list <= max_list) only those tiles
+// the windows of the listed (tile << 9 | lane) entries of lane-tagged records
+hipError_t launch_uniq_lanes(const KmerInput &in, int k, int canonical, int km, uint64_t pool,
+                             const UniqArgs &u, const uint32_t *list, const uint32_t *n_list,
+                             uint32_t max_list, hipStream_t s);
 hipError_t launch_uniq_gen(const KmerInput &in, int k, int canonical, int km, uint64_t pool,
                            const UniqArgs &u, hipStream_t s, const uint32_t *tiles = nullptr,
                            const uint32_t *n_list = nullptr, uint32_t max_list = 0);
@@ -295,7 +318,8 @@ hipError_t launch_uniq_gen(const KmerInput &in, int k, int canonical, int km, ui
 hipError_t launch_uniq_tiles(const GenPartArgs &ga, int wide, const UniqArgs &u,
                              const uint32_t *tbuckets, const uint32_t *n_tb, uint32_t max_tb,
                              uint32_t slices, uint32_t *tiles, uint32_t *n_list, uint32_t max_list,
-                             uint32_t *flag, uint32_t *mark, uint32_t epoch, hipStream_t s);
+                             uint32_t *flag, uint32_t *mark, uint32_t epoch, uint32_t *lanes,
+                             uint32_t hit_queue, hipStream_t s);
 hipError_t launch_split(const GenPartArgs &ga, const PartArgs &fine, hipStream_t s);
 // the exact table's kmer_per_neuron: a key array (wpk u64 words per key, *n_keys
 // of them on the device, at most max_n) hashed and partitioned like the count

@@ -343,6 +343,79 @@ __global__ __launch_bounds__(kPartBlock) void k_uniq_gen(KmerInput in, int k, Fa
   }
 }
 
+// Uniques of the lane-tagged wide records: entry (tile << 9 | lane) of the
+// list k_uniq_tiles built is one k_part_gen lane that produced a top row's
+// record; its kPer windows are keyed without staging a tile: canonical keys
+// (KM 0 / 2) roll through the lane's kPer + k - 1 bytes (five 16-B loads into
+// the thread's LDS slot), the rest are keyed per window from global memory.
+// Hashed; those of top rows go into the set.  Grid-stride over the
+// device-side list length.
+constexpr int kLaneBytes = 80;  // kPer + 64 - 1 rounded up to 16 B
+template <int KM, bool CANON>
+__global__ __launch_bounds__(256) void k_uniq_lanes(KmerInput in, int k, FastMod fm, UniqArgs u,
+                                                    const uint32_t *__restrict__ list,
+                                                    const uint32_t *__restrict__ n_list,
+                                                    uint32_t max_list) {
+  extern __shared__ uint64_t dyn[];  // probe table
+  __shared__ uint4 s_b[256 * (kLaneBytes / 16)];
+  uint64_t *tbl_idx = dyn;
+  uint32_t *tbl_slot = reinterpret_cast<uint32_t *>(dyn + u.tbl_size);
+  build_top_tbl(u, tbl_idx, tbl_slot);  // contains __syncthreads
+  constexpr bool kRoll = CANON && KM != 1;
+  uint4 *mine = s_b + threadIdx.x * (kLaneBytes / 16);
+  const uint8_t *bb = reinterpret_cast<const uint8_t *>(mine);
+  const int sh = 2 * k - 2;
+  const uint32_t n = *n_list < max_list ? *n_list : max_list;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const uint32_t ent = list[e];
+    const uint64_t tile = ent >> 9;
+    const uint64_t p0 = tile * (uint64_t)kPartTile + (uint64_t)(ent & 511u) * kPer;
+    const bool roll = kRoll && p0 + kLaneBytes <= in.n_bases;
+    if (roll) {
+#pragma unroll
+      for (int c = 0; c < kLaneBytes / 16; ++c)
+        mine[c] = *reinterpret_cast<const uint4 *>(in.bases + p0 + 16 * c);
+    }
+    Key128 fwd{0, 0}, rev{0, 0};
+    auto push = [&](uint8_t x) {  // one base into both rolling keys (2k bits)
+      const uint64_t c = code_of(x), r = comp_of(x);
+      fwd.hi = (fwd.hi << 2) | (fwd.lo >> 62);
+      fwd.lo = (fwd.lo << 2) | c;
+      if (k < 32) {
+        fwd.lo &= (1ull << (2 * k)) - 1ull;
+        fwd.hi = 0;
+      } else if (k < 64) {
+        fwd.hi &= (1ull << (2 * k - 64)) - 1ull;
+      }
+      rev.lo = (rev.lo >> 2) | (rev.hi << 62);
+      rev.hi >>= 2;
+      if (sh >= 64) rev.hi |= r << (sh - 64);
+      else rev.lo |= r << sh;
+    };
+    if (roll)
+      for (int i = 0; i < k - 1; ++i) push(bb[i]);
+    // the record holding p0 (windows must end inside their record)
+    uint64_t r = in.n_recs ? rec_of(in.offsets, in.n_recs, in.tile_rec[tile], p0) : 0;
+    for (int j = 0; j < kPer; ++j) {
+      const uint64_t p = p0 + (uint64_t)j;
+      if (roll) push(bb[j + k - 1]);
+      if (p + (uint64_t)k > in.n_bases || p < in.pos_lo || p >= in.pos_hi) continue;
+      while (r + 1 < in.n_recs && in.offsets[r + 1] <= p) ++r;
+      if (!in.n_recs || p + (uint64_t)k > in.offsets[r + 1]) continue;  // crosses a record end
+      Key128 key{0, 0};
+      if (roll) key = key128_less(rev, fwd) ? rev : fwd;
+      else if (KM == 2) key = global_window_key128<CANON>(in.bases, p, k);
+      else if (KM == 1) key.lo = compat_key<CANON>(in.bases, in.offsets[r], p, k);
+      else key.lo = global_window_key<CANON>(in.bases, p, k);
+      const uint64_t idx = fastmod(gen_hash<KM>(key), fm);
+      const int slot = probe_top(tbl_idx, tbl_slot, u.tbl_size - 1, idx);
+      if (slot < 0) continue;
+      if (KM == 2) set_insert128(u, (uint32_t)slot, key);
+      else set_insert(u, (uint32_t)slot, key.lo);
+    }
+  }
+}
+
 __global__ void k_set_fill128(unsigned long long *__restrict__ S, const uint64_t *__restrict__ mask) {
   const uint64_t n = 3 * (*mask + 1);
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -710,20 +783,44 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
 #endif
 }
 
+// Spikes of a neuron in the derived state: the LIF from (v, r) = (0, 0) of
+// its count (k_lif_apply's fresh branch).
+__device__ __forceinline__ uint64_t fresh_spikes(uint64_t cnt, const LifParams &lp,
+                                                 const LifEntry *tbl, int tbl_n, float &v,
+                                                 uint32_t &r) {
+  v = 0.0f;
+  r = 0u;
+  if ((lp.skip_zero && cnt == 0) || lp.steps == 0) return 0;
+  if (cnt < (uint64_t)tbl_n) {
+    const LifEntry e = tbl[cnt];
+    v = e.v;
+    r = e.r;
+    return e.spikes;
+  }
+  return lif_closed(lif_current(cnt, lp.steps), lp.steps, lp.thr, lp.leak, lp.refr, v, r);
+}
+
 // partials == nullptr: add the histogram into pa.currents instead (u64; plain
 // read-modify-write of the bins this workgroup owns when slices == 1, atomics
 // otherwise; bins that stayed zero are not touched)
 #ifndef NK_HIST_KU
 #define NK_HIST_KU 4
 #endif
-template <int BB, int KU = NK_HIST_KU>  // 2^BB bins per bucket (pa.bin_bits)
+// LIF: the write-through K1b also runs the LIF from the reset state (pa.lif)
+template <int BB, int KU = NK_HIST_KU, bool LIF = false>  // 2^BB bins per bucket (pa.bin_bits)
 __global__ __launch_bounds__(kHistBlock) void k_bucket_hist(PartArgs pa, uint64_t pool,
                                                             uint32_t slices,
                                                             uint32_t *__restrict__ partials) {
   constexpr uint32_t kBins = 1u << BB;
   __shared__ uint32_t h[kBins + 1];  // + a spill bin for pad records
+  __shared__ uint32_t s_sh[LIF ? kHistBins : 1];  // spike histogram of the bucket
+  __shared__ unsigned long long s_acc[2];
   const uint32_t b = blockIdx.x, r = blockIdx.y;  // buckets on x: up to 65536 of them
   for (int i = threadIdx.x; i <= (int)kBins; i += kHistBlock) h[i] = 0;
+  if (LIF) {
+    for (int i = threadIdx.x; i < kHistBins; i += kHistBlock) s_sh[i] = 0;
+    if (threadIdx.x < 2) s_acc[threadIdx.x] = 0;
+  }
   auto bin = [](uint32_t off) { return off < kBins ? off : kBins; };
   __syncthreads();
   uint64_t n = pa.fill[b] & ((1ull << 40) - 1);
@@ -781,7 +878,7 @@ __global__ __launch_bounds__(kHistBlock) void k_bucket_hist(PartArgs pa, uint64_
   if (!partials && pa.out) {  // write-through: every bin, the overflow target folded + re-zeroed
     const bool ov = pa.overflow[b] || (pa.over_coarse && pa.over_coarse[b >> pa.coarse_shift]);
     unsigned long long *o = pa.out + nb0, *ovf = pa.currents + nb0;
-    for (uint32_t t = threadIdx.x; t < nbins; t += kHistBlock) {
+    auto count = [&](uint32_t t) -> unsigned long long {
       unsigned long long x = h[t];
       if (ov) {
         const unsigned long long e = ovf[t];
@@ -790,8 +887,59 @@ __global__ __launch_bounds__(kHistBlock) void k_bucket_hist(PartArgs pa, uint64_
           ovf[t] = 0;
         }
       }
-      o[t] = x;
+      return x;
+    };
+    if (!LIF) {
+      for (uint32_t t = threadIdx.x; t < nbins; t += kHistBlock) o[t] = count(t);
+      return;
     }
+    // fused LIF from the reset state (k_lif_apply's fresh branch): 4 bins per
+    // lane, the currents as two 16-B stores and the u8 mirror as one 4-B store
+    const K1bLif &L = pa.lif;
+    unsigned long long my_sp = 0, my_mx = 0;
+    auto lif = [&](unsigned long long x) -> uint32_t {
+      float v;
+      uint32_t rr;
+      const uint64_t sp = fresh_spikes(x, L.lp, L.tbl, L.tbl_n, v, rr);
+      if (sp) {
+        my_sp += sp;
+        my_mx = sp > my_mx ? sp : my_mx;
+        atomicAdd(&s_sh[sp < (uint64_t)(kHistBins - 1) ? (uint32_t)sp : (uint32_t)(kHistBins - 1)], 1u);
+      }
+      return sp < 255 ? (uint32_t)sp : 255u;
+    };
+    uint8_t *m8 = L.sc8 + nb0;
+    for (uint32_t t = 4 * threadIdx.x; t < nbins; t += 4 * kHistBlock) {
+      if (t + 4 <= nbins) {
+        const unsigned long long x0 = count(t), x1 = count(t + 1), x2 = count(t + 2), x3 = count(t + 3);
+        reinterpret_cast<ulonglong2 *>(o + t)[0] = make_ulonglong2(x0, x1);
+        reinterpret_cast<ulonglong2 *>(o + t)[1] = make_ulonglong2(x2, x3);
+        *reinterpret_cast<uint32_t *>(m8 + t) = lif(x0) | lif(x1) << 8 | lif(x2) << 16 | lif(x3) << 24;
+      } else {
+        for (uint32_t u = t; u < nbins; ++u) {
+          const unsigned long long x = count(u);
+          o[u] = x;
+          m8[u] = (uint8_t)lif(x);
+        }
+      }
+    }
+    for (int sh = 32; sh > 0; sh >>= 1) {
+      my_sp += __shfl_down(my_sp, sh, 64);
+      const unsigned long long om = __shfl_down(my_mx, sh, 64);
+      my_mx = om > my_mx ? om : my_mx;
+    }
+    if ((threadIdx.x & 63) == 0 && my_sp) {
+      atomicAdd(&s_acc[0], my_sp);
+      atomicMax(&s_acc[1], my_mx);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && s_acc[0]) {
+      atomicAdd(&L.stats[0], s_acc[0]);
+      atomicMax(&L.stats[1], s_acc[1]);
+    }
+    uint32_t *hc = L.hist + (size_t)(b & (kHistCopies - 1)) * kHistBins;
+    for (int i = threadIdx.x + 1; i < kHistBins; i += kHistBlock)
+      if (s_sh[i]) atomicAdd(&hc[i], s_sh[i]);
     return;
   }
   if (!partials) {
@@ -1415,23 +1563,6 @@ __device__ void final_top(uint64_t pool, const uint64_t *currents, uint32_t nb,
   }
 }
 
-// Spikes of a neuron in the derived state: the LIF from (v, r) = (0, 0) of
-// its count (k_lif_apply's fresh branch).
-__device__ __forceinline__ uint64_t fresh_spikes(uint64_t cnt, const LifParams &lp,
-                                                 const LifEntry *tbl, int tbl_n, float &v,
-                                                 uint32_t &r) {
-  v = 0.0f;
-  r = 0u;
-  if ((lp.skip_zero && cnt == 0) || lp.steps == 0) return 0;
-  if (cnt < (uint64_t)tbl_n) {
-    const LifEntry e = tbl[cnt];
-    v = e.v;
-    r = e.r;
-    return e.spikes;
-  }
-  return lif_closed(lif_current(cnt, lp.steps), lp.steps, lp.thr, lp.leak, lp.refr, v, r);
-}
-
 __device__ __forceinline__ uint64_t spikes_at(const SpikeSrc &s, uint64_t i) {
   if (s.sc8) {  // 1 B per neuron; 255 means "255 or more": the exact value below
     const uint32_t v = s.sc8[i];
@@ -1673,6 +1804,24 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(SpikeSrc sc, uint64_t poo
 
 constexpr int kTopChunk = kBlock * 8;  // neurons per block in count/emit
 
+// spike counts of neurons base .. base + 7 (0 past the pool): from the u8
+// mirror with one 8-B load where aligned and whole
+__device__ __forceinline__ void spikes8(const SpikeSrc &sc, uint64_t base, uint64_t pool,
+                                        uint64_t (&v)[8]) {
+  if (sc.sc8 && base + 8 <= pool && !((uintptr_t)(sc.sc8 + base) & 7)) {
+    const uint2 w = *reinterpret_cast<const uint2 *>(sc.sc8 + base);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t b = ((j < 4 ? w.x : w.y) >> (8 * (j & 3))) & 0xFFu;
+      v[j] = b;
+      if (b == 255u) v[j] = spikes_at(sc, base + j);  // 255 or more: the exact value
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = base + j < pool ? spikes_at(sc, base + j) : 0;
+}
+
 // one pass over the spike counts: the rows above T are emitted (any order:
 // k_topn_sort orders them) and each block's ties (== T) counted
 __global__ __launch_bounds__(kBlock) void k_topn_count(SpikeSrc sc,
@@ -1681,17 +1830,20 @@ __global__ __launch_bounds__(kBlock) void k_topn_count(SpikeSrc sc,
                                                        TopCand *__restrict__ cand) {
   __shared__ uint32_t s[kBlock / 64];
   const uint64_t T = st->T;
-  const uint64_t base = (uint64_t)blockIdx.x * kTopChunk;
+  // thread t owns 8 consecutive neurons of the block's chunk (the u8 mirror:
+  // one 8-B load per lane)
+  const uint64_t base = (uint64_t)blockIdx.x * kTopChunk + (uint64_t)threadIdx.x * 8;
+  uint64_t v[8];
+  spikes8(sc, base, pool, v);
   uint32_t c = 0;
   for (int j = 0; j < 8; ++j) {
-    const uint64_t i = base + (uint64_t)j * kBlock + threadIdx.x;
+    const uint64_t i = base + j;
     if (i >= pool) break;
-    const uint64_t v = spikes_at(sc, i);
-    if (v == T) ++c;
-    if (v > T && T != ~0ULL) {
+    if (v[j] == T) ++c;
+    if (v[j] > T && T != ~0ULL) {
       const unsigned long long pos = atomicAdd((unsigned long long *)&st->emit_above, 1ull);
       cand[pos].idx = i;
-      cand[pos].sc = v;
+      cand[pos].sc = v[j];
     }
   }
   for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
@@ -1749,9 +1901,9 @@ __global__ __launch_bounds__(kBlock) void k_topn_emit(SpikeSrc sc,
   const uint64_t base = (uint64_t)blockIdx.x * kTopChunk + (uint64_t)threadIdx.x * 8;
   uint32_t ties = 0;
   uint64_t v[8];
+  spikes8(sc, base, pool, v);
   for (int j = 0; j < 8; ++j) {
     uint64_t i = base + j;
-    v[j] = i < pool ? spikes_at(sc, i) : 0;
     if (i < pool && v[j] == T) ++ties;
   }
   s_scan[threadIdx.x] = ties;
@@ -2164,6 +2316,29 @@ hipError_t launch_uniq_gen(const KmerInput &in, int k, int canonical, int km, ui
   return hipGetLastError();
 }
 
+hipError_t launch_uniq_lanes(const KmerInput &in, int k, int canonical, int km, uint64_t pool,
+                             const UniqArgs &u, const uint32_t *list, const uint32_t *n_list,
+                             uint32_t max_list, hipStream_t s) {
+  if (!in.n_tiles || !max_list) return hipSuccess;
+  if (km < 0 || km > 2 || k < 1 || k > 64 || (km == 0 && k > 32) || (km == 1 && k <= 32))
+    return hipErrorInvalidValue;
+  const FastMod fm = make_fastmod(pool);
+  const dim3 g((unsigned)std::min<uint64_t>((max_list + 255) / 256, 1024)), b(256);
+  const size_t dyn = tbl_bytes(u);
+#define NK_UL(KM_, C_) hipLaunchKernelGGL((k_uniq_lanes<KM_, C_>), g, b, dyn, s, in, k, fm, u, list, n_list, max_list)
+  if (canonical) {
+    if (km == 0) NK_UL(0, true);
+    else if (km == 1) NK_UL(1, true);
+    else NK_UL(2, true);
+  } else {
+    if (km == 0) NK_UL(0, false);
+    else if (km == 1) NK_UL(1, false);
+    else NK_UL(2, false);
+  }
+#undef NK_UL
+  return hipGetLastError();
+}
+
 hipError_t launch_count128(const KmerInput &in, int k, int canonical, uint64_t pool,
                            uint64_t *currents, hipStream_t s) {
   UniqArgs u{};
@@ -2262,6 +2437,12 @@ hipError_t launch_bucket_hist(const PartArgs &pa, uint64_t pool, uint32_t slices
                               uint32_t *partials, hipStream_t s) {
   if (!pa.n_buckets) return hipSuccess;
   const dim3 g(pa.n_buckets, slices);
+  if (pa.lif.sc8) {  // the fused LIF: write-through only
+    if (partials || !pa.out || slices != 1 || pa.bin_bits != 15) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_bucket_hist<15, NK_HIST_KU, true>), g, dim3(kHistBlock), 0, s, pa, pool, slices,
+                       partials);
+    return hipGetLastError();
+  }
   switch (pa.bin_bits) {
     case 13: hipLaunchKernelGGL(k_bucket_hist<13>, g, dim3(kHistBlock), 0, s, pa, pool, slices, partials); break;
     case 14: hipLaunchKernelGGL(k_bucket_hist<14>, g, dim3(kHistBlock), 0, s, pa, pool, slices, partials); break;

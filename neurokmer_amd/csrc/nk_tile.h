@@ -314,4 +314,26 @@ __device__ __forceinline__ uint64_t global_window_key(const uint8_t *b, uint64_t
   }
 }
 
+// --kmer-width=128 key straight from global memory (window_key128's value;
+// uniques hits only): canonical = min(fwd, reverse complement) as u128,
+// otherwise pack_kmer over the valid bytes
+template <bool CANON>
+__device__ __forceinline__ Key128 global_window_key128(const uint8_t *b, uint64_t p, int k) {
+  Key128 fwd{0, 0}, rev{0, 0};
+  for (int i = 0; i < k; ++i) {
+    const uint8_t x = b[p + i];
+    if (!CANON && !valid_byte(x)) continue;  // pack_kmer skips the byte
+    const uint64_t c = code_of(x);
+    fwd.hi = (fwd.hi << 2) | (fwd.lo >> 62);
+    fwd.lo = (fwd.lo << 2) | c;
+    if (CANON) {
+      const uint64_t r = comp_of(x);
+      if (i < 32) rev.lo |= r << (2 * i);
+      else rev.hi |= r << (2 * i - 64);
+    }
+  }
+  if (!CANON) return fwd;
+  return key128_less(rev, fwd) ? rev : fwd;
+}
+
 }  // namespace nk

@@ -138,7 +138,7 @@ __device__ __forceinline__ void sort_and_store(const uint32_t (&E)[PER], const u
     } else {  // region full: count directly (exact, slow, rare)
       for (int i = 0; i < 8; ++i) {
         const uint32_t o = (uint32_t)s_rec[g * 8 + i];
-        if (o != S::kPad) atomicAdd(&currents[(bg << bin_bits) | o], 1ULL);
+        if (o != S::kPad) atomicAdd(&currents[(bg << bin_bits) | (o & ((1u << bin_bits) - 1u))], 1ULL);
       }
     }
   }
@@ -168,6 +168,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part_gen(KmerInput in, int k, Fa
   const int bb = ga.bin_bits;
   const bool small_pool = fm.p < (1ull << 30);  // the 32-bit modulo (nk_device.h) holds
   const uint32_t omask = (uint32_t)((1ull << bb) - 1ull);
+  const uint32_t ltag = (WIDE && ga.lane_tag) ? ((uint32_t)tid << bb) : 0u;  // (GenPartArgs::lane_tag)
   for (uint32_t b = tid; b <= nb; b += kPartBlock) s_cnt[b] = 0;
   stage_tile<kPartTile, kPartBlock, kRaw>(L, in, tile, k);  // syncs
 
@@ -184,7 +185,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part_gen(KmerInput in, int k, Fa
     const uint32_t idx = small_pool ? fastmod32(h, fm) : (uint32_t)fastmod(h, fm);
     const uint32_t b = ok ? (idx >> bb) : nb;
     E[j] = (b << 16) | atomicAdd(&s_cnt[b], 1u);
-    O[j] = idx & omask;
+    O[j] = (idx & omask) | ltag;
   }
   sort_and_store<WIDE, kPer>(E, O, nb, s_cnt, s_start, s_base, s_fit, s_rec, s_gmap, ga.fill,
                              ga.overflow, ga.cap, reinterpret_cast<typename S::Rec *>(ga.rec), 0,
@@ -208,6 +209,7 @@ __global__ __launch_bounds__(kPartBlock) void k_split(GenPartArgs ga, PartArgs p
   const uint64_t t0 = (uint64_t)blockIdx.x * kPartTile;
   if (t0 >= n) return;  // uniform
   const uint32_t F = 1u << (ga.bin_bits - kBinBits);
+  const uint32_t cmask = (uint32_t)((1ull << ga.bin_bits) - 1ull);
   for (uint32_t f = tid; f <= F; f += kPartBlock) s_cnt[f] = 0;
   __syncthreads();
   const uint32_t *src = reinterpret_cast<const uint32_t *>(ga.rec) + (uint64_t)cb * ga.cap;
@@ -226,7 +228,7 @@ __global__ __launch_bounds__(kPartBlock) void k_split(GenPartArgs ga, PartArgs p
     const uint4 &w = v[j >> 2];
     const uint32_t o = (j & 3) == 0 ? w.x : (j & 3) == 1 ? w.y : (j & 3) == 2 ? w.z : w.w;
     const bool ok = o != 0xFFFFFFFFu && i0 + j < n;
-    const uint32_t f = ok ? (o >> kBinBits) : F;
+    const uint32_t f = ok ? ((o & cmask) >> kBinBits) : F;  // (lane tag bits dropped)
     E[j] = (f << 16) | atomicAdd(&s_cnt[f], 1u);
     O[j] = o & (kBinsPerBucket - 1);
   }
@@ -239,9 +241,12 @@ __global__ __launch_bounds__(kPartBlock) void k_split(GenPartArgs ga, PartArgs p
 // records.  One workgroup per (top bucket, slice): the bucket's records are
 // matched against its top offsets; a hit's segment (binary search of the
 // descriptors by first-record index) names its tile, which goes to the list
-// once per workgroup.  The uniques rescan then runs on the listed tiles only:
-// at config 5 (0.45 k-mers per neuron) a few tiles instead of all 14,000.
+// once per pass (mark[tile] = epoch); lane-tagged records also set their
+// lane's bit (lanes[tile][16]).  The uniques rescan then runs on the listed
+// tiles only (and, tagged, hashes only the marked lanes): at config 5 (0.45
+// k-mers per neuron) a fraction of the 14,000 tiles.
 constexpr int kTileSeen = 256;
+constexpr int kHitQueue = 4096;
 template <bool WIDE>
 __global__ __launch_bounds__(kHistBlock) void k_uniq_tiles(GenPartArgs ga, UniqArgs u,
                                                            const uint32_t *__restrict__ tbuckets,
@@ -249,22 +254,24 @@ __global__ __launch_bounds__(kHistBlock) void k_uniq_tiles(GenPartArgs ga, UniqA
                                                            uint32_t slices, uint32_t *__restrict__ tiles,
                                                            uint32_t *__restrict__ n_list,
                                                            uint32_t max_list, uint32_t *__restrict__ flag,
-                                                           uint32_t *__restrict__ mark, uint32_t epoch) {
+                                                           uint32_t *__restrict__ mark, uint32_t epoch,
+                                                           uint32_t *__restrict__ lanes, uint32_t qcap) {
   using Rec = typename GenShape<WIDE>::Rec;
   __shared__ uint32_t t_off[kMaxTopN];
   __shared__ uint32_t s_seen[kTileSeen];
-  __shared__ uint32_t t_n, s_ns;
+  __shared__ uint32_t t_n, h_n;
+  __shared__ uint32_t h_i[kHitQueue], h_rec[kHitQueue];  // queued hits: record index, record
   if (blockIdx.y >= *n_tb) return;  // uniform
   const uint32_t b = tbuckets[blockIdx.y], r = blockIdx.x;
-  if (threadIdx.x == 0) { t_n = 0; s_ns = 0; }
-  // (a slot claimed but not yet written reads as the sentinel: never a false
-  // duplicate -- LDS left by earlier kernels holds small integers like tile ids)
+  if (threadIdx.x == 0) { t_n = 0; h_n = 0; }
+  // (LDS left by earlier kernels holds small integers like tile ids: a
+  // sentinel, never a false duplicate)
   for (int i = threadIdx.x; i < kTileSeen; i += kHistBlock) s_seen[i] = 0xFFFFFFFFu;
   __syncthreads();
+  const uint32_t omask = (uint32_t)((1ull << ga.bin_bits) - 1ull);
   for (uint32_t i = threadIdx.x; i < u.n_top; i += kHistBlock) {
     const uint64_t idx = u.top[i].idx;
-    if ((idx >> ga.bin_bits) == b)
-      t_off[atomicAdd(&t_n, 1u)] = (uint32_t)(idx & ((1ull << ga.bin_bits) - 1ull));
+    if ((idx >> ga.bin_bits) == b) t_off[atomicAdd(&t_n, 1u)] = (uint32_t)idx & omask;
   }
   __syncthreads();
   const uint32_t tn = t_n;
@@ -272,14 +279,23 @@ __global__ __launch_bounds__(kHistBlock) void k_uniq_tiles(GenPartArgs ga, UniqA
   if (n > ga.cap) n = ga.cap;
   uint64_t n_seg = ga.fill[b] >> 40;
   if (n_seg > ga.max_segs) n_seg = ga.max_segs;
-  const uint64_t lo = n * r / slices, hi = n * (r + 1) / slices;
+  // slice bounds on 64-record boundaries (the region base is 64-aligned): only
+  // the last slice's tail is not a whole 4-record group
+  auto bound = [&](uint32_t q) -> uint64_t { return q >= slices ? n : ((n * q / slices) & ~63ull); };
+  const uint64_t lo = bound(r), hi = bound(r + 1);
   const Rec *src = reinterpret_cast<const Rec *>(ga.rec) + (uint64_t)b * ga.cap;
   const uint2 *d = ga.desc + (uint64_t)b * ga.max_segs;
-  for (uint64_t i = lo + threadIdx.x; i < hi; i += kHistBlock) {
-    const uint32_t off = (uint32_t)src[i];
-    bool hit = false;
-    for (uint32_t t = 0; t < tn; ++t) hit |= t_off[t] == off;  // (pads never match)
-    if (!hit) continue;
+  const bool tagged = WIDE && ga.lane_tag && lanes;
+  // a record -> the list entry it adds (~0u: none): a top row's record names
+  // its tile (segment binary search) and, tagged, its lane; each entry once
+  // per pass (tile: mark[tile] = epoch; lane: its bit)
+  auto match = [&](uint32_t rec) -> bool {
+    const uint32_t off = rec & omask;
+    bool h = false;
+    for (uint32_t t = 0; t < tn; ++t) h |= t_off[t] == off;  // (pads never match)
+    return h;
+  };
+  auto entry = [&](uint64_t i, uint32_t rec) -> uint32_t {
     uint64_t a = 0, z = n_seg;  // last segment with first record <= i
     while (z - a > 1) {
       const uint64_t m = (a + z) >> 1;
@@ -287,19 +303,77 @@ __global__ __launch_bounds__(kHistBlock) void k_uniq_tiles(GenPartArgs ga, UniqA
       else z = m;
     }
     const uint32_t tile = d[a].x;
-    bool dup = false;
-    const uint32_t ns = s_ns < (uint32_t)kTileSeen ? s_ns : (uint32_t)kTileSeen;
-    for (uint32_t j = 0; j < ns && !dup; ++j) dup = s_seen[j] == tile;
-    if (dup) continue;
-    const uint32_t at = atomicAdd(&s_ns, 1u);
-    if (at < (uint32_t)kTileSeen) s_seen[at] = tile;
-    // once per pass over all workgroups (the list holds at most n_tiles
-    // entries: the rescan's grid is sized for that)
-    if (atomicExch(&mark[tile], epoch) == epoch) continue;
-    const uint32_t g = atomicAdd(n_list, 1u);
-    if (g < max_list) tiles[g] = tile;
+    if (tagged) {
+      const uint32_t lane = rec >> ga.bin_bits, bit = 1u << (lane & 31);
+      if (atomicOr(&lanes[(uint64_t)tile * kLaneWords + (lane >> 5)], bit) & bit) return ~0u;
+      return (tile << 9) | lane;
+    }
+    // a direct-mapped LDS cache of the tiles this workgroup listed (O(1); a
+    // miss only costs the global mark)
+    uint32_t &seen = s_seen[tile & (kTileSeen - 1)];
+    if (seen == tile) return ~0u;
+    seen = tile;
+    return atomicExch(&mark[tile], epoch) == epoch ? ~0u : tile;
+  };
+  // appends of a wave's active lanes: one counter atomic per wave (the top
+  // rows are hot: thousands of records each)
+  const uint32_t lane_id = threadIdx.x & 63u;
+  auto append = [&](uint32_t ent) {
+    const bool w = ent != ~0u;
+    const uint64_t m = __ballot(w);
+    if (!m) return;
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if ((int)lane_id == leader) base = atomicAdd(n_list, (uint32_t)__popcll(m));
+    base = __shfl(base, leader, 64);
+    if (!w) return;
+    const uint32_t g = base + (uint32_t)__popcll(m & ((1ull << lane_id) - 1ull));
+    if (g < max_list) tiles[g] = ent;
     else atomicOr(flag, 1u);  // list full: the caller rescans everything
+  };
+  // 4 records per lane per load (16 B wide, 8 B narrow), 4 loads in flight
+  constexpr int kU = 4;
+  constexpr uint64_t kStep = 4ull * kHistBlock;
+  for (uint64_t i0 = lo + 4ull * threadIdx.x; i0 < hi; i0 += kU * kStep) {
+    uint32_t v[kU][4];
+#pragma unroll
+    for (int q = 0; q < kU; ++q) {
+      const uint64_t ii = i0 + q * kStep;
+      if (ii + 4 <= hi) {
+        if (WIDE) {
+          const uint4 w = *reinterpret_cast<const uint4 *>(src + ii);
+          v[q][0] = w.x; v[q][1] = w.y; v[q][2] = w.z; v[q][3] = w.w;
+        } else {
+          const uint2 w = *reinterpret_cast<const uint2 *>(src + ii);
+          v[q][0] = w.x & 0xFFFFu; v[q][1] = w.x >> 16; v[q][2] = w.y & 0xFFFFu; v[q][3] = w.y >> 16;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[q][e] = ii + e < hi ? (uint32_t)src[ii + e] : (uint32_t)GenShape<WIDE>::kPad;
+      }
+    }
+    // hits are queued in LDS and resolved together below: a wave resolving
+    // its hits one record step at a time chains 14 dependent descriptor loads
+    // per hit (measured 470 us at config 5: ~9 hits per wave, 147 k hits)
+#pragma unroll
+    for (int q = 0; q < kU; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint64_t ii = i0 + q * kStep + e;
+        if (ii < hi && match(v[q][e])) {
+          const uint32_t at = atomicAdd(&h_n, 1u);
+          if (at < qcap) {
+            h_i[at] = (uint32_t)ii;
+            h_rec[at] = v[q][e];
+          } else {
+            append(entry(ii, v[q][e]));  // queue full: resolved in place
+          }
+        }
+      }
   }
+  __syncthreads();
+  const uint32_t nq = h_n < qcap ? h_n : qcap;
+  for (uint32_t j = threadIdx.x; j < nq; j += kHistBlock) append(entry(h_i[j], h_rec[j]));
 }
 
 // K1k: the exact table's distinct keys -> kmer_per_neuron, as a count of a key
@@ -422,13 +496,15 @@ hipError_t launch_part_gen(const KmerInput &in, int k, int canonical, int km, ui
 hipError_t launch_uniq_tiles(const GenPartArgs &ga, int wide, const UniqArgs &u,
                              const uint32_t *tbuckets, const uint32_t *n_tb, uint32_t max_tb,
                              uint32_t slices, uint32_t *tiles, uint32_t *n_list, uint32_t max_list,
-                             uint32_t *flag, uint32_t *mark, uint32_t epoch, hipStream_t s) {
+                             uint32_t *flag, uint32_t *mark, uint32_t epoch, uint32_t *lanes,
+                             uint32_t hit_queue, hipStream_t s) {
   if (!max_tb || !ga.desc) return hipSuccess;
+  const uint32_t qcap = hit_queue < (uint32_t)kHitQueue ? hit_queue : (uint32_t)kHitQueue;
   const dim3 g(slices ? slices : 1, max_tb), b(kHistBlock);
   if (wide) hipLaunchKernelGGL(k_uniq_tiles<true>, g, b, 0, s, ga, u, tbuckets, n_tb, slices ? slices : 1,
-                               tiles, n_list, max_list, flag, mark, epoch);
+                               tiles, n_list, max_list, flag, mark, epoch, lanes, qcap);
   else hipLaunchKernelGGL(k_uniq_tiles<false>, g, b, 0, s, ga, u, tbuckets, n_tb, slices ? slices : 1,
-                          tiles, n_list, max_list, flag, mark, epoch);
+                          tiles, n_list, max_list, flag, mark, epoch, lanes, qcap);
   return hipGetLastError();
 }
 

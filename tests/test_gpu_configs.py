@@ -337,7 +337,9 @@ POOL2 = 2_000_000
 @pytest.mark.parametrize("k,pool,canon,width,tile_list", [
     (40, 2_000_003, True, 64, None),      # Gen: dense hits (57 k-mers per neuron)
     (40, 2_000_003, True, 64, 3),         # ... list overflow -> the full rescan
-    (63, 40_000_003, True, 128, None),    # Wide, 128-bit keys
+    (63, 40_000_003, True, 128, None),    # Wide, 128-bit keys (lane-tagged records)
+    (63, 40_000_003, True, 128, "untagged"),  # ... without lane tags: whole listed tiles
+    (33, 30_000_001, True, 64, "queue1"),  # hits resolved in place (LDS hit queue of 1)
     (33, 30_000_001, False, 64, 2),       # Wide, pack_kmer keys, list overflow
     (63, C5_POOL, True, 64, None),        # config-5 pool, compat keys
 ])
@@ -350,7 +352,9 @@ def test_uniques_from_kept_records(k, pool, canon, width, tile_list):
                                      motif_len=120, n_rate=0.002, mixed_case=True)
     r = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, canon, width=width)
     r.process_parallel_arrays(bases, offs, THREADS)
-    kv = {"NK_UNIQ_TILE_LIST": tile_list} if tile_list else {}
+    kv = ({"NK_NO_LANE_TAG": 1} if tile_list == "untagged" else
+          {"NK_UNIQ_HIT_QUEUE": 1} if tile_list == "queue1" else
+          {"NK_UNIQ_TILE_LIST": tile_list} if tile_list else {})
     with env(**kv):
         g = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, canon, kmer_width=width)
         g.process_parallel_arrays(bases, offs)
@@ -358,6 +362,50 @@ def test_uniques_from_kept_records(k, pool, canon, width, tile_list):
         g.process_parallel_arrays(bases, offs)  # state carries over
     r.process_parallel_arrays(bases, offs, THREADS)
     assert_same(g, r)
+    g.close()
+
+
+@pytest.mark.parametrize("k,pool,width,top_n", [
+    (40, 2_000_003, 64, 100),    # Gen, top-N not fused into the LIF (top_n > 64)
+    (33, 30_000_001, 64, 20),    # Wide
+    (63, 40_000_003, 128, 20),   # Wide, 128-bit keys
+])
+def test_k1b_fused_lif(k, pool, width, top_n):
+    """The LIF from the reset state run inside the write-through K1b (Gen/Wide,
+    one batch, a top-N not fused into the LIF kernel): bit-exact vs the oracle
+    on a process call, a second call (state carries: the LIF kernel runs), and
+    the split API (accumulate + finalize, in-memory and streaming rule), with
+    the counts touched (device_currents) or the steps changed in between (the
+    K1b result is dropped and the LIF kernel runs)."""
+    bases, offs = synth.make_records(1_000_000, 5, seed=900 + k, repeats_per_mb=3000,
+                                     motif_len=120, n_rate=0.002, mixed_case=True)
+    r = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, True, width=width)
+    r.process_parallel_arrays(bases, offs, THREADS)
+    g = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, True, kmer_width=width, top_n=top_n)
+    g.process_parallel_arrays(bases, offs)
+    assert_same(g, r, n=top_n)
+    g.process_parallel_arrays(bases, offs)
+    r.process_parallel_arrays(bases, offs, THREADS)
+    assert_same(g, r, n=top_n)
+    d_b = torch.from_numpy(np.concatenate([bases, np.zeros(16, np.uint8)])).cuda()
+    d_o = torch.from_numpy(offs.view(np.int64)).cuda()
+    torch.cuda.synchronize()
+    for streaming, between in ((False, None), (True, None), (False, "currents"), (False, "steps")):
+        g.reset()
+        r = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, True, width=width)
+        g.accumulate_device(d_b.data_ptr(), d_o.data_ptr(), offs.size - 1, bases.size)
+        if between == "currents":
+            g.device_currents_ptr()
+        elif between == "steps":
+            g.set_steps(700)
+            r.set_steps(700)
+        g.finalize(streaming=streaming)
+        if streaming:
+            r.process_streaming_arrays(bases, offs, THREADS)
+        else:
+            r.process_parallel_arrays(bases, offs, THREADS)
+        assert_same(g, r, n=top_n)
+        g.set_steps(1000)
     g.close()
 
 
