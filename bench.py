@@ -62,6 +62,10 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 METRIC = "Mk-mers/sec at k=31, pool=2M; total-spikes bit-exact vs CPU ref"
+SIDE_METRIC = {  # side lines (not BASELINE.json's metric): their own labels
+    "config4": "Mk-mers/sec at k=31, pool=2M, one input split across the GPUs (strong scaling)",
+    "config5": "Mk-mers/sec at k=63, pool=256M, 128-bit keys (BASELINE.json configs[4])",
+}
 K = 31
 POOL = 2_000_000
 BASES = 115_000_000
@@ -174,6 +178,10 @@ def main() -> int:
     # own communicator) unless --dist-python drives it from Python with torch's
     # collectives between the library calls (the round-2 protocol, for A/B)
     ap.add_argument("--dist-python", action="store_true")
+    # diagnosis: the process group (and the library's communicator) set up, the
+    # step itself the plain one-GPU step (what RCCL's presence alone costs)
+    ap.add_argument("--dist-init-only", action="store_true")
+    ap.add_argument("--nk-comm", action="store_true", help="the library's communicator under gloo too")
     ap.add_argument("--inflight", type=int, default=None, choices=(1, 2, 3, 4),
                     help="batches in flight (default: 3 on one GPU, 1 across ranks and for "
                          "config5): > 1 "
@@ -226,8 +234,8 @@ def main() -> int:
     from neurokmer_amd import SpikingKmerCounter, synth
     from neurokmer_amd import dist as nkdist
     from neurokmer_amd.counter import diag_hash_ms
-    comm = nkdist.Comm(device=dev_idx) if dist_on and backend == "nccl" and not args.dist_python \
-        else None
+    comm = nkdist.Comm(device=dev_idx) if dist_on and (backend == "nccl" or args.nk_comm) and \
+        not args.dist_python else None
 
     # ---- this rank's input (resident in HBM) -------------------------------
     if args.workload in ("config2", "config5"):
@@ -307,7 +315,7 @@ def main() -> int:
         merged on the device; `between` (the next batch's count) is enqueued
         once the all-reduce is, so that count waits for the all-reduce only."""
         c = ctrs[j]
-        if not dist_on:
+        if not dist_on or args.dist_init_only:
             if between is not None:
                 between()
             c.finalize(False, st.cuda_stream)
@@ -460,7 +468,8 @@ def main() -> int:
         frac_h = valu.get("frac_of_hash_only", 0.0)
         bound = "valu" if frac_h >= 0.6 and frac_h >= hbm_frac else ("hbm" if hbm_frac >= 0.6 else "latency")
         out = {
-            "metric": METRIC, "value": round(value, 3), "unit": "Mk-mers/s", "n_gpus": world,
+            "metric": METRIC if args.workload == "config2" else SIDE_METRIC[args.workload],
+            "value": round(value, 3), "unit": "Mk-mers/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "settle_steps": settle,
             "ms_per_step": round(ms_step, 4),
             "inflight": args.inflight,
@@ -479,7 +488,9 @@ def main() -> int:
                        "collectives": ("in-library RCCL (nk_finalize_dist)" if comm is not None
                                        else (f"torch.distributed {backend} from Python" if dist_on
                                              else None))},
-            "roofline": {"bound": bound, "kernel": "k_part<canonical> (K1a)",
+            "roofline": {"bound": bound,
+                         "kernel": ("k_part<canonical> (K1a)" if k <= 32 and pool <= (1 << 24)
+                                    else "the count: k_part_gen (K1g) + k_split (K1s)"),
                          "achieved": round(achieved / 1e9, 2), "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": round(hbm_frac, 4),
                          "traffic": traffic, "traffic_source": pmc.get("source") if traffic else None,
