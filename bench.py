@@ -207,8 +207,15 @@ def main() -> int:
     ndev = torch.cuda.device_count()  # counts devices without initialising them
     shared = world > ndev  # rehearsal: ranks share devices
     dev_idx = local % max(ndev, 1)
-    backend = args.dist_backend or ("gloo" if shared else "nccl")
     dist_on = world > 1 or args.force_dist
+    # the device collectives: the library's own RCCL communicator (the whole
+    # finish inside nk_finalize_dist) unless --dist-python drives torch's.  The
+    # process group then only bootstraps it (the unique id) and times the run
+    # (barriers, max over ranks): gloo.  A torch RCCL group in the process
+    # slowed K1a by 5-20 % even when unused (1-rank rehearsal: 0.599-0.628 vs
+    # 0.576-0.577 ms per step with gloo, plain 0.546-0.549, profiles/r03_s10..s12)
+    lib_comm = dist_on and not shared and not args.dist_python
+    backend = args.dist_backend or ("gloo" if shared or lib_comm else "nccl")
     if args.inflight is None:
         # across ranks the finish holds the collectives: beside the next
         # batch's count their kernels wait for its workgroups, so the
@@ -234,8 +241,7 @@ def main() -> int:
     from neurokmer_amd import SpikingKmerCounter, synth
     from neurokmer_amd import dist as nkdist
     from neurokmer_amd.counter import diag_hash_ms
-    comm = nkdist.Comm(device=dev_idx) if dist_on and (backend == "nccl" or args.nk_comm) and \
-        not args.dist_python else None
+    comm = nkdist.Comm(device=dev_idx) if (lib_comm or (dist_on and args.nk_comm)) else None
 
     # ---- this rank's input (resident in HBM) -------------------------------
     if args.workload in ("config2", "config5"):
@@ -485,7 +491,9 @@ def main() -> int:
                        "kmers_rank0": nk_rank, "kmers_total": total_kmers,
                        "parallelism": f"dp{world}" + (f" (rehearsal: {world} ranks on {ndev} GPU, "
                                                       f"{backend})" if shared else ""),
-                       "collectives": ("in-library RCCL (nk_finalize_dist)" if comm is not None
+                       "collectives": ((f"in-library RCCL communicator (nk_finalize_dist); "
+                                        f"torch.distributed {backend} for bootstrap and timing")
+                                       if comm is not None
                                        else (f"torch.distributed {backend} from Python" if dist_on
                                              else None))},
             "roofline": {"bound": bound,

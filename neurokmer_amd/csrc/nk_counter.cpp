@@ -201,6 +201,11 @@ struct nk_counter {
   // finalize is skipped while nothing else touched the currents or the state
   bool k1b_lif = false;
   LifParams k1b_lp{};
+  // nk_finalize_dist: the world size of the merge that follows the next export
+  // (the export's header kernel empties the merge set, nk_merge_export then
+  // skips k_merge_prep for that capacity)
+  uint32_t merge_world_hint = 0;
+  uint64_t merge_prepped = 0;
   // min(spike count, 255) per neuron, written by a LIF whose top-N is not fused
   // (large pools): what the top-N passes read first (1 B instead of 8 per neuron)
   DevBuf<uint8_t> sc8;
@@ -462,6 +467,7 @@ int counter_key_words(const nk_counter *c) { return c->w128 ? 2 : 1; }
 bool counter_kpn_global(const nk_counter *c) {
   return c->opts.exact_counts && c->exact_built && c->kpn_global;
 }
+void counter_merge_hint(nk_counter *c, uint32_t world) { c->merge_world_hint = world; }
 uint64_t *counter_currents_on(nk_counter *c, hipStream_t stream) {
   if (c->cur_in_wire) {
     fail(NK_E_INVALID, "the currents are in the wire vector until nk_finalize_export");
@@ -948,6 +954,13 @@ static hipError_t batch_count(nk_counter *c, const CountPlan &cp, const KmerInpu
   return launch_zero(z, s);
 }
 
+// a positive integer from the environment (tests: force the rare branches)
+static uint32_t env_u32(const char *name, uint32_t dflt) {
+  const char *e = getenv(name);
+  const unsigned long v = e ? strtoul(e, nullptr, 10) : 0;
+  return v ? (uint32_t)v : dflt;
+}
+
 // defer_partials: leave K1c (currents += partials) to the LIF kernel of the
 // same process call instead of a separate pass
 static bool top_fused(const nk_counter *c, uint64_t want);
@@ -1322,13 +1335,6 @@ static int enqueue_select(nk_counter *c, uint64_t want, hipStream_t s, uint64_t 
 #ifndef NK_U1_SLICE_BUDGET
 #define NK_U1_SLICE_BUDGET 1024  // scan workgroups per launch (A/B: 1024 with 4 loads in flight best)
 #endif
-// a positive integer from the environment (tests: force the rare branches)
-static uint32_t env_u32(const char *name, uint32_t dflt) {
-  const char *e = getenv(name);
-  const unsigned long v = e ? strtoul(e, nullptr, 10) : 0;
-  return v ? (uint32_t)v : dflt;
-}
-
 static int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, bool post_done,
                            hipStream_t s) {
   const bool part = c->part_used && !rescan;
@@ -1823,10 +1829,15 @@ static int merge_keys(nk_counter *c, const MergeSrc &src, uint64_t max_keys, int
 // the segment header flags).  sep: into the merge set (mset_*, muniq,
 // mspecial), leaving this shard's own set and uniques as they are (a redo
 // still exports them)
-static int enqueue_merge(nk_counter *c, const MergeSrc &src, uint64_t max_keys, uint32_t m,
-                         hipStream_t s, bool sep) {
+static uint64_t merge_cap(uint64_t max_keys) {
   uint64_t cap = 64;
   while (cap < 2 * max_keys + 2) cap <<= 1;
+  return cap;
+}
+
+static int enqueue_merge(nk_counter *c, const MergeSrc &src, uint64_t max_keys, uint32_t m,
+                         hipStream_t s, bool sep) {
+  const uint64_t cap = merge_cap(max_keys);
   int rc;
   uint64_t &alloc = sep ? c->mset_alloc : c->set_alloc;
   DevBuf<unsigned long long> &keys = sep ? c->mset_keys : c->set_keys;
@@ -1844,7 +1855,11 @@ static int enqueue_merge(nk_counter *c, const MergeSrc &src, uint64_t max_keys, 
   uint64_t *mask = sep ? c->mset_mask_d.p : c->set_mask_d.p;
   uint32_t *uq = sep ? c->muniq.p : c->uniq.p, *sp = sep ? c->mspecial.p : c->special.p;
   if (!sep) c->set_cap = cap;
-  HIPCHK(launch_merge_prep(keys.p, mask, cap, c->w128 ? 1 : 0, uq, sp, m, c->trunc_d.p, s));
+  // (the export's header kernel already emptied the merge set at this capacity)
+  const bool prepped = sep && c->merge_prepped == cap && c->mset_alloc >= cap;
+  c->merge_prepped = 0;
+  if (!prepped)
+    HIPCHK(launch_merge_prep(keys.p, mask, cap, c->w128 ? 1 : 0, uq, sp, m, c->trunc_d.p, s));
   UniqArgs u{};
   u.top = c->cand.p;
   u.n_top = m;
@@ -1855,10 +1870,11 @@ static int enqueue_merge(nk_counter *c, const MergeSrc &src, uint64_t max_keys, 
   u.special = sp;
   MergeSrc ms = src;
   ms.trunc = c->trunc_d.p;
-  if (c->w128)
+  if (c->w128) {
     HIPCHK(launch_set_merge128(ms, c->pool, u, s));
-  else
+  } else {
     HIPCHK(launch_set_merge(ms, c->pool, u, s));
+  }
   return NK_OK;
 }
 
@@ -1970,9 +1986,27 @@ int nk_finalize_export(nk_counter *c, int streaming, const uint32_t *d_wire, uin
   } else if ((rc = lif_top_uniques(c, streaming, false, s, d_wire))) {  // blocking, corrected
     return rc;
   }
+  // the merge that follows (nk_finalize_dist knows its world size): its set
+  // emptied by the header kernel
+  MergePrep mp{};
+  c->merge_prepped = 0;
+  if (c->merge_world_hint && want && !getenv("NK_NO_MERGE_PREP_FUSE")) {
+    const uint64_t mcap = merge_cap((uint64_t)c->merge_world_hint * cap);
+    if (mcap > c->mset_alloc) {
+      if ((rc = c->mset_keys.ensure(c->w128 ? 3 * mcap : mcap))) return rc;
+      c->mset_alloc = mcap;
+    }
+    if ((rc = c->trunc_d.ensure(1)) || (rc = c->mset_mask_d.ensure(1)) ||
+        (rc = c->muniq.ensure(kMaxTopN)) || (rc = c->mspecial.ensure(kMaxTopN)))
+      return rc;
+    mp = MergePrep{c->mset_keys.p, c->mset_mask_d.p, mcap, c->muniq.p, c->mspecial.p, (uint32_t)want,
+                   c->trunc_d.p};
+    c->merge_prepped = mcap;
+  }
+  c->merge_world_hint = 0;
   HIPCHK(launch_export(c->set_keys.p, c->set_mask_d.p, c->set_alloc, c->w128 ? 1 : 0, uniq,
                        fused, c->special.p, (uint32_t)want, want ? c->topst.p : nullptr,
-                       c->post_flags.p, cap, d_seg, c->export_n.p, s));
+                       c->post_flags.p, cap, d_seg, c->export_n.p, s, mp));
   c->export_pending = true;
   c->export_blocking = !fused;
   c->export_want = (uint32_t)want;

@@ -259,6 +259,7 @@ int nk_finalize_dist(nk_counter *c, nk_comm *m, int streaming, uint64_t total_km
   }
   const size_t stride = 1 + (size_t)nk::counter_key_words(c) * cap;
   OOM(b.seg.ensure(stride) && b.all.ensure(W * stride), "export segments");
+  nk::counter_merge_hint(c, (uint32_t)W);
   RC(nk_finalize_export(c, streaming, wire, b.seg.p, cap, stream));
   NCCLCHK(rccl().all_gather(b.seg.p, b.all.p, stride, ncclUint64, m->comm, s));
   int redo = 0;

@@ -19,5 +19,8 @@ int counter_key_words(const nk_counter *c);
 bool counter_kpn_global(const nk_counter *c);
 // the u64 currents complete on stream s (lazily-zero currents materialised,
 // pending K1b partials folded, no host wait); null on error
+// the world size of the merge after the next nk_finalize_export (its set is
+// then emptied by the export's header kernel)
+void counter_merge_hint(nk_counter *c, uint32_t world);
 uint64_t *counter_currents_on(nk_counter *c, hipStream_t s);
 }  // namespace nk

@@ -280,11 +280,23 @@ hipError_t launch_merge_prep(unsigned long long *set_keys, uint64_t *mask, uint6
 hipError_t launch_wire32(const uint64_t *cur, const uint32_t *partials, uint32_t slices,
                          const uint32_t *over, int over_bits, uint64_t pool, uint32_t *wire,
                          hipStream_t s);
+// the merge that follows an export, prepared by the export's header kernel
+// (k_merge_prep's work: the merge set emptied at capacity cap, its mask, the
+// merge's uniques column and kEmpty flags, the truncation word): S == null: none
+struct MergePrep {
+  unsigned long long *S = nullptr;
+  uint64_t *mask = nullptr;
+  uint64_t cap = 0;
+  uint32_t *uniq = nullptr;
+  uint32_t *special = nullptr;
+  uint32_t m = 0;
+  uint32_t *trunc = nullptr;
+};
 hipError_t launch_export(const unsigned long long *set_keys, const uint64_t *set_mask,
                          uint64_t set_alloc, int w128, bool uniq, bool appended,
                          const uint32_t *special, uint32_t n_top, const TopState *st,
                          const uint32_t *post_flags, uint64_t cap_out, uint64_t *dst,
-                         unsigned long long *count, hipStream_t s);
+                         unsigned long long *count, hipStream_t s, const MergePrep &mp = MergePrep{});
 hipError_t launch_gather(const TopState *st, const uint64_t *stats, const uint64_t *mask,
                          const uint32_t *flags, const uint32_t *flag3, const TopCand *cand,
                          const uint32_t *uniq, uint32_t m, uint8_t *out, uint64_t *done,

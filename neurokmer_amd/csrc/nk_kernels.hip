@@ -2060,10 +2060,30 @@ __global__ void k_export_keys(const unsigned long long *__restrict__ S,
   }
 }
 
+// the segment header (one lane) and, with mp.S, the next merge's prep (the
+// whole grid: one launch fewer between the export and the merge)
 __global__ void k_export_hdr(unsigned long long *__restrict__ count, const uint32_t *__restrict__ special,
                              uint32_t n_top, const TopState *__restrict__ st,
                              const uint32_t *__restrict__ post_flags, int w128, uint64_t cap_out,
-                             uint64_t *__restrict__ dst) {
+                             uint64_t *__restrict__ dst, MergePrep mp) {
+  if (mp.S) {
+    const uint64_t nw = w128 ? 3 * mp.cap : mp.cap;
+    const unsigned long long fill = w128 ? 0ull : kEmpty;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw;
+         i += (uint64_t)gridDim.x * blockDim.x)
+      mp.S[i] = fill;
+    if (blockIdx.x == 0) {
+      for (uint32_t t = threadIdx.x; t < mp.m; t += blockDim.x) {
+        mp.uniq[t] = 0;
+        mp.special[t] = 0;
+      }
+      if (threadIdx.x == 0) {
+        *mp.mask = mp.cap - 1;
+        *mp.trunc = 0;
+      }
+    }
+  }
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
   uint64_t n = *count;
   *count = 0;  // ready for the next export
   uint64_t flags = (st && st->refine) ? 4u : 0u;
@@ -2128,15 +2148,20 @@ hipError_t launch_export(const unsigned long long *set_keys, const uint64_t *set
                          uint64_t set_alloc, int w128, bool uniq, bool appended,
                          const uint32_t *special, uint32_t n_top, const TopState *st,
                          const uint32_t *post_flags, uint64_t cap_out, uint64_t *dst,
-                         unsigned long long *count, hipStream_t s) {
+                         unsigned long long *count, hipStream_t s, const MergePrep &mp) {
   if (uniq && !appended) {  // scan the set; grid for the largest capacity, blocks past *set_mask + 1 idle
     unsigned g = (unsigned)((set_alloc + 255) / 256);
     if (g > 1024) g = 1024;
     hipLaunchKernelGGL(k_export_keys, dim3(g), dim3(256), 0, s, set_keys, set_mask, w128, cap_out,
                        dst, count);
   }
-  hipLaunchKernelGGL(k_export_hdr, dim3(1), dim3(1), 0, s, count, special, n_top, st,
-                     uniq ? post_flags : nullptr, w128, cap_out, dst);
+  unsigned g = 1, b = 1;
+  if (mp.S) {
+    g = (unsigned)std::min<uint64_t>(((w128 ? 3 : 1) * mp.cap + 255) / 256, 2048);
+    b = 256;
+  }
+  hipLaunchKernelGGL(k_export_hdr, dim3(g ? g : 1), dim3(b), 0, s, count, special, n_top, st,
+                     uniq ? post_flags : nullptr, w128, cap_out, dst, mp);
   return hipGetLastError();
 }
 
