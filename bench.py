@@ -235,6 +235,7 @@ def main() -> int:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
         else:
+            os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")  # one node, 127.0.0.1
             dist.init_process_group(backend)
     dev = torch.device("cuda", dev_idx)
 
