@@ -217,13 +217,19 @@ def main() -> int:
     lib_comm = dist_on and not shared and not args.dist_python
     backend = args.dist_backend or ("gloo" if shared or lib_comm else "nccl")
     if args.inflight is None:
-        # across ranks the finish holds the collectives: beside the next
-        # batch's count their kernels wait for its workgroups, so the
-        # overlapped step measured slower (1-rank RCCL rehearsal, 0.698 vs
-        # 0.624 ms, profiles/r02_s21)
         # config 5 (P = 256 M): its finish is a 256 M-neuron LIF + top-N pass
-        # that gains nothing beside a count (5.15 vs 5.02-5.07 ms, r02_s29)
-        args.inflight = 1 if dist_on or args.workload == "config5" else 3
+        # that gains nothing beside a count (5.15 vs 5.02-5.07 ms, r02_s29).
+        # Across ranks with the in-library finish two batches in flight (the
+        # next count enqueued before this batch's finish: 1-rank rehearsal
+        # 0.5618 vs 0.5743 ms one at a time, profiles/r03_s17); three measured
+        # slower (0.68 ms, r03_s12), and so did the Python-driven finish with
+        # any overlap (0.698 vs 0.624 ms, profiles/r02_s21)
+        if args.workload == "config5":
+            args.inflight = 1
+        elif dist_on:
+            args.inflight = 2 if lib_comm else 1
+        else:
+            args.inflight = 3
     if dist_on:
         if "RANK" not in os.environ:  # --force-dist without a launcher: a 1-rank group
             with socket.socket() as sk:

@@ -1259,8 +1259,7 @@ static int enqueue_lif(nk_counter *c, int streaming, uint32_t fuse_want, bool pa
   // (a LIF with no count since the last one: that one's derived state first)
   int rc = settle_state(c, s);
   if (rc) return rc;
-  const bool k1b = k1b_lif_holds(c, lif_params(c, streaming), fuse_want, wire) &&
-                   !getenv("NK_NO_K1B_LIF_USE");
+  const bool k1b = k1b_lif_holds(c, lif_params(c, streaming), fuse_want, wire);
   c->k1b_lif = false;
   if (k1b) {  // sc8, hist and stats are this LIF's: the state is derived
     c->lif_zeroed = false;

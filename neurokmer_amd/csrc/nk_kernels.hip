@@ -2427,22 +2427,12 @@ hipError_t launch_pad_keys(const uint64_t *src, const unsigned long long *n_src,
   return hipGetLastError();
 }
 
-// A/B experiments: NK_K1A_DYN_LDS=bytes of unused dynamic LDS per K1a
-// workgroup (fewer resident workgroups per CU leave room for other kernels)
-static size_t k1a_dyn_lds() {
-  static const size_t v = [] {
-    const char *e = getenv("NK_K1A_DYN_LDS");
-    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)0;
-  }();
-  return v;
-}
-
 hipError_t launch_part(const KmerInput &in, int k, int canonical, uint64_t pool,
                        const PartArgs &pa, hipStream_t s) {
   if (!in.n_tiles) return hipSuccess;
   FastMod fm = make_fastmod(pool);
   const dim3 g((unsigned)in.n_tiles), bl(kPartBlock);
-  const size_t dyn = k1a_dyn_lds();
+  const size_t dyn = 0;
   if (pa.n_buckets > (uint32_t)kMaxBuckets) return hipErrorInvalidValue;
   if (pa.n_buckets <= 256) {
 #if !defined(NK_K1A_NO_K16)  // (A/B: the masked low word)
