@@ -219,14 +219,28 @@ struct nk_counter {
   DevBuf<uint32_t> xp_cnt;
   DevBuf<unsigned long long> xp_ctr;
   DevBuf<uint8_t> x_tmp;
-  DevBuf<unsigned long long> x_n;  // [0] keys of the last input, [1] distinct keys
+  // [0] keys of the last input (sorted build) / of a process_sequence record,
+  // [1] table entries (sorted: distinct keys; grouped: span + side part),
+  // [2] grouped: first index of the side part, [3] side part's entries,
+  // [4] grouped span, [5] side records, [6] grouped: distinct keys, [7] scratch
+  DevBuf<unsigned long long> x_n;
   // kmer_per_neuron by partition (table_kpn): fine / coarse bucket regions,
   // K1b partials, and the overflow + slices == 1 target (all zero between uses)
   DevBuf<uint16_t> xk_off;
   DevBuf<uint32_t> xk_over, xk_wrec, xk_wover, xk_part;
   DevBuf<unsigned long long> xk_fill, xk_wfill, xk_cur;
   size_t xk_cur_zeroed = 0;
-  bool exact_built = false;        // the sorted table holds the last process/accumulate input
+  bool exact_built = false;        // the table holds the last process/accumulate input
+  // the grouped table (nk_table.hip): ent per neuron; the count's K1a<KEYS>
+  // keys (p_key, kept_keys: the count arena holds this input's keyed records)
+  // or the table's own K1a<KEYS> arena (xg_*), the regrouped records, the side list
+  bool x_grouped = false;
+  bool kept_keys = false;
+  DevBuf<uint64_t> x_ent, p_key, xg_key, xg_key2, xg_side;
+  DevBuf<uint16_t> xg_off;
+  DevBuf<uint32_t> xg_over, xg_cnt, xg_gst, xg_trec;
+  DevBuf<unsigned long long> xg_fill, xg_bctr;
+  DevBuf<uint8_t> xg_bin2;
   // process_sequence: delta counts on top of the sorted table, kmer_per_neuron
   DevBuf<unsigned long long> d_keys, d_meta;
   DevBuf<uint32_t> d_vals;
@@ -591,6 +605,10 @@ void nk_free(nk_counter *c) {
   c->x_keys.release(); c->x_sorted.release(); c->x_uniq.release(); c->x_q.release();
   c->x_cnt.release(); c->x_tile_rec.release(); c->kpn.release(); c->x_out.release();
   c->x_pres.release(); c->x_tmp.release(); c->x_n.release();
+  c->x_ent.release(); c->p_key.release(); c->xg_key.release(); c->xg_key2.release();
+  c->xg_side.release(); c->xg_off.release(); c->xg_over.release(); c->xg_cnt.release();
+  c->xg_gst.release(); c->xg_trec.release(); c->xg_fill.release(); c->xg_bin2.release();
+  c->xg_bctr.release();
   c->d_keys.release(); c->d_meta.release(); c->d_vals.release(); c->touched.release();
   c->tile_rec.release(); c->hist.release(); c->tie_cnt.release(); c->uniq.release();
   c->span.release();
@@ -707,16 +725,33 @@ static int table_kpn(nk_counter *c, const uint64_t *uniq, const unsigned long lo
   return NK_OK;
 }
 
-// The exact k-mer table of this input (opts.exact_counts; nk_exact.h).  One
-// host synchronisation (the key count sizes the sort).
-static int build_exact(nk_counter *c, const KmerInput &in0, hipStream_t s) {
+// the table as the lookup kernels read it (n null: no table)
+static TableView table_view(const nk_counter *c) {
+  TableView t{};
+  if (!c->exact_built) return t;
+  t.uniq = c->x_uniq.p;
+  t.cnt = c->x_cnt.p;
+  t.n = c->x_n.p + 1;
+  if (c->x_grouped) {
+    t.ent = c->x_ent.p;
+    t.fm = make_fastmod(c->pool);
+  }
+  return t;
+}
+
+// The exact k-mer table of this input sorted by key (nk_exact.h "sorted"
+// layout): every key extracted, rocPRIM radix sort + RLE, kmer_per_neuron by
+// partition.  One host synchronisation (the key count sizes the sort).  For
+// 128-bit keys, k > 32, pools past 16.7 M, inputs past one count batch, and
+// the grouped build's fallback.
+static int build_sorted(nk_counter *c, const KmerInput &in0, hipStream_t s) {
   int rc;
   // NK_KMER_128: u128 keys (two u64 words each) over their 2k significant bits
   const int w = c->w128 ? 2 : 1;
   const int end_bit = c->w128 ? (int)(2 * c->k) : (c->k <= 32 ? (int)(2 * c->k) : 64);
   KmerInput in = in0;
   in.n_tiles = n_tiles_for(in.n_bases, kTile);
-  if ((rc = c->x_n.ensure(2)) || (rc = c->x_tile_rec.ensure(std::max<uint64_t>(in.n_tiles, 1))) ||
+  if ((rc = c->x_n.ensure(8)) || (rc = c->x_tile_rec.ensure(std::max<uint64_t>(in.n_tiles, 1))) ||
       (rc = c->x_keys.ensure(w * std::max<uint64_t>(in.n_bases, 1))) || (rc = c->kpn.ensure(c->pool)))
     return rc;
   in.tile_rec = c->x_tile_rec.p;
@@ -741,6 +776,7 @@ static int build_exact(nk_counter *c, const KmerInput &in0, hipStream_t s) {
     HIPCHK(exact_sort_rle(c->x_keys.p, c->x_sorted.p, n, end_bit, c->x_uniq.p, c->x_cnt.p,
                           c->x_n.p + 1, c->x_tmp.p, c->x_tmp.n, s));
   if ((rc = table_kpn(c, c->x_uniq.p, c->x_n.p + 1, n, w, s))) return rc;
+  c->x_grouped = false;
   c->x_lazy = false;
   c->exact_built = true;
   c->kpn_valid = true;
@@ -750,11 +786,157 @@ static int build_exact(nk_counter *c, const KmerInput &in0, hipStream_t s) {
   return NK_OK;
 }
 
+static uint64_t count_chunk();
+static uint32_t env_u32(const char *name, uint32_t dflt);
+
+// The grouped table (nk_table.hip) applies: u64 keys of k <= 32, a pool the
+// partitioned count covers, one count batch, and few enough keys per neuron
+// for a group's distinct keys to fit the LDS table.  NK_EXACT_SORT=1 (tests,
+// A/B) takes the sorted build.
+static bool grouped_ok(const nk_counter *c, uint64_t n_bases) {
+  if (c->w128 || c->k > 32 || !c->pool || !n_bases) return false;
+  const char *e = getenv("NK_EXACT_SORT");
+  if (e && atoi(e)) return false;
+  if (((c->pool + kBinsPerBucket - 1) >> kBinBits) > (uint64_t)kMaxBuckets) return false;
+  if (n_bases > count_chunk()) return false;
+  return xgroup_fits(n_bases, c->pool, xgroup_bits(n_bases, c->pool));
+}
+
+// side list capacity: records that leave the grouped path (overflowed K1a
+// regions, groups with too many distinct keys); past it the sorted build runs
+static uint64_t side_cap_for(uint64_t n_bases) {
+  const uint64_t e = env_u32("NK_XSIDE_CAP", 0);
+  return e ? e : std::max<uint64_t>(n_bases / 8, 1ull << 20);
+}
+
+// the K1a<KEYS> arguments whose records feed the grouped table: the key
+// array (the count's p_key, or the table's own) and the side list
+static int keyed_args(nk_counter *c, uint64_t n_bases, PartArgs &pa, bool own, hipStream_t s) {
+  int rc;
+  const uint64_t sc = side_cap_for(n_bases);
+  DevBuf<uint64_t> &kb = own ? c->xg_key : c->p_key;
+  if ((rc = c->x_n.ensure(8)) || (rc = c->xg_side.ensure(sc)) ||
+      (rc = kb.ensure((uint64_t)pa.n_buckets * pa.cap)))
+    return rc;
+  HIPCHK(hipMemsetAsync(c->x_n.p + 5, 0, 8, s));  // [5] side records
+  pa.key = kb.p;
+  pa.spill = c->xg_side.p;
+  pa.n_spill = c->x_n.p + 5;
+  pa.spill_cap = sc;
+  return NK_OK;
+}
+
+// The grouped table from the keyed records of a K1a<KEYS> pass: the count's
+// own (keyed: its PartArgs) or, without one, a K1a<KEYS> pass of the table's
+// own over the input (no currents touched).  One host synchronisation (the
+// side list's size); the sorted build when the side list overflowed.
+static int build_grouped(nk_counter *c, const KmerInput &in0, const PartArgs *keyed, hipStream_t s) {
+  int rc;
+  const uint64_t P = c->pool, n_bases = in0.n_bases;
+  PartArgs pa{};
+  if (keyed) {
+    pa = *keyed;
+  } else {
+    uint32_t bits = kXMinBinBits;
+    while (bits < kBinBits && ((P + (1ull << bits) - 1) >> bits) > 256) ++bits;
+    const uint64_t B = (P + (1ull << bits) - 1) >> bits;
+    pa.n_buckets = (uint32_t)B;
+    // 1.25x the fair share + the 8-record padding of each (tile, bucket) segment
+    pa.cap = ((n_bases / B * 5 / 4 + kPartTile + 4 * n_tiles_for(n_bases, kPartTile)) + 63) & ~63ull;
+    pa.bin_bits = bits;
+    KmerInput in = in0;
+    in.n_tiles = n_tiles_for(n_bases, kPartTile);
+    if ((rc = c->xg_off.ensure(B * pa.cap)) || (rc = c->xg_fill.ensure(B)) ||
+        (rc = c->xg_over.ensure(B)) || (rc = c->xg_trec.ensure(std::max<uint64_t>(in.n_tiles, 1))))
+      return rc;
+    pa.off = c->xg_off.p;
+    pa.fill = c->xg_fill.p;
+    pa.overflow = c->xg_over.p;
+    pa.currents = nullptr;  // the table only: the currents are the count's
+    if ((rc = keyed_args(c, n_bases, pa, /*own=*/true, s))) return rc;
+    in.tile_rec = c->xg_trec.p;
+    HIPCHK(hipMemsetAsync(c->xg_fill.p, 0, B * 8, s));
+    HIPCHK(hipMemsetAsync(c->xg_over.p, 0, B * 4, s));
+    HIPCHK(launch_tile_rec(in, kPartTile, c->xg_trec.p, s));
+    HIPCHK(launch_part(in, (int)c->k, c->canonical, P, pa, s));
+  }
+  XGroupArgs t{};
+  t.n_buckets = pa.n_buckets;
+  t.cap = pa.cap;
+  t.bin_bits = pa.bin_bits;
+  t.off = pa.off;
+  t.key = pa.key;
+  t.fill = pa.fill;
+  t.overflow = pa.overflow;
+  t.gbits = xgroup_bits(n_bases, P);
+  t.ggbits = xgroup_group_bits(t.gbits, pa.bin_bits);
+  t.n_groups = 1u << (pa.bin_bits - t.ggbits);
+  t.n_slices = (uint32_t)((pa.cap + kXSlice - 1) / kXSlice);
+  const uint64_t B = pa.n_buckets, slots = B * pa.cap;
+  const uint64_t n_tab = std::max<uint64_t>(n_bases, 1) + pa.spill_cap;  // grouped span + side part
+  if ((rc = c->xg_cnt.ensure(B * t.n_slices * t.n_groups)) ||
+      (rc = c->xg_gst.ensure(B * (t.n_groups + 1))) || (rc = c->xg_key2.ensure(slots)) ||
+      (rc = c->xg_bin2.ensure(slots)) || (rc = c->xg_bctr.ensure(2 * B)) ||
+      (rc = c->x_uniq.ensure(n_tab)) || (rc = c->x_cnt.ensure(n_tab)) ||
+      (rc = c->x_ent.ensure(P)) || (rc = c->kpn.ensure(P)))
+    return rc;
+  t.xcnt = c->xg_cnt.p;
+  t.gstart = c->xg_gst.p;
+  t.key2 = c->xg_key2.p;
+  t.bin2 = c->xg_bin2.p;
+  t.side = pa.spill;
+  t.n_side = pa.n_spill;
+  t.side_cap = pa.spill_cap;
+  t.pool = P;
+  t.uniq = c->x_uniq.p;
+  t.cnt = c->x_cnt.p;
+  t.bbase = c->xg_bctr.p;
+  t.bdist = c->xg_bctr.p + B;
+  t.span = c->x_n.p + 4;
+  t.ent = c->x_ent.p;
+  t.kpn = c->kpn.p;
+  t.hash_max = env_u32("NK_XHASH_MAX", 0);
+  HIPCHK(xgroup_build(t, s));
+  unsigned long long cnt[2] = {0, 0};  // grouped span, side records
+  HIPCHK(hipMemcpyAsync(cnt, c->x_n.p + 4, 16, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (cnt[1] > t.side_cap) return build_sorted(c, in0, s);
+  if (cnt[1]) {  // the side part: sorted, run-length encoded after the grouped span
+    const int end_bit = (int)(2 * c->k);
+    if ((rc = c->x_sorted.ensure(cnt[1])) || (rc = c->x_tmp.ensure(exact_temp_bytes(cnt[1], end_bit))))
+      return rc;
+    HIPCHK(exact_sort_rle(t.side, c->x_sorted.p, cnt[1], end_bit, c->x_uniq.p + cnt[0],
+                          c->x_cnt.p + cnt[0], c->x_n.p + 3, c->x_tmp.p, c->x_tmp.n, s));
+    HIPCHK(exact_kpn(c->x_uniq.p + cnt[0], c->x_n.p + 3, cnt[1], P, c->kpn.p, s));
+    HIPCHK(xgroup_finish(t, c->x_n.p + 1, c->x_n.p + 3, s));
+  } else {
+    HIPCHK(xgroup_finish(t, c->x_n.p + 1, nullptr, s));
+  }
+  c->x_grouped = true;
+  c->x_lazy = false;
+  c->exact_built = true;
+  c->kpn_valid = true;
+  c->kpn_global = false;
+  c->d_dirty = true;  // counts.clear() (src/spiking_hash.rs:157,426)
+  c->d_bound = 0;
+  return NK_OK;
+}
+
+// The exact k-mer table of this input (opts.exact_counts; nk_exact.h):
+// grouped by neuron where it applies (keyed: the count's K1a<KEYS> records of
+// this input), else sorted by key.
+static int build_exact(nk_counter *c, const KmerInput &in, hipStream_t s,
+                       const PartArgs *keyed = nullptr) {
+  if (keyed || grouped_ok(c, in.n_bases)) return build_grouped(c, in, keyed, s);
+  return build_sorted(c, in, s);
+}
+
 // A process/accumulate call replaces `counts` and `kmer_per_neuron` with its
 // input's (src/spiking_hash.rs:157-172,426-427,467-473): built now with
 // opts.exact_counts, else marked to be built from that input on demand.
-static int table_for_input(nk_counter *c, const KmerInput &in, hipStream_t s) {
-  if (c->opts.exact_counts) return build_exact(c, in, s);
+static int table_for_input(nk_counter *c, const KmerInput &in, hipStream_t s,
+                           const PartArgs *keyed = nullptr) {
+  if (c->opts.exact_counts) return build_exact(c, in, s, keyed);
   c->exact_built = false;
   c->kpn_valid = false;
   c->kpn_global = false;
@@ -826,8 +1008,10 @@ static uint64_t count_chunk() {
 // Sizes the buffers for a batch of about est_bases bases (slack: extra
 // records per bucket region; max_segs: Part's descriptors per bucket) and
 // lists the arrays to zero before the first batch.
+// part_bits: the narrowest Part buckets to try (the exact table's K1a<KEYS>
+// count takes 4096-neuron buckets, up to 512 of them: nk_table.hip)
 static int plan_count(nk_counter *c, uint64_t est_bases, uint64_t slack, uint64_t max_segs,
-                      CountPlan &cp, ZeroList &z, bool keep_gen = false) {
+                      CountPlan &cp, ZeroList &z, bool keep_gen = false, int part_bits = 0) {
   cp = CountPlan{};
   const uint64_t P = c->pool;
   if (!P) return NK_OK;
@@ -852,7 +1036,7 @@ static int plan_count(nk_counter *c, uint64_t est_bases, uint64_t slack, uint64_
     // bucket counters.  Narrower buckets would need no histogram slices and a
     // shorter uniques scan, but measured slower overall (more K1a segments and
     // reservations, hotter LDS histogram bins): the default keeps 32768 bins
-    pbits = NK_PART_MIN_BITS;
+    pbits = part_bits ? part_bits : NK_PART_MIN_BITS;
     while (pbits < kBinBits && ((P + (1ull << pbits) - 1) >> pbits) > 256) ++pbits;
     B = (P + (1ull << pbits) - 1) >> pbits;
   }
@@ -877,6 +1061,9 @@ static int plan_count(nk_counter *c, uint64_t est_bases, uint64_t slack, uint64_
     cap = est / B * 5 / 4 + 8 * ((cap_c + kPartTile - 1) / kPartTile) + 1024;
   } else {
     cap = est / B * 5 / 4 + slack;
+    // narrow buckets: K1a pads each (tile, bucket) segment to 8 records, ~3.5
+    // records per tile (at 245 buckets about 10 % of the records)
+    if (part_bits) cap += 4 * n_tiles_for(est, kPartTile);
   }
   cap = (cap + 63) & ~63ull;
   // one round of 1-per-CU workgroups (128 KiB LDS each) on 256 CUs
@@ -999,8 +1186,11 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
   // count_chunk() positions the regions hold one batch at a time
   const uint64_t chunk = count_chunk();
   const uint64_t est = std::min<uint64_t>(n_bases, chunk);
+  // the exact table grouped by neuron from this count's own records (K1a also
+  // writes each record's key, nk_table.hip), in 4096-neuron buckets
+  const bool want_keyed = c->opts.exact_counts && grouped_ok(c, n_bases);
   int rc = plan_count(c, est, kPartTile, n_tiles_for(est, kPartTile), cp, z,
-                     /*keep_gen=*/n_bases <= chunk);
+                     /*keep_gen=*/n_bases <= chunk, want_keyed ? kXMinBinBits : 0);
   if (rc) return rc;
   in.n_tiles = n_tiles_for(n_bases, cp.tile);
   const bool batched = cp.path != CountPath::Atomic && n_bases > chunk;
@@ -1107,6 +1297,8 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
     span = c->span.p + 2 * (c->span_calls++ % nk_counter::kCountRing);
     cp.pa.span = span;
   }
+  const bool keyed = c->part_used && want_keyed;
+  if (keyed && (rc = keyed_args(c, n_bases, cp.pa, /*own=*/false, s))) return rc;
   HIPCHK(mark(c, 0, s));
   HIPCHK(launch_prep(in, cp.tile, c->tile_rec.p, z, s, span));
   c->cur_fresh = false;
@@ -1136,7 +1328,7 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
   c->have_input = true;
   c->top_valid = false;
   c->input_owned = d_bases == c->in_bases.p;
-  if ((rc = table_for_input(c, in, s))) return rc;
+  if ((rc = table_for_input(c, in, s, keyed ? &cp.pa : nullptr))) return rc;
   return NK_OK;
 }
 
@@ -2601,7 +2793,7 @@ int nk_process_sequence(nk_counter *c, const uint8_t *seq, size_t len) {
   if ((rc = settle_state(c, s)) || (rc = materialize(c, true, s)) || (rc = fold_pending(c, s)))
     return rc;
   if ((rc = c->in_bases.ensure(len + 16)) || (rc = c->in_offs.ensure(2)) ||
-      (rc = c->x_n.ensure(2)) || (rc = c->kpn.ensure(c->pool)))
+      (rc = c->x_n.ensure(8)) || (rc = c->kpn.ensure(c->pool)))
     return rc;
   const uint64_t offs[2] = {0, (uint64_t)len};
   HIPCHK(hipMemcpyAsync(c->in_bases.p, seq, len, hipMemcpyHostToDevice, s));
@@ -2631,8 +2823,7 @@ int nk_process_sequence(nk_counter *c, const uint8_t *seq, size_t len) {
   HIPCHK(launch_tile_rec(in, kTile, c->x_tile_rec.p, s));
   HIPCHK(exact_keys(in, (int)c->k, c->canonical, c->x_keys.p, c->x_n.p, s));
   HIPCHK(seq_accumulate(c->x_keys.p, c->x_n.p, add, c->pool, (unsigned long long *)c->cur.p,
-                        c->touched.p, delta_args(c), c->exact_built ? c->x_uniq.p : nullptr,
-                        c->exact_built ? c->x_n.p + 1 : nullptr, s));
+                        c->touched.p, delta_args(c), table_view(c), s));
   ZeroList z{};
   z.ptr[0] = c->hist.p;  z.bytes[0] = kHistBins * kHistCopies * 4;
   z.ptr[1] = c->stats.p; z.bytes[1] = 16;
@@ -2672,9 +2863,7 @@ int nk_get_counts(nk_counter *c, const uint64_t *kmers, size_t n, uint32_t *out,
   if ((rc = c->x_q.ensure(n)) || (rc = c->x_out.ensure(n)) || (rc = c->x_pres.ensure(n)))
     return rc;
   HIPCHK(hipMemcpyAsync(c->x_q.p, kmers, n * 8, hipMemcpyHostToDevice, s));
-  HIPCHK(exact_lookup2(c->exact_built ? c->x_uniq.p : nullptr, c->x_cnt.p,
-                       c->exact_built ? c->x_n.p + 1 : nullptr, delta_args(c), c->x_q.p, n,
-                       c->x_out.p, c->x_pres.p, s));
+  HIPCHK(exact_lookup2(table_view(c), delta_args(c), c->x_q.p, n, c->x_out.p, c->x_pres.p, s));
   std::vector<uint32_t> pres(n);
   HIPCHK(hipMemcpyAsync(out, c->x_out.p, n * 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(pres.data(), c->x_pres.p, n * 4, hipMemcpyDeviceToHost, s));
@@ -2723,7 +2912,8 @@ long nk_distinct_kmers(nk_counter *c) {
   if (rc) return rc;
   HIPCHK(hipStreamSynchronize(s));
   unsigned long long n = 0, m[2] = {0, 0};
-  if (c->exact_built) HIPCHK(hipMemcpy(&n, c->x_n.p + 1, 8, hipMemcpyDeviceToHost));
+  // grouped: [6] (the span [1] holds the zero-count tails of the buckets)
+  if (c->exact_built) HIPCHK(hipMemcpy(&n, c->x_n.p + (c->x_grouped ? 6 : 1), 8, hipMemcpyDeviceToHost));
   if (!c->d_dirty) HIPCHK(hipMemcpy(m, c->d_meta.p, 16, hipMemcpyDeviceToHost));
   // meta[1]: keys process_sequence added that the sorted table did not hold
   // (k_seq_accumulate; the ~0 key included)
@@ -2753,7 +2943,8 @@ int nk_exact_partition(nk_counter *c, uint32_t world, uint64_t *send_counts,
   std::vector<unsigned long long> cnt(world, 0);
   if (n) {
     HIPCHK(hipMemsetAsync(c->xp_ctr.p, 0, world * 8, s));
-    HIPCHK(exact_owner_hist(c->x_uniq.p, c->x_n.p + 1, n, world, c->xp_ctr.p, s));
+    HIPCHK(exact_owner_hist(c->x_uniq.p, c->x_n.p + 1, n, world, c->xp_ctr.p, s,
+                            c->x_grouped ? c->x_cnt.p : nullptr));
     HIPCHK(hipMemcpyAsync(cnt.data(), c->xp_ctr.p, world * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     std::vector<unsigned long long> cur(world);
@@ -2764,7 +2955,7 @@ int nk_exact_partition(nk_counter *c, uint32_t world, uint64_t *send_counts,
     }
     HIPCHK(hipMemcpyAsync(c->xp_ctr.p, cur.data(), world * 8, hipMemcpyHostToDevice, s));
     HIPCHK(exact_owner_scatter(c->x_uniq.p, c->x_cnt.p, c->x_n.p + 1, n, world, c->xp_ctr.p,
-                               c->xp_keys.p, c->xp_cnt.p, s));
+                               c->xp_keys.p, c->xp_cnt.p, s, c->x_grouped));
     HIPCHK(hipStreamSynchronize(s));  // cur[] is host memory the copy reads
   }
   for (uint32_t r = 0; r < world; ++r) send_counts[r] = cnt[r];
@@ -2783,7 +2974,7 @@ int nk_exact_adopt(nk_counter *c, const uint64_t *d_keys, const uint32_t *d_coun
   hipStream_t s = pick_stream(c, stream);
   const int end_bit = c->k <= 32 ? (int)(2 * c->k) : 64;
   const uint64_t nn = std::max<uint64_t>(n, 1);
-  if ((rc = c->x_n.ensure(2)) || (rc = c->x_sorted.ensure(nn)) || (rc = c->x_cs.ensure(nn)) ||
+  if ((rc = c->x_n.ensure(8)) || (rc = c->x_sorted.ensure(nn)) || (rc = c->x_cs.ensure(nn)) ||
       (rc = c->x_uniq.ensure(nn)) || (rc = c->x_cnt.ensure(nn)) || (rc = c->kpn.ensure(c->pool)) ||
       (rc = c->x_tmp.ensure(exact_merge_temp_bytes(nn, end_bit))))
     return rc;
@@ -2791,6 +2982,7 @@ int nk_exact_adopt(nk_counter *c, const uint64_t *d_keys, const uint32_t *d_coun
                            c->x_cnt.p, c->x_n.p + 1, c->x_tmp.p, c->x_tmp.n, s));
   if ((rc = table_kpn(c, c->x_uniq.p, c->x_n.p + 1, n, 1, s))) return rc;
   HIPCHK(hipStreamSynchronize(s));  // the caller may free the received buffers
+  c->x_grouped = false;
   c->exact_built = true;
   c->kpn_valid = true;
   c->kpn_global = true;

@@ -217,22 +217,13 @@ __global__ void k_kpn(const uint64_t *__restrict__ uniq, const unsigned long lon
     atomicAdd(&kpn[fastmod(sip13_u64(uniq[i]), fm)], 1u);
 }
 
-__global__ void k_lookup(const uint64_t *__restrict__ uniq, const uint32_t *__restrict__ cnt,
-                         const unsigned long long *__restrict__ n_uniq,
-                         const uint64_t *__restrict__ q, uint64_t nq, uint32_t *__restrict__ out,
-                         uint32_t *__restrict__ present) {
-  const uint64_t n = *n_uniq;
+__global__ void k_lookup(TableView t, const uint64_t *__restrict__ q, uint64_t nq,
+                         uint32_t *__restrict__ out, uint32_t *__restrict__ present) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nq;
        i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t key = q[i];
-    uint64_t lo = 0, hi = n;  // first index with uniq >= key
-    while (lo < hi) {
-      const uint64_t mid = (lo + hi) >> 1;
-      if (uniq[mid] < key) lo = mid + 1;
-      else hi = mid;
-    }
-    const bool hit = lo < n && uniq[lo] == key;
-    out[i] = hit ? cnt[lo] : 0u;
+    uint64_t at;
+    const bool hit = table_find(t, q[i], &at);
+    out[i] = hit ? t.cnt[at] : 0u;
     present[i] = hit ? 1u : 0u;
   }
 }
@@ -249,18 +240,6 @@ __device__ __forceinline__ uint64_t dmix(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
   z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
   return z ^ (z >> 31);
-}
-
-__device__ __forceinline__ bool in_sorted(const uint64_t *uniq, uint64_t n, uint64_t key,
-                                          uint64_t *at) {
-  uint64_t lo = 0, hi = n;
-  while (lo < hi) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if (uniq[mid] < key) lo = mid + 1;
-    else hi = mid;
-  }
-  *at = lo;
-  return lo < n && uniq[lo] == key;
 }
 
 // counts[key] += v in the delta; returns true if the key was new to the delta
@@ -320,10 +299,8 @@ __global__ void k_delta_rehash(DeltaArgs from, DeltaArgs to) {
 __global__ void k_seq_accumulate(const uint64_t *__restrict__ keys,
                                  const unsigned long long *__restrict__ n_keys, FastMod fm,
                                  unsigned long long *__restrict__ currents,
-                                 uint8_t *__restrict__ touched, DeltaArgs d,
-                                 const uint64_t *__restrict__ uniq,
-                                 const unsigned long long *__restrict__ n_uniq) {
-  const uint64_t n = *n_keys, nu = n_uniq ? *n_uniq : 0;
+                                 uint8_t *__restrict__ touched, DeltaArgs d, TableView t) {
+  const uint64_t n = *n_keys;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t key = keys[i];
@@ -331,7 +308,7 @@ __global__ void k_seq_accumulate(const uint64_t *__restrict__ keys,
     atomicAdd(&currents[idx], 1ULL);  // :217-223,236-241,251-254
     touched[idx] = 1;                 // local_unique[idx] = true
     uint64_t at;
-    if (delta_add(d, key, 1) && !in_sorted(uniq, nu, key, &at))
+    if (delta_add(d, key, 1) && !table_find(t, key, &at))
       atomicAdd(&d.meta[1], 1ull);    // a key new to `counts`
   }
 }
@@ -396,19 +373,16 @@ __global__ __launch_bounds__(256) void k_seq_lif(uint64_t pool, unsigned long lo
     if (sh[i]) atomicAdd(&hc[i], sh[i]);
 }
 
-__global__ void k_lookup2(const uint64_t *__restrict__ uniq, const uint32_t *__restrict__ cnt,
-                          const unsigned long long *__restrict__ n_uniq, DeltaArgs d,
-                          const uint64_t *__restrict__ q, uint64_t nq, uint32_t *__restrict__ out,
-                          uint32_t *__restrict__ present) {
-  const uint64_t n = n_uniq ? *n_uniq : 0;
+__global__ void k_lookup2(TableView t, DeltaArgs d, const uint64_t *__restrict__ q, uint64_t nq,
+                          uint32_t *__restrict__ out, uint32_t *__restrict__ present) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nq;
        i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t key = q[i];
     uint64_t at;
-    const bool hm = in_sorted(uniq, n, key, &at);
+    const bool hm = table_find(t, key, &at);
     uint32_t dv = 0;
     const bool hd = d.keys && delta_get(d, key, &dv);
-    out[i] = (hm ? cnt[at] : 0u) + (hd ? dv : 0u);  // u32 wrap like AtomicU32
+    out[i] = (hm ? t.cnt[at] : 0u) + (hd ? dv : 0u);  // u32 wrap like AtomicU32
     present[i] = (hm || hd) ? 1u : 0u;
   }
 }
@@ -484,7 +458,8 @@ constexpr int kOwnerPer = 16;  // entries per thread (4096 per 256-thread block)
 __global__ __launch_bounds__(256) void k_owner_hist(const uint64_t *__restrict__ uniq,
                                                     const unsigned long long *__restrict__ n_uniq,
                                                     uint32_t world,
-                                                    unsigned long long *__restrict__ cnt) {
+                                                    unsigned long long *__restrict__ cnt,
+                                                    const uint32_t *__restrict__ tcnt) {
   __shared__ uint32_t h[kOwnerMax];
   for (uint32_t r = threadIdx.x; r < world; r += 256) h[r] = 0;
   __syncthreads();
@@ -492,7 +467,7 @@ __global__ __launch_bounds__(256) void k_owner_hist(const uint64_t *__restrict__
   const uint64_t base = (uint64_t)blockIdx.x * 256 * kOwnerPer;
   for (int j = 0; j < kOwnerPer; ++j) {
     const uint64_t i = base + (uint64_t)j * 256 + threadIdx.x;
-    if (i < n) atomicAdd(&h[exact_owner(uniq[i], world)], 1u);
+    if (i < n && (!tcnt || tcnt[i])) atomicAdd(&h[exact_owner(uniq[i], world)], 1u);
   }
   __syncthreads();
   for (uint32_t r = threadIdx.x; r < world; r += 256)
@@ -507,7 +482,8 @@ __global__ __launch_bounds__(256) void k_owner_scatter(const uint64_t *__restric
                                                        uint32_t world,
                                                        unsigned long long *__restrict__ cursor,
                                                        uint64_t *__restrict__ out_keys,
-                                                       uint32_t *__restrict__ out_cnt) {
+                                                       uint32_t *__restrict__ out_cnt,
+                                                       int skip_zero) {
   __shared__ uint32_t h[kOwnerMax];
   __shared__ unsigned long long b0[kOwnerMax];
   for (uint32_t r = threadIdx.x; r < world; r += 256) h[r] = 0;
@@ -517,8 +493,9 @@ __global__ __launch_bounds__(256) void k_owner_scatter(const uint64_t *__restric
   uint32_t own[kOwnerPer], rk[kOwnerPer];
   for (int j = 0; j < kOwnerPer; ++j) {
     const uint64_t i = base + (uint64_t)j * 256 + threadIdx.x;
-    own[j] = i < n ? exact_owner(uniq[i], world) : world;
-    rk[j] = i < n ? atomicAdd(&h[own[j]], 1u) : 0u;
+    const bool live = i < n && (!skip_zero || cnt[i]);
+    own[j] = live ? exact_owner(uniq[i], world) : world;
+    rk[j] = live ? atomicAdd(&h[own[j]], 1u) : 0u;
   }
   __syncthreads();
   for (uint32_t r = threadIdx.x; r < world; r += 256)
@@ -526,7 +503,7 @@ __global__ __launch_bounds__(256) void k_owner_scatter(const uint64_t *__restric
   __syncthreads();
   for (int j = 0; j < kOwnerPer; ++j) {
     const uint64_t i = base + (uint64_t)j * 256 + threadIdx.x;
-    if (i >= n) continue;
+    if (own[j] == world) continue;
     const uint64_t at = b0[own[j]] + rk[j];
     out_keys[at] = uniq[i];
     out_cnt[at] = cnt[i];
@@ -534,22 +511,23 @@ __global__ __launch_bounds__(256) void k_owner_scatter(const uint64_t *__restric
 }
 
 hipError_t exact_owner_hist(const uint64_t *uniq, const unsigned long long *n_uniq, size_t max_n,
-                            uint32_t world, unsigned long long *cnt, hipStream_t s) {
+                            uint32_t world, unsigned long long *cnt, hipStream_t s,
+                            const uint32_t *tcnt) {
   if (!max_n) return hipSuccess;
   if (!world || world > (uint32_t)kOwnerMax) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_owner_hist, dim3(grid_for(max_n, 256 * kOwnerPer)), dim3(256), 0, s, uniq,
-                     n_uniq, world, cnt);
+                     n_uniq, world, cnt, tcnt);
   return hipGetLastError();
 }
 
 hipError_t exact_owner_scatter(const uint64_t *uniq, const uint32_t *cnt,
                                const unsigned long long *n_uniq, size_t max_n, uint32_t world,
                                unsigned long long *cursor, uint64_t *out_keys, uint32_t *out_cnt,
-                               hipStream_t s) {
+                               hipStream_t s, bool skip_zero) {
   if (!max_n) return hipSuccess;
   if (!world || world > (uint32_t)kOwnerMax) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_owner_scatter, dim3(grid_for(max_n, 256 * kOwnerPer)), dim3(256), 0, s,
-                     uniq, cnt, n_uniq, world, cursor, out_keys, out_cnt);
+                     uniq, cnt, n_uniq, world, cursor, out_keys, out_cnt, skip_zero ? 1 : 0);
   return hipGetLastError();
 }
 
@@ -589,12 +567,11 @@ hipError_t exact_kpn(const uint64_t *uniq, const unsigned long long *n_uniq, siz
   return hipGetLastError();
 }
 
-hipError_t exact_lookup(const uint64_t *uniq, const uint32_t *cnt,
-                        const unsigned long long *n_uniq, const uint64_t *q, size_t nq,
-                        uint32_t *out, uint32_t *present, hipStream_t s) {
+hipError_t exact_lookup(const TableView &t, const uint64_t *q, size_t nq, uint32_t *out,
+                        uint32_t *present, hipStream_t s) {
   if (!nq) return hipSuccess;
-  hipLaunchKernelGGL(k_lookup, dim3(grid_for(nq, 4096)), dim3(256), 0, s, uniq, cnt, n_uniq, q,
-                     (uint64_t)nq, out, present);
+  hipLaunchKernelGGL(k_lookup, dim3(grid_for(nq, 4096)), dim3(256), 0, s, t, q, (uint64_t)nq, out,
+                     present);
   return hipGetLastError();
 }
 
@@ -611,14 +588,13 @@ hipError_t delta_rehash(const DeltaArgs &from, const DeltaArgs &to, hipStream_t 
 
 hipError_t seq_accumulate(const uint64_t *keys, const unsigned long long *n_keys, size_t max_n,
                           uint64_t pool, unsigned long long *currents, uint8_t *touched,
-                          const DeltaArgs &d, const uint64_t *uniq,
-                          const unsigned long long *n_uniq, hipStream_t s) {
+                          const DeltaArgs &d, const TableView &t, hipStream_t s) {
   if (!max_n || !pool) return hipSuccess;
   FastMod fm;
   fm.p = pool;
   fm.magic = (~0ULL) / pool;
   hipLaunchKernelGGL(k_seq_accumulate, dim3(grid_for(max_n, 4096)), dim3(256), 0, s, keys, n_keys,
-                     fm, currents, touched, d, uniq, n_uniq);
+                     fm, currents, touched, d, t);
   return hipGetLastError();
 }
 
@@ -632,12 +608,11 @@ hipError_t seq_lif(uint64_t pool, unsigned long long *currents, uint8_t *touched
   return hipGetLastError();
 }
 
-hipError_t exact_lookup2(const uint64_t *uniq, const uint32_t *cnt,
-                         const unsigned long long *n_uniq, const DeltaArgs &d, const uint64_t *q,
-                         size_t nq, uint32_t *out, uint32_t *present, hipStream_t s) {
+hipError_t exact_lookup2(const TableView &t, const DeltaArgs &d, const uint64_t *q, size_t nq,
+                         uint32_t *out, uint32_t *present, hipStream_t s) {
   if (!nq) return hipSuccess;
-  hipLaunchKernelGGL(k_lookup2, dim3(grid_for(nq, 4096)), dim3(256), 0, s, uniq, cnt, n_uniq, d, q,
-                     (uint64_t)nq, out, present);
+  hipLaunchKernelGGL(k_lookup2, dim3(grid_for(nq, 4096)), dim3(256), 0, s, t, d, q, (uint64_t)nq,
+                     out, present);
   return hipGetLastError();
 }
 

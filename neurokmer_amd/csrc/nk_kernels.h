@@ -146,6 +146,13 @@ struct PartArgs {
   // launch (s_memrealtime, 100 MHz), folded with atomicMin / atomicMax by one
   // lane per workgroup: the kernel's duration without an event in the stream
   unsigned long long *span = nullptr;
+  // exact table (nk_table.hip): non-null = K1a also writes each record's key
+  // ([bucket][cap], beside off; pos is then not written) and appends the keys
+  // of records past a full region to spill[*n_spill++] (< spill_cap)
+  uint64_t *key = nullptr;
+  uint64_t *spill = nullptr;
+  unsigned long long *n_spill = nullptr;
+  uint64_t spill_cap = 0;
   // K1b write-through (one slice per bucket, one batch): every bin of the
   // bucket is written to out (no zeroed or read-modified currents); the
   // overflow target `currents` is then a separate array kept zero -- a bucket

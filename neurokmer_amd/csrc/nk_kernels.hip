@@ -534,8 +534,12 @@ __device__ __forceinline__ uint32_t in_vgpr(uint32_t x) {
 
 constexpr uint32_t kSpanTail = 2048;  // last-dispatched workgroups that stamp the span's end
 
-// K16: k >= 16, so the low word of the window mask is all ones
-template <bool CANON, int MAXB, bool K16 = false>
+// K16: k >= 16, so the low word of the window mask is all ones.
+// KEYS (the exact table, nk_table.hip): each record's key is re-extracted from
+// the staged tile at store time and written beside its bin offset (pa.key);
+// the position array is not written.  Records past a full region are counted
+// directly as always (pa.currents, when set) and their keys spilled.
+template <bool CANON, int MAXB, bool K16 = false, bool KEYS = false>
 __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMod fm, PartArgs pa) {
   using S = PartShape<MAXB>;
   constexpr int kSortSlots = S::kSortSlots;
@@ -701,7 +705,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
       fit = eb >= pa.cap ? 0u : (uint32_t)(pa.cap - eb < c ? pa.cap - eb : c);
       // past the region, or past the descriptor table (chunked input: a tile can
       // add a segment per launch): the uniques of this bucket fall back to a rescan
-      if (fit < c || seg >= pa.max_segs) pa.overflow[b] = 1u;
+      if (fit < c || (seg >= pa.max_segs && (!KEYS || pa.desc))) pa.overflow[b] = 1u;
       base = (uint32_t)eb;
     }
     s_base[b] = base;
@@ -757,12 +761,36 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
       // 0.4177-0.4179 vs 0.4205-0.4217 ms with plain stores)
       typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
       __builtin_nontemporal_store(u32x4{off.x, off.y, off.z, off.w}, reinterpret_cast<u32x4 *>(pa.off + dst));
-      __builtin_nontemporal_store(u32x4{pos.x, pos.y, pos.z, pos.w}, reinterpret_cast<u32x4 *>(pa.pos + dst));
+      if constexpr (KEYS) {
+        if (pa.pos)  // the count's arena: positions kept for a multi-GPU uniques pass
+          __builtin_nontemporal_store(u32x4{pos.x, pos.y, pos.z, pos.w}, reinterpret_cast<u32x4 *>(pa.pos + dst));
+        const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        uint64_t kk[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          kk[i] = (w[i] & 0xFFFFu) != kPadOff ? window_key<kPartTile, !CANON, CANON>(L, (int)(w[i] >> 16), k)
+                                               : 0ull;
+        // plain stores: a lane's 64 B are four 16-B stores 64 B apart across
+        // the wave, completed in L2 (nontemporal ones left partial lines:
+        // K1a<KEYS> 1.2 ms vs 0.40, profiles/r03_t2)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          reinterpret_cast<ulonglong2 *>(pa.key + dst)[i] = make_ulonglong2(kk[2 * i], kk[2 * i + 1]);
+      } else {
+        __builtin_nontemporal_store(u32x4{pos.x, pos.y, pos.z, pos.w}, reinterpret_cast<u32x4 *>(pa.pos + dst));
+      }
     } else {  // bucket region full: count directly (correct, slow, rare)
       const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-      for (int i = 0; i < 8; ++i)
-        if ((w[i] & 0xFFFFu) != kPadOff)
+      for (int i = 0; i < 8; ++i) {
+        if ((w[i] & 0xFFFFu) == kPadOff) continue;
+        if (!KEYS || pa.currents)
           atomicAdd(&pa.currents[((uint64_t)b << pa.bin_bits) | (w[i] & 0xFFFFu)], 1ULL);
+        if constexpr (KEYS) {  // the table takes this bucket from the side list
+          const unsigned long long at = atomicAdd(pa.n_spill, 1ull);
+          if (at < pa.spill_cap)
+            pa.spill[at] = window_key<kPartTile, !CANON, CANON>(L, (int)(w[i] >> 16), k);
+        }
+      }
     }
   }
   if (pa.span && blockIdx.x + kSpanTail >= gridDim.x) {  // its last stores are issued: end time
@@ -2434,6 +2462,18 @@ hipError_t launch_part(const KmerInput &in, int k, int canonical, uint64_t pool,
   const dim3 g((unsigned)in.n_tiles), bl(kPartBlock);
   const size_t dyn = 0;
   if (pa.n_buckets > (uint32_t)kMaxBuckets) return hipErrorInvalidValue;
+  if (pa.key) {  // the exact table's records (key beside the bin offset)
+    if (!pa.spill || !pa.n_spill) return hipErrorInvalidValue;
+    if (pa.n_buckets <= 256) {
+      if (canonical && k >= 16) hipLaunchKernelGGL((k_part<true, 256, true, true>), g, bl, dyn, s, in, k, fm, pa);
+      else if (canonical) hipLaunchKernelGGL((k_part<true, 256, false, true>), g, bl, dyn, s, in, k, fm, pa);
+      else hipLaunchKernelGGL((k_part<false, 256, false, true>), g, bl, dyn, s, in, k, fm, pa);
+    } else {
+      if (canonical) hipLaunchKernelGGL((k_part<true, kMaxBuckets, false, true>), g, bl, dyn, s, in, k, fm, pa);
+      else hipLaunchKernelGGL((k_part<false, kMaxBuckets, false, true>), g, bl, dyn, s, in, k, fm, pa);
+    }
+    return hipGetLastError();
+  }
   if (pa.n_buckets <= 256) {
 #if !defined(NK_K1A_NO_K16)  // (A/B: the masked low word)
     if (canonical && k >= 16) hipLaunchKernelGGL((k_part<true, 256, true>), g, bl, dyn, s, in, k, fm, pa);
@@ -2459,6 +2499,7 @@ hipError_t launch_bucket_hist(const PartArgs &pa, uint64_t pool, uint32_t slices
     return hipGetLastError();
   }
   switch (pa.bin_bits) {
+    case 12: hipLaunchKernelGGL(k_bucket_hist<12>, g, dim3(kHistBlock), 0, s, pa, pool, slices, partials); break;
     case 13: hipLaunchKernelGGL(k_bucket_hist<13>, g, dim3(kHistBlock), 0, s, pa, pool, slices, partials); break;
     case 14: hipLaunchKernelGGL(k_bucket_hist<14>, g, dim3(kHistBlock), 0, s, pa, pool, slices, partials); break;
     case 15: hipLaunchKernelGGL(k_bucket_hist<15>, g, dim3(kHistBlock), 0, s, pa, pool, slices, partials); break;

@@ -9,7 +9,7 @@ import zlib
 import numpy as np
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.abspath(__file__)), ".."))
 from neurokmer_amd import SpikingKmerCounter as Counter, synth  # noqa: E402
 
 tag = sys.argv[1] if len(sys.argv) > 1 else "A"
