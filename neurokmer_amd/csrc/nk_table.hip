@@ -44,6 +44,7 @@ constexpr int kGroupN = 1 << kXGroupBits;          // largest group
 constexpr int kHashBits = 12;
 constexpr int kHashSlots = 1 << kHashBits;          // LDS table of k_xgroup
 constexpr uint32_t kHashMax = kHashSlots * 5 / 8;   // distinct keys a pass may hold
+constexpr int kSlotsPer = kHashSlots / kXsBlock;    // 16
 constexpr uint16_t kPadBin = 0xFFFFu;
 constexpr unsigned long long kHashEmpty = ~0ull;
 
@@ -80,8 +81,7 @@ __global__ __launch_bounds__(kXsBlock) void k_xcount(XGroupArgs t) {
   if (threadIdx.x < NG) t.xcnt[((uint64_t)b * t.n_slices + sl) * NG + threadIdx.x] = h[threadIdx.x];
 }
 
-// exclusive scan of one value per thread over a block of WAVES wave64s
-template <int WAVES = kXsBlock / 64>
+// exclusive scan of one value per thread over a 256-thread block
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_w, uint32_t *total) {
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t x = v;
@@ -91,13 +91,9 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_w, u
   }
   if (lane == 63) s_w[wv] = x;
   __syncthreads();
-  uint32_t pre = 0, tot = 0;
-#pragma unroll
-  for (int i = 0; i < WAVES; ++i) {
-    pre += (uint32_t)i < wv ? s_w[i] : 0u;
-    tot += s_w[i];
-  }
-  *total = tot;
+  uint32_t pre = 0;
+  for (uint32_t i = 0; i < wv; ++i) pre += s_w[i];
+  *total = s_w[0] + s_w[1] + s_w[2] + s_w[3];
   __syncthreads();
   return pre + x - v;
 }
@@ -298,29 +294,27 @@ constexpr int kMaxProbe = 128;  // a longer probe sends the pass to the side lis
 
 // a batch of the group's records: kp / bp = the group's first record (launch-
 // uniform per workgroup), i0 + u * 256 + tid < n the records of this batch
-template <int BLOCK, int XGB>
 __device__ __forceinline__ void xg_load(const uint64_t *kp, const uint8_t *bp, uint32_t i0, uint32_t n,
-                                        uint32_t p0, uint32_t pn, uint32_t (&bn)[XGB],
-                                        uint64_t (&ky)[XGB]) {
+                                        uint32_t (&bn)[kXgBatch],
+                                        uint64_t (&ky)[kXgBatch]) {
 #pragma unroll
-  for (int u = 0; u < XGB; ++u) {
-    const uint32_t i = i0 + (uint32_t)u * BLOCK + threadIdx.x;
+  for (int u = 0; u < kXgBatch; ++u) {
+    const uint32_t i = i0 + (uint32_t)u * kXsBlock + threadIdx.x;
     bn[u] = i < n ? (uint32_t)bp[i] : 0xFFu;
   }
 #pragma unroll
-  for (int u = 0; u < XGB; ++u) {
-    const uint32_t i = i0 + (uint32_t)u * BLOCK + threadIdx.x;
-    ky[u] = (bn[u] - p0 < pn) ? kp[i] : 0ull;  // only this pass's records
+  for (int u = 0; u < kXgBatch; ++u) {
+    const uint32_t i = i0 + (uint32_t)u * kXsBlock + threadIdx.x;
+    // not predicated on the bin just loaded (that made the key loads a second
+    // dependent round trip); another pass's records are filtered at insert
+    ky[u] = i < n ? kp[i] : 0ull;
   }
 }
 
-template <int BLOCK, bool DIRECT>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BLOCK == 512 ? 6 : 3))) void k_xgroup(XGroupArgs t) {
-  constexpr int XGB = kXgBatch * 256 / BLOCK;  // records per thread in flight
-  constexpr int kSlotsPer = kHashSlots / BLOCK;
+__global__ __launch_bounds__(kXsBlock) void k_xgroup(XGroupArgs t) {
   __shared__ unsigned long long hk[kHashSlots];
   __shared__ uint32_t hc[kHashSlots];
-  __shared__ uint32_t bc[kGroupN], bcur[kGroupN], spc[kGroupN], s_w[BLOCK / 64];
+  __shared__ uint32_t bc[kGroupN], bcur[kGroupN], spc[kGroupN], s_w[4];
   __shared__ uint32_t s_fail;
   const uint32_t g = blockIdx.x, b = blockIdx.y, NG = t.n_groups, tid = threadIdx.x;
   const uint64_t n0 = ((uint64_t)b << t.bin_bits) + ((uint64_t)g << t.ggbits);
@@ -344,9 +338,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BLOCK == 
   for (uint32_t p0 = 0; p0 < nG; p0 += W) {
     const uint32_t pn = nG - p0 < W ? nG - p0 : W;  // neurons of this pass
 #pragma unroll
-    for (int i = 0; i < kSlotsPer; ++i) hk[tid + i * BLOCK] = kHashEmpty;
+    for (int i = 0; i < kSlotsPer; ++i) hk[tid + i * kXsBlock] = kHashEmpty;
 #pragma unroll
-    for (int i = 0; i < kSlotsPer; ++i) hc[tid + i * BLOCK] = 0;
+    for (int i = 0; i < kSlotsPer; ++i) hc[tid + i * kXsBlock] = 0;
     if (tid < kGroupN) bc[tid] = spc[tid] = 0;
     if (tid == 0) s_fail = 0;
     __syncthreads();
@@ -358,17 +352,17 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BLOCK == 
     const uint64_t *kp = t.key2 + gs;
     const uint8_t *bp = t.bin2 + gs;
     const uint32_t nrec = (uint32_t)(ge - gs);
-    for (uint32_t i0 = 0; i0 < nrec && !big; i0 += BLOCK * XGB) {
-      uint32_t cb[XGB];
-      uint64_t ck[XGB];
-      xg_load<BLOCK, XGB>(kp, bp, i0, nrec, p0, pn, cb, ck);
+    for (uint32_t i0 = 0; i0 < nrec && !big; i0 += kXsBlock * kXgBatch) {
+      uint32_t cb[kXgBatch];
+      uint64_t ck[kXgBatch];
+      xg_load(kp, bp, i0, nrec, cb, ck);
       if (*(volatile uint32_t *)&s_fail) break;
 #pragma unroll
-      for (int u0 = 0; u0 < XGB; u0 += XGB) {
-        uint32_t hh[XGB];
-        unsigned long long pv[XGB];
+      for (int u0 = 0; u0 < kXgBatch; u0 += 8) {
+        uint32_t hh[8];
+        unsigned long long pv[8];
 #pragma unroll
-        for (int u = 0; u < XGB; ++u) {
+        for (int u = 0; u < 8; ++u) {
           const uint64_t key = ck[u0 + u];
           hh[u] = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - kHashBits));
           pv[u] = (cb[u0 + u] - p0 < pn && key != kHashEmpty)
@@ -376,7 +370,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BLOCK == 
                       : 0ull;
         }
 #pragma unroll
-        for (int u = 0; u < XGB; ++u) {
+        for (int u = 0; u < 8; ++u) {
           const uint32_t bin = cb[u0 + u];
           if (bin - p0 >= pn) continue;  // another pass's neuron (or past the group)
           const uint64_t key = ck[u0 + u];
@@ -406,25 +400,24 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BLOCK == 
     if (!s_fail) {
 #pragma unroll
       for (int i = 0; i < kSlotsPer; ++i) {
-        const int sidx = tid + i * BLOCK;
+        const int sidx = tid + i * kXsBlock;
         rk[i] = hk[sidx];
         rc[i] = hc[sidx];
         if (rk[i] != kHashEmpty) atomicAdd(&bc[rc[i] >> kCntBits], 1u);
       }
     }
-    if constexpr (DIRECT) __builtin_amdgcn_sched_barrier(0);  // (re-read below: nothing held)
     __syncthreads();
     const uint32_t nb = p0 + tid;  // one neuron per thread (tid < pn)
     const uint32_t len = tid < pn ? bc[nb] + (spc[nb] ? 1u : 0u) : 0u;
     uint32_t D;
-    const uint32_t pre = block_excl_scan<BLOCK / 64>(len, s_w, &D);
+    const uint32_t pre = block_excl_scan(len, s_w, &D);
     if (big || s_fail || D > hmax) {  // too many distinct keys for the LDS table: this pass to the side list
       if (tid < pn) {
         t.ent[n0 + p0 + tid] = kSideEnt;
         t.kpn[n0 + p0 + tid] = 0;
       }
       const uint32_t lane = tid & 63;
-      for (uint64_t r0 = gs; r0 < ge; r0 += BLOCK) {
+      for (uint64_t r0 = gs; r0 < ge; r0 += kXsBlock) {
         const uint64_t r = r0 + tid;
         const bool take = r < ge && t.bin2[r] - p0 < pn;
         const uint64_t m = __ballot(take);
@@ -444,28 +437,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BLOCK == 
       t.kpn[n0 + nb] = len;  // kmer_per_neuron (src/spiking_hash.rs:167-172)
     }
     __syncthreads();
-    if constexpr (DIRECT) {
-      // entries straight to the table in neuron order (per-neuron cursors;
-      // the ~0 key last in its neuron): the group's range is written whole,
-      // so L2 merges the scattered 8-B / 4-B stores into full lines
-#pragma unroll
-      for (int i = 0; i < kSlotsPer; ++i) {
-        const unsigned long long k2 = hk[tid + i * BLOCK];  // the table is unchanged since the read-back
-        const uint32_t c2 = hc[tid + i * BLOCK];
-        if (k2 != kHashEmpty) {
-          const uint32_t q = atomicAdd(&bcur[c2 >> kCntBits], 1u);
-          t.uniq[at + q] = k2;
-          t.cnt[at + q] = c2 & kCntMask;
-        }
-      }
-      __syncthreads();
-      if (tid < pn && spc[nb]) {
-        t.uniq[at + bcur[nb]] = kHashEmpty;
-        t.cnt[at + bcur[nb]] = spc[nb];
-      }
-      __syncthreads();
-      continue;
-    }
     // entries -> LDS in neuron order (the ~0 key, the largest, last in its neuron)
 #pragma unroll
     for (int i = 0; i < kSlotsPer; ++i)
@@ -480,14 +451,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BLOCK == 
       hc[bcur[nb]] = spc[nb];
     }
     __syncthreads();
-    for (uint32_t i = tid; i < D; i += BLOCK) {
+    for (uint32_t i = tid; i < D; i += kXsBlock) {
       t.uniq[at + i] = hk[i];
       t.cnt[at + i] = hc[i];
     }
     __syncthreads();
   }
   // the rest of the group's range: (0, count 0); its distinct keys to the bucket
-  for (unsigned long long i = tbase + used + tid; i < tbase + (ge - gs); i += BLOCK) {
+  for (unsigned long long i = tbase + used + tid; i < tbase + (ge - gs); i += kXsBlock) {
     t.uniq[i] = 0;
     t.cnt[i] = 0;
   }
@@ -545,27 +516,13 @@ hipError_t xgroup_build(const XGroupArgs &t, hipStream_t s) {
   hipLaunchKernelGGL(k_xcount, gs, dim3(kXsBlock), 0, s, t);
   hipLaunchKernelGGL(k_xscan, dim3(t.n_buckets), dim3(kXsBlock), 0, s, t);
   hipLaunchKernelGGL(k_xbase, dim3(1), dim3(512), 0, s, t);
-  static const int xcd = [] {
-    const char *e = getenv("NK_XS_XCD");
-    return e ? atoi(e) : 1;
-  }();
+  static const int xcd = env_int("NK_XS_XCD", 1);
   if (xcd)
     hipLaunchKernelGGL(k_xscatter, dim3(8u * ((t.n_buckets + 7u) / 8u) * t.n_slices), dim3(kXsBlock), 0, s,
                        t, 1);
   else
     hipLaunchKernelGGL(k_xscatter, gs, dim3(kXsBlock), 0, s, t, 0);
-  // A/B knobs: NK_XG_BLOCK=512 (twice the waves per LDS table), NK_XG_DIRECT=1
-  // (entries stored from the read-back, no LDS reordering)
-  static const int xg_block = env_int("NK_XG_BLOCK", 256), xg_direct = env_int("NK_XG_DIRECT", 0);
-  const dim3 gg(t.n_groups, t.n_buckets);
-  if (xg_block == 512 && xg_direct)
-    hipLaunchKernelGGL((k_xgroup<512, true>), gg, dim3(512), 0, s, t);
-  else if (xg_block == 512)
-    hipLaunchKernelGGL((k_xgroup<512, false>), gg, dim3(512), 0, s, t);
-  else if (xg_direct)
-    hipLaunchKernelGGL((k_xgroup<256, true>), gg, dim3(256), 0, s, t);
-  else
-    hipLaunchKernelGGL((k_xgroup<256, false>), gg, dim3(256), 0, s, t);
+  hipLaunchKernelGGL(k_xgroup, dim3(t.n_groups, t.n_buckets), dim3(kXsBlock), 0, s, t);
   return hipGetLastError();
 }
 
