@@ -789,6 +789,16 @@ static int build_sorted(nk_counter *c, const KmerInput &in0, hipStream_t s) {
 static uint64_t count_chunk();
 static uint32_t env_u32(const char *name, uint32_t dflt);
 
+// neurons per K1a<KEYS> bucket (log2): kXMinBinBits; NK_XBIN_BITS (A/B,
+// 13..15) trades K1a's bucket count against passes per group in k_xgroup
+static uint32_t xbin_bits() {
+  static const uint32_t b = [] {
+    const uint32_t v = env_u32("NK_XBIN_BITS", kXMinBinBits);
+    return v < (uint32_t)kXMinBinBits ? (uint32_t)kXMinBinBits : v > (uint32_t)kBinBits ? (uint32_t)kBinBits : v;
+  }();
+  return b;
+}
+
 // The grouped table (nk_table.hip) applies: u64 keys of k <= 32, a pool the
 // partitioned count covers, one count batch, and few enough keys per neuron
 // for a group's distinct keys to fit the LDS table.  NK_EXACT_SORT=1 (tests,
@@ -837,7 +847,7 @@ static int build_grouped(nk_counter *c, const KmerInput &in0, const PartArgs *ke
   if (keyed) {
     pa = *keyed;
   } else {
-    uint32_t bits = kXMinBinBits;
+    uint32_t bits = xbin_bits();
     while (bits < kBinBits && ((P + (1ull << bits) - 1) >> bits) > 256) ++bits;
     const uint64_t B = (P + (1ull << bits) - 1) >> bits;
     pa.n_buckets = (uint32_t)B;
@@ -1190,7 +1200,7 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
   // writes each record's key, nk_table.hip), in 4096-neuron buckets
   const bool want_keyed = c->opts.exact_counts && grouped_ok(c, n_bases);
   int rc = plan_count(c, est, kPartTile, n_tiles_for(est, kPartTile), cp, z,
-                     /*keep_gen=*/n_bases <= chunk, want_keyed ? kXMinBinBits : 0);
+                     /*keep_gen=*/n_bases <= chunk, want_keyed ? xbin_bits() : 0);
   if (rc) return rc;
   in.n_tiles = n_tiles_for(n_bases, cp.tile);
   const bool batched = cp.path != CountPath::Atomic && n_bases > chunk;
