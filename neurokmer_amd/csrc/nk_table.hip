@@ -38,8 +38,6 @@ namespace {
 constexpr int kXsBlock = 256;
 constexpr int kXsPer = 8;                           // records per 16-B load of bins
 constexpr int kXsRound = kXsBlock * kXsPer;         // 2048
-constexpr int kSub = 4096;                          // records per LDS sub-tile of k_xscatter
-constexpr int kSubPer = kSub / kXsBlock;            // 16 per thread
 constexpr int kGroupN = 1 << kXGroupBits;          // largest group
 constexpr int kHashBits = 12;
 constexpr int kHashSlots = 1 << kHashBits;          // LDS table of k_xgroup
@@ -150,7 +148,9 @@ __global__ __launch_bounds__(512) void k_xbase(XGroupArgs t) {
 // linear index, so linear index L runs on XCD L % 8; bucket b's slices all go
 // to XCD b % 8, one after another, so the adjacent pieces of a group's runs
 // that consecutive slices write meet in one L2 (NK_XS_XCD=0: plain order)
+template <int kSub>  // records per LDS sub-tile
 __global__ __launch_bounds__(kXsBlock) void k_xscatter(XGroupArgs t, int xcd_order) {
+  constexpr int kSubPer = kSub / kXsBlock;  // per thread
   __shared__ unsigned long long s_key[kSub];
   __shared__ uint8_t s_bin[kSub], s_grp[kSub];
   __shared__ uint32_t cnt[kXMaxGroups], st[kXMaxGroups], gcur[kXMaxGroups], s_w[4];
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(kXsBlock) void k_xscatter(XGroupArgs t, int xcd_ord
   // this thread's 16 records of a sub-tile: s0 + j * 2048 + tid * 8 + i (16-B
   // loads contiguous across the wave); the bins and keys of the next sub-tile
   // are loaded while this one is sorted and written
-  constexpr int kJ = kSubPer / kXsPer;  // 2
+  constexpr int kJ = kSubPer / kXsPer;  // 16-B loads of bins per thread and sub-tile
   uint4 vo[kJ];
   ulonglong2 vk[kJ][kXsPer / 2];
   auto load_sub = [&](uint64_t s0) {
@@ -516,12 +516,20 @@ hipError_t xgroup_build(const XGroupArgs &t, hipStream_t s) {
   hipLaunchKernelGGL(k_xcount, gs, dim3(kXsBlock), 0, s, t);
   hipLaunchKernelGGL(k_xscan, dim3(t.n_buckets), dim3(kXsBlock), 0, s, t);
   hipLaunchKernelGGL(k_xbase, dim3(1), dim3(512), 0, s, t);
-  static const int xcd = env_int("NK_XS_XCD", 1);
-  if (xcd)
-    hipLaunchKernelGGL(k_xscatter, dim3(8u * ((t.n_buckets + 7u) / 8u) * t.n_slices), dim3(kXsBlock), 0, s,
-                       t, 1);
+  // one k_xscatter workgroup per CU: each keeps ~512 group runs with a partial
+  // 128-B line open in L2 (keys and bins), and three per CU overflowed the
+  // XCD's L2 with them (exact step 2.97-2.99 ms with 3 per CU, 2.98-3.06 with
+  // 2, 2.92-2.94 with 1 -- 80 KB of unused dynamic LDS --, profiles/r03_xspad);
+  // the LDS one workgroup per CU may use holds 8192-record sub-tiles, runs
+  // twice as long (2.92-2.94 vs 2.94-2.95 ms, profiles/r03_xssub).  A/B:
+  // NK_XS_SUB=4096 (+ NK_XS_LDS_PAD bytes of padding; 0: three per CU).
+  static const int xcd = env_int("NK_XS_XCD", 1), xs_sub = env_int("NK_XS_SUB", 8192),
+                   xs_pad = env_int("NK_XS_LDS_PAD", xs_sub == 8192 ? 0 : 80000);
+  const dim3 gx = xcd ? dim3(8u * ((t.n_buckets + 7u) / 8u) * t.n_slices) : gs;
+  if (xs_sub == 8192)
+    hipLaunchKernelGGL(k_xscatter<8192>, gx, dim3(kXsBlock), (unsigned)xs_pad, s, t, xcd);
   else
-    hipLaunchKernelGGL(k_xscatter, gs, dim3(kXsBlock), 0, s, t, 0);
+    hipLaunchKernelGGL(k_xscatter<4096>, gx, dim3(kXsBlock), (unsigned)xs_pad, s, t, xcd);
   hipLaunchKernelGGL(k_xgroup, dim3(t.n_groups, t.n_buckets), dim3(kXsBlock), 0, s, t);
   return hipGetLastError();
 }
