@@ -300,8 +300,14 @@ def main() -> int:
     # A stream per handle measured slower with 3 in flight: the third count's
     # queue was not served until the finish queue went idle (0.529-0.537 vs
     # 0.507-0.514 ms, profiles/r02_s31; NK_BENCH_COUNT_STREAM_PER_HANDLE=1).
+    # NK_BENCH_COUNT_STREAMS=2 (A/B): handles alternate between two count
+    # streams, so one batch's K1a may start while the previous batch's K1b runs.
+    n_cs = int(os.environ.get("NK_BENCH_COUNT_STREAMS", "1"))
     if os.environ.get("NK_BENCH_COUNT_STREAM_PER_HANDLE") == "1":
         count_streams = [torch.cuda.Stream(device=dev) for _ in range(args.inflight)]
+    elif n_cs > 1:
+        pool_cs = [torch.cuda.Stream(device=dev) for _ in range(n_cs)]
+        count_streams = [pool_cs[j % n_cs] for j in range(args.inflight)]
     else:
         count_streams = [torch.cuda.Stream(device=dev)] * args.inflight
     run_stream = count_streams[0]
