@@ -301,7 +301,9 @@ def main() -> int:
     # queue was not served until the finish queue went idle (0.529-0.537 vs
     # 0.507-0.514 ms, profiles/r02_s31; NK_BENCH_COUNT_STREAM_PER_HANDLE=1).
     # NK_BENCH_COUNT_STREAMS=2 (A/B): handles alternate between two count
-    # streams, so one batch's K1a may start while the previous batch's K1b runs.
+    # streams, so one batch's K1a may start while the previous batch's K1b
+    # runs: measured slower (0.5166 vs 0.5026 ms, five interleaved pairs,
+    # profiles/r03_cs2), not the default.
     n_cs = int(os.environ.get("NK_BENCH_COUNT_STREAMS", "1"))
     if os.environ.get("NK_BENCH_COUNT_STREAM_PER_HANDLE") == "1":
         count_streams = [torch.cuda.Stream(device=dev) for _ in range(args.inflight)]
