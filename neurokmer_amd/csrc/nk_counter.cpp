@@ -906,6 +906,7 @@ static int build_grouped(nk_counter *c, const KmerInput &in0, const PartArgs *ke
   t.ent = c->x_ent.p;
   t.kpn = c->kpn.p;
   t.hash_max = env_u32("NK_XHASH_MAX", 0);
+  t.hash_bits = xgroup_hash_bits();
   HIPCHK(xgroup_build(t, s));
   unsigned long long cnt[2] = {0, 0};  // grouped span, side records
   HIPCHK(hipMemcpyAsync(cnt, c->x_n.p + 4, 16, hipMemcpyDeviceToHost, s));

@@ -101,11 +101,13 @@ struct XGroupArgs {
   uint64_t *ent;                      // [pool]
   uint32_t *kpn;                      // [pool] kmer_per_neuron (side neurons: 0, added later)
   uint32_t hash_max = 0;              // tests: fewer distinct keys per pass (0: the LDS table's)
+  uint32_t hash_bits = 12;            // log2 LDS table slots of k_xgroup (xgroup_hash_bits())
 };
 // 2^gbits neurons per LDS pass for n_records records over `pool` neurons, and
 // whether the expected distinct keys of a pass fit the LDS table; the group
 // bits for a bucket of 2^bin_bits neurons
 uint32_t xgroup_bits(uint64_t n_records, uint64_t pool);
+uint32_t xgroup_hash_bits();
 inline uint32_t xgroup_group_bits(uint32_t gbits, uint32_t bin_bits) {
   const uint32_t lo = bin_bits > 8 ? bin_bits - 8 : 0;  // <= 256 groups per bucket
   return gbits > lo ? gbits : lo;

@@ -39,10 +39,6 @@ constexpr int kXsBlock = 256;
 constexpr int kXsPer = 8;                           // records per 16-B load of bins
 constexpr int kXsRound = kXsBlock * kXsPer;         // 2048
 constexpr int kGroupN = 1 << kXGroupBits;          // largest group
-constexpr int kHashBits = 12;
-constexpr int kHashSlots = 1 << kHashBits;          // LDS table of k_xgroup
-constexpr uint32_t kHashMax = kHashSlots * 5 / 8;   // distinct keys a pass may hold
-constexpr int kSlotsPer = kHashSlots / kXsBlock;    // 16
 constexpr uint16_t kPadBin = 0xFFFFu;
 constexpr unsigned long long kHashEmpty = ~0ull;
 
@@ -311,7 +307,12 @@ __device__ __forceinline__ void xg_load(const uint64_t *kp, const uint8_t *bp, u
   }
 }
 
-__global__ __launch_bounds__(kXsBlock) void k_xgroup(XGroupArgs t) {
+// HB: log2 of the LDS table's slots (12: 48 KB, three workgroups per CU; 11:
+// 24 KB, six, with half the neurons per pass)
+template <int HB, int WPE>
+__global__ __launch_bounds__(kXsBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void k_xgroup(XGroupArgs t) {
+  constexpr int kHashBits = HB, kHashSlots = 1 << HB, kSlotsPer = kHashSlots / kXsBlock;
+  constexpr uint32_t kHashMax = kHashSlots * 5 / 8;
   __shared__ unsigned long long hk[kHashSlots];
   __shared__ uint32_t hc[kHashSlots];
   __shared__ uint32_t bc[kGroupN], bcur[kGroupN], spc[kGroupN], s_w[4];
@@ -492,18 +493,24 @@ static int env_int(const char *name, int dflt) {
   return e ? atoi(e) : dflt;
 }
 
+uint32_t xgroup_hash_bits() {
+  static const int hb = env_int("NK_XG_HB", 12) == 11 ? 11 : 12;  // A/B: 11 = 2048-slot tables
+  return (uint32_t)hb;
+}
+
 uint32_t xgroup_bits(uint64_t n_records, uint64_t pool) {
-  // about kHashSlots / 2 distinct keys per pass at most (a neuron's records
+  // about (table slots) / 2 distinct keys per pass at most (a neuron's records
   // bound its distinct keys)
   const double per = pool ? (double)n_records / (double)pool : 0.0;
+  const double half = (double)(1u << xgroup_hash_bits()) / 2;
   uint32_t gb = kXGroupBits;
-  while (gb > 0 && (double)(1u << gb) * per > (double)kHashSlots / 2) --gb;
+  while (gb > 0 && (double)(1u << gb) * per > half) --gb;
   return gb;
 }
 
 bool xgroup_fits(uint64_t n_records, uint64_t pool, uint32_t gbits) {
   const double per = pool ? (double)n_records / (double)pool : 0.0;
-  return (double)(1u << gbits) * per <= (double)kHashMax * 0.8;
+  return (double)(1u << gbits) * per <= (double)((1u << xgroup_hash_bits()) * 5 / 8) * 0.8;
 }
 
 hipError_t xgroup_build(const XGroupArgs &t, hipStream_t s) {
@@ -530,7 +537,14 @@ hipError_t xgroup_build(const XGroupArgs &t, hipStream_t s) {
     hipLaunchKernelGGL(k_xscatter<8192>, gx, dim3(kXsBlock), (unsigned)xs_pad, s, t, xcd);
   else
     hipLaunchKernelGGL(k_xscatter<4096>, gx, dim3(kXsBlock), (unsigned)xs_pad, s, t, xcd);
-  hipLaunchKernelGGL(k_xgroup, dim3(t.n_groups, t.n_buckets), dim3(kXsBlock), 0, s, t);
+  static const int wpe = env_int("NK_XG_WPE", 4);  // 2048-slot tables: waves per SIMD (A/B: 4 or 5)
+  const dim3 gg(t.n_groups, t.n_buckets);
+  if (t.hash_bits == 11 && wpe == 5)
+    hipLaunchKernelGGL((k_xgroup<11, 5>), gg, dim3(kXsBlock), 0, s, t);
+  else if (t.hash_bits == 11)
+    hipLaunchKernelGGL((k_xgroup<11, 4>), gg, dim3(kXsBlock), 0, s, t);
+  else
+    hipLaunchKernelGGL((k_xgroup<12, 3>), gg, dim3(kXsBlock), 0, s, t);
   return hipGetLastError();
 }
 
