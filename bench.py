@@ -8,15 +8,23 @@ Workloads (--workload):
   config2 (default, weak scaling): 115,000,000 synthetic bases in 7 records
       per GPU, k=31, pool_size=2,000,000, --canonical, in-memory semantics
       (process_parallel).  The metric's configuration (BASELINE.json configs[1]).
-  config4 (strong scaling): one fixed input of --total-bases bases in records
-      of 115e6/7 bases (default 8 x 115e6 bases), split over the ranks by
-      dist.shard_records (byte ranges, records cut with a k-1 halo), k=31,
-      pool 2M; currents all-reduced over RCCL (u32 wire while the total k-mers
-      stay below 2^31).
-  config5 (weak scaling, a side line: BASELINE.json configs[4]): k=63 with
-      128-bit keys, pool 256,000,000, --bases per rank (default 115e6 in 7
-      records); N>1 finishes pool-sliced (dist.finalize_step_sliced: reduce-
-      scatter of the currents, LIF + top rows of each rank's 1/N of the pool).
+  config3 (a side line: BASELINE.json configs[2]): a 10 GB synthetic FASTQ
+      (150-bp reads) in /dev/shm streamed through nk_process_file_streaming,
+      k=31, pool 16,000,000 (bench_side.py).
+  config4 (strong scaling, a side line: configs[3]): one 100 Gbase input
+      (--total-bases) in records of 115e6/7 bases, split into --shard-of
+      shards (default: the world size) by dist.shard_records (byte ranges,
+      records cut with a k-1 halo); rank r counts shard r.  On one GPU
+      `--shard-of 8` times the per-GPU shard of the 8-GPU run (12.5 Gbases).
+      k=31, pool 2M; currents all-reduced over RCCL.  Generated on the device.
+  config5 (weak scaling, a side line: configs[4]): k=63 with 128-bit keys,
+      pool 256,000,000, --bases per rank (default 12.5e9 = 100 Gbases / 8, in
+      7 records, generated on the device); N>1 finishes pool-sliced
+      (dist.finalize_step_sliced: reduce-scatter of the currents, LIF + top
+      rows of each rank's 1/N of the pool).
+  Side lines (rank 0, N=1) add `parity` (full-size properties + a bit-exact
+  oracle compare on a 115 Mbase prefix), a prefix-timed `cpu_baseline` and
+  the committed PMC traffic of their count kernels (profiles/pmc_<workload>.json).
 
 One step = reset the neuron pool, then one full pass of the hot path over the
 resident input: tile/record index -> K1a hash + partition -> K1b bucket
@@ -63,6 +71,7 @@ import numpy as np  # noqa: E402
 
 METRIC = "Mk-mers/sec at k=31, pool=2M; total-spikes bit-exact vs CPU ref"
 SIDE_METRIC = {  # side lines (not BASELINE.json's metric): their own labels
+    "config3": "Mk-mers/sec at k=31, pool=16M, 10 GB FASTQ streamed from the page cache",
     "config4": "Mk-mers/sec at k=31, pool=2M, one input split across the GPUs (strong scaling)",
     "config5": "Mk-mers/sec at k=63, pool=256M, 128-bit keys (BASELINE.json configs[4])",
 }
@@ -71,6 +80,9 @@ POOL = 2_000_000
 BASES = 115_000_000
 RECS = 7
 REC_LEN4 = BASES // RECS  # config 4 record length
+C4_TOTAL = 100_000_000_000  # config 4: 100 Gbases over the GPUs
+C5_BASES = 12_500_000_000  # config 5: 100 Gbases / 8 per GPU
+HOST_GEN_MAX = 1_000_000_000  # larger inputs are generated on the device
 HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md chip table)
 
 
@@ -87,6 +99,21 @@ def load_pmc():
             return json.load(f)
     except Exception:
         return {}
+
+
+def load_side_pmc(workload: str, n_bases: int, k: int, pool: int, width: int) -> dict:
+    """profiles/pmc_<workload>.json (tools/pmc_side.py): HBM bytes and VALU
+    instructions of one step's count kernels, when measured on this shape."""
+    try:
+        with open(os.path.join(ROOT, "profiles", f"pmc_{workload}.json")) as f:
+            d = json.load(f)
+    except Exception:
+        return {}
+    shape = d.get("shape", {})
+    if (shape.get("bases"), shape.get("k"), shape.get("pool"), shape.get("width")) != \
+            (n_bases, k, pool, width):
+        return {}
+    return d
 
 
 def spawn_ranks(n: int) -> int:
@@ -156,9 +183,16 @@ def main() -> int:
     # extra in all): 50 steps amortise it (profiles/r02_s22)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=("config2", "config4", "config5"), default="config2")
-    ap.add_argument("--bases", type=int, default=BASES, help="config2: bases per rank")
-    ap.add_argument("--total-bases", type=int, default=8 * BASES, help="config4: bases in all")
+    ap.add_argument("--workload", choices=("config2", "config3", "config4", "config5"),
+                    default="config2")
+    ap.add_argument("--bases", type=int, default=None,
+                    help="config2/5: bases per rank (default 115e6 / 12.5e9)")
+    ap.add_argument("--total-bases", type=int, default=C4_TOTAL, help="config4: bases in all")
+    ap.add_argument("--shard-of", type=int, default=0,
+                    help="config4: split the input into this many shards (default: world size)")
+    ap.add_argument("--no-side-parity", action="store_true",
+                    help="side lines: skip the properties / prefix oracle compare")
+    ap.add_argument("--fastq", default=None, help="config3: the FASTQ (default: generated in /dev/shm)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip end_to_end and the exact_counts step (rank 0, N=1)")
@@ -197,6 +231,12 @@ def main() -> int:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch with "
               f"torchrun --nproc-per-node {args.gpus} (or no torchrun)", file=sys.stderr)
         return 2
+
+    if args.workload == "config3":
+        import bench_side
+        return bench_side.config3(args)
+    if args.bases is None:
+        args.bases = C5_BASES if args.workload == "config5" else BASES
 
     import torch
     import torch.distributed as dist
@@ -251,32 +291,50 @@ def main() -> int:
     comm = nkdist.Comm(device=dev_idx) if (lib_comm or (dist_on and args.nk_comm)) else None
 
     # ---- this rank's input (resident in HBM) -------------------------------
+    bases = None  # host copy (host-generated inputs only)
     if args.workload in ("config2", "config5"):
-        bases, offsets = synth.make_records(args.bases, RECS, seed=synth.SEED ^ (rank * 0x9E37),
-                                            repeats_per_mb=64, motif_len=200)
+        seed = synth.SEED ^ (rank * 0x9E37)
+        if args.bases <= HOST_GEN_MAX:
+            bases, offsets = synth.make_records(args.bases, RECS, seed=seed,
+                                                repeats_per_mb=64, motif_len=200)
+            d_bases = torch.from_numpy(bases).to(dev)
+        else:  # the same stream generated on the device (bench_side.py checks a prefix)
+            d_bases, offsets = synth.make_records_torch(args.bases, RECS, seed=seed,
+                                                        repeats_per_mb=64, motif_len=200,
+                                                        device=dev)
+        n_bases = args.bases
         nk_rank = n_kmers(offsets, k)
         total_kmers = world * nk_rank  # same size on every rank
         scaling = "weak"
-        workload = (f"config {args.workload[-1]}: {bases.size:,} bases in {RECS} records per GPU, "
+        workload = (f"config {args.workload[-1]}: {n_bases:,} bases in {RECS} records per GPU, "
                     f"k={k}, kmer_width={args.kmer_width}, pool_size={pool:,}, --canonical, "
                     + ("process_parallel" if args.workload == "config2" or world == 1 else
                        "pool-sliced finish"))
     else:
         T = args.total_bases
+        n_shards = args.shard_of or world
+        if n_shards < world:
+            print("bench.py: --shard-of must be >= the world size", file=sys.stderr)
+            return 2
         n_rec = max(1, -(-T // REC_LEN4))
         glob = np.minimum(np.arange(n_rec + 1, dtype=np.int64) * REC_LEN4, T).astype(np.uint64)
-        lo, hi, rel, _skip = nkdist.shard_records(glob, world, k)[rank]  # k <= 32: no warm-up
-        bases = synth.random_bases(hi - lo, seed=synth.SEED, start=lo)
+        shards = nkdist.shard_records(glob, n_shards, k)
+        lo, hi, rel, _skip = shards[rank]  # k <= 32: no warm-up
+        n_bases = hi - lo
+        d_bases = torch.zeros(n_bases + 16, dtype=torch.uint8, device=dev)
+        synth.random_bases_torch(n_bases, synth.SEED, lo, dev, out=d_bases)
         offsets = rel.astype(np.uint64)
+        args.shard_lo = lo
         nk_rank = n_kmers(offsets, k)
-        total_kmers = n_kmers(glob, k)
+        total_kmers = sum(n_kmers(sh[2].astype(np.uint64), k) for sh in shards[:world])
         scaling = "strong"
         workload = (f"config 4 (strong scaling): {T:,} bases in {n_rec} records of {REC_LEN4:,}, "
-                    f"split by shard_records over {world} rank(s), k={k}, pool_size={pool:,}, "
-                    f"--canonical")
+                    f"split by shard_records into {n_shards} shards"
+                    + (f", rank r counts shard r (here: shard 0 of {n_shards} on {world} GPU)"
+                       if n_shards != world else f" over {world} rank(s)")
+                    + f", k={k}, pool_size={pool:,}, --canonical")
     n_recs = offsets.size - 1
-    log(f"rank {rank}/{world}: {bases.size:,} bases, {n_recs} records on cuda:{dev_idx}")
-    d_bases = torch.from_numpy(bases).to(dev)
+    log(f"rank {rank}/{world}: {n_bases:,} bases, {n_recs} records on cuda:{dev_idx}")
     d_offs = torch.from_numpy(offsets.view(np.int64)).to(dev)
     torch.cuda.synchronize()
 
@@ -319,13 +377,24 @@ def main() -> int:
     s_handle = run_stream.cuda_stream
 
     start_host_s = []  # host time of each start() (the enqueue of a count)
+    # side lines (configs 4/5): hipEvents on the count stream around each
+    # step's whole count (a multi-GB input runs several batches per count)
+    side = args.workload in ("config4", "config5")
+    count_ev = []
 
     def start(j):
         """Enqueue one batch's count on handle j (returns at once)."""
         t_s = time.perf_counter()
-        c, sh = ctrs[j], count_streams[j].cuda_stream
+        c, cs = ctrs[j], count_streams[j]
+        sh = cs.cuda_stream
         c.reset(sh, blocking=False)
-        c.accumulate_device(d_bases.data_ptr(), d_offs.data_ptr(), n_recs, bases.size, sh)
+        if side:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(cs)
+        c.accumulate_device(d_bases.data_ptr(), d_offs.data_ptr(), n_recs, n_bases, sh)
+        if side:
+            e1.record(cs)
+            count_ev.append((e0, e1))
         start_host_s.append(time.perf_counter() - t_s)
 
     def finish(j, st, between=None):
@@ -421,7 +490,9 @@ def main() -> int:
 
     marks = []
     del start_host_s[:]
+    del count_ev[:]
     t0, dt = timed(args.steps, args.inflight, marks)
+    count_ms = [a.elapsed_time(b) for a, b in count_ev]
     start_ms = sorted(start_host_s)
     start_ms = (round(start_ms[len(start_ms) // 2] * 1e3, 4), round(start_ms[-1] * 1e3, 4)) \
         if start_ms else None
@@ -466,11 +537,17 @@ def main() -> int:
         k1_ms = float(np.mean(sp)) if sp else (float(np.mean(ev_ms)) if ev_ms else float("nan"))
         # roofline of the dominant kernel (K1a), algorithmic bytes per launch =
         # input bases read once + one 8-B counter update per k-mer
-        alg_bytes = bases.size + 8 * nk_rank
+        alg_bytes = n_bases + 8 * nk_rank
+        cm = float(np.median(count_ms)) if (side and count_ms) else None
+        if cm:  # side lines: the whole count of a step (every batch) between hipEvents
+            k1_ms = cm
         achieved = alg_bytes / (k1_ms * 1e-3)
         pmc = load_pmc()
         cfg2 = args.workload == "config2" and args.bases == BASES and k == K and pool == POOL
         traffic = pmc.get("hbm_bytes_per_launch") if cfg2 else None
+        side_pmc = load_side_pmc(args.workload, n_bases, k, pool, args.kmer_width) if side else {}
+        if side_pmc:
+            traffic = side_pmc.get("hbm_bytes_per_count")
         # the limiter, measured in this run: the same GPU's rate for the hash
         # work alone (SipHash-1-3 + exact % pool of register-generated keys, no
         # memory traffic: nk_diag_hash_ms) against K1a's k-mer rate
@@ -482,6 +559,8 @@ def main() -> int:
             valu.update({"hash_only_ms": round(floor_ms, 4),
                          "hash_only_gkmers_per_s": round(nk_rank / (floor_ms * 1e-3) / 1e9, 2),
                          "frac_of_hash_only": round(floor_ms / k1_ms, 4)})
+        if side_pmc.get("valu_instr_per_count"):
+            valu["valu_instr_per_count"] = side_pmc["valu_instr_per_count"]
         if cfg2 and pmc.get("valu_instr_per_launch"):
             valu["valu_instr_per_launch"] = pmc["valu_instr_per_launch"]
             valu["pmc_source"] = pmc.get("source")
@@ -502,7 +581,7 @@ def main() -> int:
                      ("^rank, 64x200-bp planted repeats per MB)" if args.workload != "config4"
                       else ", one global stream sharded by byte range)")),
             "config": {"workload": workload, "k": k, "kmer_width": args.kmer_width,
-                       "pool_size": pool, "bases_rank0": int(bases.size), "records_rank0": n_recs,
+                       "pool_size": pool, "bases_rank0": int(n_bases), "records_rank0": n_recs,
                        "kmers_rank0": nk_rank, "kmers_total": total_kmers,
                        "parallelism": f"dp{world}" + (f" (rehearsal: {world} ranks on {ndev} GPU, "
                                                       f"{backend})" if shared else ""),
@@ -512,14 +591,21 @@ def main() -> int:
                                        else (f"torch.distributed {backend} from Python" if dist_on
                                              else None))},
             "roofline": {"bound": bound,
-                         "kernel": ("k_part<canonical> (K1a)" if k <= 32 and pool <= (1 << 24)
+                         "kernel": ("the count of a step: every batch's K1 (k_part / k_part_gen "
+                                    "+ k_split) + K1b (k_bucket_hist)" if cm else
+                                    "k_part<canonical> (K1a)" if k <= 32 and pool <= (1 << 24)
                                     else "the count: k_part_gen (K1g) + k_split (K1s)"),
                          "achieved": round(achieved / 1e9, 2), "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": round(hbm_frac, 4),
-                         "traffic": traffic, "traffic_source": pmc.get("source") if traffic else None,
+                         "traffic": traffic,
+                         "traffic_source": ((side_pmc.get("source") if side_pmc else pmc.get("source"))
+                                            if traffic else None),
                          "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(k1_ms, 4),
-                         "avg_launch_source": ("in-kernel s_memrealtime span over the one-in-flight timed steps"
-                                               if sp else "hipEvents"),
+                         "avg_launch_source": (
+                             "hipEvents on the count stream around each timed step's count "
+                             "(every batch's K1 + K1b), median" if cm else
+                             ("in-kernel s_memrealtime span over the one-in-flight timed steps"
+                              if sp else "hipEvents")),
                          "launches_timed": len(sp),
                          "avg_launch_ms_events": round(float(np.mean(ev_ms)), 4) if ev_ms else None,
                          "valu": valu},
@@ -534,6 +620,12 @@ def main() -> int:
         if world == 1 and args.workload == "config2" and args.kmer_width == 64:
             out.update(extras(args, ctr, bases, offsets, nk_rank, d_bases, d_offs, s_handle,
                               dev_idx, SpikingKmerCounter, synth))
+        if side:
+            out["count_ms_steps"] = [round(x, 4) for x in count_ms]
+        if world == 1 and side and not args.no_side_parity:
+            import bench_side
+            out.update(bench_side.side_extras(args, ctr, d_bases, offsets, n_bases, nk_rank,
+                                              dev_idx))
         print(json.dumps(out), flush=True)
     for c in ctrs:
         c.close()
@@ -557,28 +649,41 @@ def parity_ranks(args, ctr, world, rank, dev_idx, nkdist, Counter, synth, total_
         return None
     k, pool = args.k, args.pool
     t0 = time.perf_counter()
-    if args.workload == "config4":
+    dev = torch.device("cuda", dev_idx)
+    if args.workload == "config4":  # every shard of this run: [0, last shard's end)
         T = args.total_bases
         n_rec = max(1, -(-T // REC_LEN4))
-        offs = np.minimum(np.arange(n_rec + 1, dtype=np.int64) * REC_LEN4, T).astype(np.uint64)
-        bases = synth.random_bases(T, seed=synth.SEED, start=0)
+        glob = np.minimum(np.arange(n_rec + 1, dtype=np.int64) * REC_LEN4, T).astype(np.uint64)
+        n_shards = args.shard_of or world
+        end = nkdist.shard_records(glob, n_shards, k)[world - 1][1]
+        offs = np.concatenate([glob[glob < end], np.array([end], np.uint64)])
+        n_all = int(end)
+        d_b = torch.zeros(n_all + 16, dtype=torch.uint8, device=dev)
+        synth.random_bases_torch(n_all, synth.SEED, 0, dev, out=d_b)
     else:
         parts, offl, at = [], [np.zeros(1, np.uint64)], 0
         for r in range(world):
-            b, o = synth.make_records(args.bases, RECS, seed=synth.SEED ^ (r * 0x9E37),
-                                      repeats_per_mb=64, motif_len=200)
-            parts.append(b)
+            seed = synth.SEED ^ (r * 0x9E37)
+            if args.bases <= HOST_GEN_MAX:
+                b, o = synth.make_records(args.bases, RECS, seed=seed, repeats_per_mb=64,
+                                          motif_len=200)
+                parts.append(torch.from_numpy(b).to(dev))
+            else:
+                b, o = synth.make_records_torch(args.bases, RECS, seed=seed, repeats_per_mb=64,
+                                                motif_len=200, device=dev, pad=0)
+                parts.append(b)
             offl.append(o[1:] + np.uint64(at))
-            at += b.size
-        bases, offs = np.concatenate(parts), np.concatenate(offl)
+            at += args.bases
+        parts.append(torch.zeros(16, dtype=torch.uint8, device=dev))
+        d_b = torch.cat(parts)
         del parts
+        offs = np.concatenate(offl)
+        n_all = at
     gen_s = time.perf_counter() - t0
-    dev = torch.device("cuda", dev_idx)
-    d_b = torch.from_numpy(np.concatenate([bases, np.zeros(16, np.uint8)])).to(dev)
     d_o = torch.from_numpy(offs.view(np.int64)).to(dev)
     torch.cuda.synchronize()
     g = Counter(k, 1.0, 0.95, 2, 1.0, pool, True, device=dev_idx, kmer_width=args.kmer_width)
-    g.process_parallel_device(d_b.data_ptr(), d_o.data_ptr(), offs.size - 1, bases.size)
+    g.process_parallel_device(d_b.data_ptr(), d_o.data_ptr(), offs.size - 1, n_all)
     if st is None:
         st = {"currents": ctr.currents(), "spike_counts": ctr.spike_counts(),
               "voltages": ctr.voltages(), "refractory": ctr.refractory()}
@@ -587,7 +692,7 @@ def parity_ranks(args, ctr, world, rank, dev_idx, nkdist, Counter, synth, total_
     top_n, top_1 = ctr.top_abundant_neurons(20), g.top_abundant_neurons(20)
     # every step starts from a reset pool: the spike counts are the last step's
     spikes_n, spikes_1 = int(st["spike_counts"].sum(dtype=np.uint64)), g.energy.total_spikes()
-    out = {"method": (f"rank 0 regenerated all {world} ranks' inputs ({bases.size:,} bases, "
+    out = {"method": (f"rank 0 regenerated all {world} ranks' inputs ({n_all:,} bases, "
                       f"{offs.size - 1} records) and ran ONE process_parallel over them on its GPU; "
                       "compared with the N-rank step's final state"),
            "currents": bool(np.array_equal(st["currents"], one["currents"])),
