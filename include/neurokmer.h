@@ -196,6 +196,21 @@ typedef struct nk_comm nk_comm;
 int nk_comm_unique_id(uint8_t id[NK_COMM_ID_BYTES]);
 nk_comm *nk_comm_new(const uint8_t id[NK_COMM_ID_BYTES], int world, int rank, int device);
 void nk_comm_free(nk_comm *m);
+/* Drop the device buffers m holds for handle c (wire, export and all-gather
+ * segments); call before nk_free(c) when m outlives c.  nk_comm_free drops
+ * every handle's. */
+void nk_comm_forget(nk_comm *m, const nk_counter *c);
+/* Loopback transport (tests and one-GPU rehearsals; not an RCCL replacement):
+ * `world` ranks as host threads of ONE process on one device, each with its
+ * own nk_comm_new_loopback communicator, every collective done by device
+ * copies and a sum kernel between host barriers (a rank that does not arrive
+ * within 120 s fails every rank's call).  RCCL refuses two ranks on one
+ * device, so this is how nk_finalize_dist / nk_finalize_sliced_dist run at
+ * world > 1 on a one-GPU box.  world: 1 .. 16. */
+typedef struct nk_loop_group nk_loop_group;
+nk_loop_group *nk_loop_group_new(int world);
+void nk_loop_group_free(nk_loop_group *g);  /* after every member's nk_comm_free */
+nk_comm *nk_comm_new_loopback(nk_loop_group *g, int rank, int device);
 /* After nk_accumulate_device(_from) on every rank: the whole multi-GPU finish
  * enqueued on `stream` with no host code between the steps (the same protocol
  * as nk_wire32 .. nk_merge_export above, the all-reduce and all-gather issued

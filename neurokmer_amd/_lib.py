@@ -47,6 +47,7 @@ EXPORTS = (
     "nk_exact_owner", "nk_exact_partition", "nk_exact_adopt", "nk_device_kmer_per_neuron",
     "nk_set_stage_timing", "nk_diag_hash_ms", "nk_diag_hash_ms_w", "nk_count_spans", "nk_simulate_spikes_auto",
     "nk_comm_unique_id", "nk_comm_new", "nk_comm_free", "nk_finalize_dist", "nk_finalize_sliced_dist",
+    "nk_comm_forget", "nk_loop_group_new", "nk_loop_group_free", "nk_comm_new_loopback",
     "nk_last_error",
     "nk_version",
 )
@@ -161,6 +162,10 @@ def load(share_torch: bool = True):
         "nk_comm_unique_id": (C.c_int, [vp]),
         "nk_comm_new": (vp, [vp, C.c_int, C.c_int, C.c_int]),
         "nk_comm_free": (None, [vp]),
+        "nk_comm_forget": (None, [vp, vp]),
+        "nk_loop_group_new": (vp, [C.c_int]),
+        "nk_loop_group_free": (None, [vp]),
+        "nk_comm_new_loopback": (vp, [vp, C.c_int, C.c_int]),
         "nk_finalize_dist": (C.c_int, [vp, vp, C.c_int, u64, sz, vp]),
         "nk_finalize_sliced_dist": (C.c_int, [vp, vp, C.c_int, u64, sz, vp]),
         "nk_last_error": (C.c_char_p, []),

@@ -11,6 +11,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <future>
 #include <string>
@@ -106,7 +107,11 @@ const char *kStageNamesLight[kStagesLight] = {"index", "count", "post", "total"}
 
 }  // namespace
 
+static std::atomic<uint64_t> g_next_uid{1};
+
 struct nk_counter {
+  // never reused (nk_dist.cpp keys a communicator's per-handle buffers by it)
+  const uint64_t uid = g_next_uid.fetch_add(1);
   size_t k = 0, pool = 0;
   float thr = 1.0f, leak = 0.95f;
   uint32_t refr = 2;
@@ -482,6 +487,7 @@ bool counter_kpn_global(const nk_counter *c) {
   return c->opts.exact_counts && c->exact_built && c->kpn_global;
 }
 void counter_merge_hint(nk_counter *c, uint32_t world) { c->merge_world_hint = world; }
+uint64_t counter_uid(const nk_counter *c) { return c->uid; }
 uint64_t *counter_currents_on(nk_counter *c, hipStream_t stream) {
   if (c->cur_in_wire) {
     fail(NK_E_INVALID, "the currents are in the wire vector until nk_finalize_export");
@@ -786,7 +792,7 @@ static int build_sorted(nk_counter *c, const KmerInput &in0, hipStream_t s) {
   return NK_OK;
 }
 
-static uint64_t count_chunk();
+static uint64_t count_chunk(uint64_t n_bases = 0, uint64_t pool = 0);
 static uint32_t env_u32(const char *name, uint32_t dflt);
 
 // neurons per K1a<KEYS> bucket (log2): kXMinBinBits; NK_XBIN_BITS (A/B,
@@ -1000,19 +1006,34 @@ static bool atomic_forced() {
 }
 
 // Positions counted per partition launch.  An input up to this size keeps its
-// records (4-5 B per k-mer) for the uniques scan; a larger one is counted in
-// batches of this many positions whose records are histogrammed and dropped
-// batch by batch (the arena is O(batch), not O(input): a config-4 shard of
-// 12.5 Gbases needs ~11 GB instead of ~62 GB) and the top rows' uniques come
-// from a rescan of the input.  NK_COUNT_CHUNK (tests) sets it, rounded to
-// whole partition tiles.
+// records (4-5 B per k-mer; 7.5 B on the wide path) for the uniques scan,
+// which then reads only the top rows' buckets; a larger one is counted in
+// batches whose records are histogrammed and dropped batch by batch, and the
+// top rows' uniques come from a rescan of the WHOLE input (a full re-hash:
+// ~115 ms of a 166 ms step at a 12.5 Gbase config-4 shard, profiles/r04_side).
+// So an input past the default batch is counted in ONE launch whenever its
+// arena fits in kKeepFrac of the free HBM (a 12.5 Gbase shard: ~63 GB Part,
+// ~95 GB wide, of 288 GB); batches remain for inputs that do not fit.
+// NK_COUNT_CHUNK (tests) forces a batch size, rounded to whole tiles.
 #ifndef NK_COUNT_CHUNK_DEFAULT
 #define NK_COUNT_CHUNK_DEFAULT (1ull << 31)
 #endif
-static uint64_t count_chunk() {
+constexpr uint64_t kKeepBytesPerBase = 10;  // arena bytes per position, upper bound (wide path + slack)
+constexpr double kKeepFrac = 0.45;
+// (pool: a bucket region of one launch stays below 2^31 records, so K1b's u32
+// bins and partials cannot wrap whatever the input)
+static uint64_t count_chunk(uint64_t n_bases, uint64_t pool) {
   const char *e = getenv("NK_COUNT_CHUNK");
   uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
-  if (!v) v = NK_COUNT_CHUNK_DEFAULT;
+  if (!v) {
+    v = NK_COUNT_CHUNK_DEFAULT;
+    const uint64_t B = std::max<uint64_t>(1, (pool + kBinsPerBucket - 1) >> kBinBits);
+    size_t fr = 0, tot = 0;
+    if (n_bases > v && pool && n_bases / B * 5 / 4 < (1ull << 31) - (1ull << 24) &&
+        !getenv("NK_COUNT_BATCHED") && hipMemGetInfo(&fr, &tot) == hipSuccess &&
+        (double)n_bases * kKeepBytesPerBase <= kKeepFrac * (double)fr)
+      v = (n_bases + kPartTile - 1) / kPartTile * kPartTile;
+  }
   return std::max<uint64_t>(kPartTile, v / kPartTile * kPartTile);
 }
 
@@ -1195,7 +1216,7 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
   // bucket regions: 1.25x the fair share + one tile of slack (overflow is
   // still exact: the excess is counted with direct atomics); past
   // count_chunk() positions the regions hold one batch at a time
-  const uint64_t chunk = count_chunk();
+  const uint64_t chunk = count_chunk(n_bases, c->pool);
   const uint64_t est = std::min<uint64_t>(n_bases, chunk);
   // the exact table grouped by neuron from this count's own records (K1a also
   // writes each record's key, nk_table.hip), in 4096-neuron buckets
@@ -2570,7 +2591,7 @@ static int acc_begin(nk_counter *c, uint64_t est_bases, uint64_t batch_bases, St
   z.ptr[z.n] = c->cur.p; z.bytes[z.n++] = c->pool * 8;
   const uint64_t B = (c->pool + kBinsPerBucket - 1) >> kBinBits;
   const bool part_like = !c->w128 && c->k <= 32 && B <= (uint64_t)kMaxBuckets &&
-                         !wide_bits_forced() && est_bases <= count_chunk();
+                         !wide_bits_forced() && est_bases <= count_chunk(est_bases, c->pool);
   const uint64_t est = part_like ? est_bases : std::min(est_bases, batch_bases);
   // segments per bucket: one per tile per launch; chunk-straddling tiles add a few
   const uint64_t max_segs = n_tiles_for(std::max<uint64_t>(est, 1), kPartTile) + 4096;

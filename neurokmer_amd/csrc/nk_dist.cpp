@@ -124,8 +124,12 @@ int need_rccl() {
 
 struct nk_comm {
   ncclComm_t comm = nullptr;
+  nk_loop_group *loop = nullptr;  // the loopback transport instead of RCCL (nk_loop.hip)
   int world = 0, rank = 0, device = 0;
-  std::unordered_map<const nk_counter *, HandleBufs> bufs;
+  // per handle, keyed by its never-reused id (a handle freed and another
+  // allocated at the same address must not inherit the buffers' state)
+  std::unordered_map<uint64_t, HandleBufs> bufs;
+  HandleBufs &of(const nk_counter *c) { return bufs[nk::counter_uid(c)]; }
 };
 
 #define NCCLCHK(expr)                                                                  \
@@ -146,6 +150,29 @@ struct nk_comm {
 
 namespace {
 
+// The three collectives the finish uses, over RCCL or the loopback transport
+// (n: elements per rank for the all-gather and the reduce-scatter's output)
+int coll(nk_comm *m, int kind, const void *send, void *recv, size_t n, bool u64, hipStream_t s) {
+  if (m->loop)
+    return nk::loop_collective(m->loop, m->rank, kind, send, recv, n, u64 ? 8 : 4, s);
+  const ncclDataType_t dt = u64 ? ncclUint64 : ncclUint32;
+  switch (kind) {
+    case 0: NCCLCHK(rccl().all_reduce(send, recv, n, dt, ncclSum, m->comm, s)); break;
+    case 1: NCCLCHK(rccl().all_gather(send, recv, n, dt, m->comm, s)); break;
+    default: NCCLCHK(rccl().reduce_scatter(send, recv, n, dt, ncclSum, m->comm, s)); break;
+  }
+  return NK_OK;
+}
+int all_reduce(nk_comm *m, const void *send, void *recv, size_t n, bool u64, hipStream_t s) {
+  return coll(m, 0, send, recv, n, u64, s);
+}
+int all_gather(nk_comm *m, const void *send, void *recv, size_t n, bool u64, hipStream_t s) {
+  return coll(m, 1, send, recv, n, u64, s);
+}
+int reduce_scatter(nk_comm *m, const void *send, void *recv, size_t n, bool u64, hipStream_t s) {
+  return coll(m, 2, send, recv, n, u64, s);
+}
+
 // The top rows' uniques column from the union of every shard's distinct top
 // k-mers (after a finish that left the rows set but the column per shard):
 // one fixed-size all-gather of [n, keys...] segments; a segment past `cap`
@@ -157,7 +184,7 @@ int union_top_kmers(nk_counter *c, nk_comm *m, HandleBufs &b, size_t cap, hipStr
     const size_t stride = 1 + (size_t)wpk * cap;
     OOM(b.useg.ensure(stride) && b.uall.ensure(W * stride), "key union buffers");
     RC(nk_top_kmers_padded(c, b.useg.p, cap, s));
-    NCCLCHK(rccl().all_gather(b.useg.p, b.uall.p, stride, ncclUint64, m->comm, s));
+    RC(all_gather(m, b.useg.p, b.uall.p, stride, true, s));
     int complete = 0;
     RC(nk_merge_top_kmers_padded(c, b.uall.p, W, stride, cap, &complete, s));
     if (complete) return NK_OK;
@@ -170,7 +197,7 @@ int union_top_kmers(nk_counter *c, nk_comm *m, HandleBufs &b, size_t cap, hipStr
     const uint64_t mine = n;
     if (hipMemcpyAsync(b.nvec.p, &mine, 8, hipMemcpyHostToDevice, s) != hipSuccess)
       return failf(NK_E_DEVICE, "key count copy failed");
-    NCCLCHK(rccl().all_gather(b.nvec.p, b.nvec.p + W, 1, ncclUint64, m->comm, s));
+    RC(all_gather(m, b.nvec.p, b.nvec.p + W, 1, true, s));
     std::vector<uint64_t> all(W);
     if (hipMemcpyAsync(all.data(), b.nvec.p + W, W * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
@@ -219,6 +246,34 @@ nk_comm *nk_comm_new(const uint8_t id[NK_COMM_ID_BYTES], int world, int rank, in
   return m;
 }
 
+nk_comm *nk_comm_new_loopback(nk_loop_group *g, int rank, int device) {
+  if (!g) {
+    failf(NK_E_INVALID, "null loopback group");
+    return nullptr;
+  }
+  if (hipSetDevice(device) != hipSuccess) {
+    failf(NK_E_NO_DEVICE, "hipSetDevice(%d) failed", device);
+    return nullptr;
+  }
+  if (nk::loop_join(g, rank, device)) return nullptr;
+  nk_comm *m = new nk_comm();
+  m->loop = g;
+  m->world = nk::loop_world(g);
+  m->rank = rank;
+  m->device = device;
+  return m;
+}
+
+void nk_comm_forget(nk_comm *m, const nk_counter *c) {
+  if (!m || !c) return;
+  auto it = m->bufs.find(nk::counter_uid(c));
+  if (it == m->bufs.end()) return;
+  (void)hipSetDevice(m->device);
+  (void)hipDeviceSynchronize();
+  it->second.release();
+  m->bufs.erase(it);
+}
+
 void nk_comm_free(nk_comm *m) {
   if (!m) return;
   (void)hipSetDevice(m->device);
@@ -237,31 +292,31 @@ int nk_finalize_dist(nk_counter *c, nk_comm *m, int streaming, uint64_t total_km
   if (!stream) return failf(NK_E_INVALID, "a stream is required");
   (void)hipSetDevice(m->device);
   hipStream_t s = (hipStream_t)stream;
-  HandleBufs &b = m->bufs[c];
+  HandleBufs &b = m->of(c);
   const uint64_t P = nk_pool_size(c);
   const size_t W = (size_t)m->world;
   if (nk::counter_kpn_global(c)) {  // exact table adopted: u64 currents, uniques from kpn
     uint64_t *cur = nk::counter_currents_on(c, s);
     if (!cur && P) return NK_E_DEVICE;
-    if (P) NCCLCHK(rccl().all_reduce(cur, cur, P, ncclUint64, ncclSum, m->comm, s));
+    if (P) RC(all_reduce(m, cur, cur, P, true, s));
     return nk_finalize(c, streaming, stream);
   }
   const uint32_t *wire = nullptr;
   if (total_kmers < (1ull << 31)) {  // no summed current can leave u32
     OOM(b.wire32.ensure(std::max<uint64_t>(P, 1)), "wire vector");
     RC(nk_wire32(c, b.wire32.p, stream));
-    if (P) NCCLCHK(rccl().all_reduce(b.wire32.p, b.wire32.p, P, ncclUint32, ncclSum, m->comm, s));
+    if (P) RC(all_reduce(m, b.wire32.p, b.wire32.p, P, false, s));
     wire = b.wire32.p;
   } else {
     uint64_t *cur = nk::counter_currents_on(c, s);
     if (!cur && P) return NK_E_DEVICE;
-    if (P) NCCLCHK(rccl().all_reduce(cur, cur, P, ncclUint64, ncclSum, m->comm, s));
+    if (P) RC(all_reduce(m, cur, cur, P, true, s));
   }
   const size_t stride = 1 + (size_t)nk::counter_key_words(c) * cap;
   OOM(b.seg.ensure(stride) && b.all.ensure(W * stride), "export segments");
   nk::counter_merge_hint(c, (uint32_t)W);
   RC(nk_finalize_export(c, streaming, wire, b.seg.p, cap, stream));
-  NCCLCHK(rccl().all_gather(b.seg.p, b.all.p, stride, ncclUint64, m->comm, s));
+  RC(all_gather(m, b.seg.p, b.all.p, stride, true, s));
   int redo = 0;
   RC(nk_merge_export(c, b.all.p, W, stride, cap, &redo, stream));
   if (!redo) return NK_OK;
@@ -278,7 +333,7 @@ int nk_finalize_sliced_dist(nk_counter *c, nk_comm *m, int streaming, uint64_t t
   if (!stream) return failf(NK_E_INVALID, "a stream is required");
   (void)hipSetDevice(m->device);
   hipStream_t s = (hipStream_t)stream;
-  HandleBufs &b = m->bufs[c];
+  HandleBufs &b = m->of(c);
   const uint64_t P = nk_pool_size(c);
   const uint64_t W = (uint64_t)m->world;
   const uint64_t S = P ? (P + W - 1) / W : 0;  // neurons per slice (the last may be short)
@@ -294,7 +349,7 @@ int nk_finalize_sliced_dist(nk_counter *c, nk_comm *m, int streaming, uint64_t t
     OOM(b.wire32.ensure(std::max<uint64_t>(W * S, 1), true) && b.part32.ensure(std::max<uint64_t>(S, 1)),
         "slice wire");
     RC(nk_wire32(c, b.wire32.p, stream));
-    if (S) NCCLCHK(rccl().reduce_scatter(b.wire32.p, b.part32.p, S, ncclUint32, ncclSum, m->comm, s));
+    if (S) RC(reduce_scatter(m, b.wire32.p, b.part32.p, S, false, s));
     slice = b.part32.p;
   } else {
     OOM(b.wire64.ensure(std::max<uint64_t>(W * S, 1), true) && b.part64.ensure(std::max<uint64_t>(S, 1)),
@@ -303,7 +358,7 @@ int nk_finalize_sliced_dist(nk_counter *c, nk_comm *m, int streaming, uint64_t t
     if (!cur && P) return NK_E_DEVICE;
     if (P && hipMemcpyAsync(b.wire64.p, cur, P * 8, hipMemcpyDeviceToDevice, s) != hipSuccess)
       return failf(NK_E_DEVICE, "wire copy failed");
-    if (S) NCCLCHK(rccl().reduce_scatter(b.wire64.p, b.part64.p, S, ncclUint64, ncclSum, m->comm, s));
+    if (S) RC(reduce_scatter(m, b.wire64.p, b.part64.p, S, true, s));
     slice = b.part64.p;
   }
   const uint64_t rows = nk::counter_rows(c);
@@ -311,7 +366,7 @@ int nk_finalize_sliced_dist(nk_counter *c, nk_comm *m, int streaming, uint64_t t
   OOM(b.sseg.ensure(stride) && b.sall.ensure(W * stride), "slice row segments");
   RC(nk_finalize_slice(c, streaming, hi > lo ? slice : nullptr, small ? 32 : 64, lo, hi, b.sseg.p,
                        rows, stream));
-  NCCLCHK(rccl().all_gather(b.sseg.p, b.sall.p, stride, ncclUint64, m->comm, s));
+  RC(all_gather(m, b.sseg.p, b.sall.p, stride, true, s));
   RC(nk_adopt_slices(c, b.sall.p, W, stride, stream));
   return union_top_kmers(c, m, b, cap, s);
 }

@@ -23,4 +23,13 @@ bool counter_kpn_global(const nk_counter *c);
 // then emptied by the export's header kernel)
 void counter_merge_hint(nk_counter *c, uint32_t world);
 uint64_t *counter_currents_on(nk_counter *c, hipStream_t s);
+// a per-process id of the handle, never reused after nk_free
+uint64_t counter_uid(const nk_counter *c);
+// the loopback transport (nk_loop.hip)
+int loop_join(nk_loop_group *g, int rank, int device);
+int loop_world(const nk_loop_group *g);
+// kind 0 all-reduce (sum, n elements), 1 all-gather (n per rank), 2
+// reduce-scatter (sum, n per rank); elem 4 or 8 bytes; blocks until done
+int loop_collective(nk_loop_group *g, int rank, int kind, const void *send, void *recv, size_t n,
+                    int elem, hipStream_t s);
 }  // namespace nk

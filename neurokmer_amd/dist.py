@@ -133,9 +133,57 @@ class Comm:
             raise _lib.NeuroKmerError(_lib.NK_E_DEVICE, _lib.last_error())
         self._h = h
 
+    @classmethod
+    def loopback(cls, group: "LoopbackGroup", rank: int, device: int = 0) -> "Comm":
+        """Rank `rank` of an in-process loopback group (nk_comm_new_loopback):
+        the ranks are host threads of this process on one device, the
+        collectives device copies between host barriers.  A rehearsal of the
+        multi-rank finish on one GPU, where RCCL refuses two ranks."""
+        from . import _lib
+        self = cls.__new__(cls)
+        self._L = _lib.load()
+        self._h = None
+        self.world, self.rank, self.device = group.world, rank, device
+        h = self._L.nk_comm_new_loopback(group._h, rank, device)
+        if not h:
+            raise _lib.NeuroKmerError(_lib.NK_E_INVALID, _lib.last_error())
+        self._h = h
+        return self
+
+    def forget(self, ctr) -> None:
+        """Free the device buffers this communicator holds for `ctr`
+        (nk_comm_forget); call before closing a handle the comm outlives."""
+        if self._h and getattr(ctr, "_h", None):
+            self._L.nk_comm_forget(self._h, ctr._h)
+
     def close(self):
         if self._h:
             self._L.nk_comm_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class LoopbackGroup:
+    """A loopback transport group of `world` ranks (nk_loop_group_new): each
+    rank is a host thread of this process with its own Comm.loopback(...).
+    Free it after every member Comm is closed."""
+
+    def __init__(self, world: int):
+        from . import _lib
+        self._L = _lib.load()
+        self.world = world
+        self._h = self._L.nk_loop_group_new(world)
+        if not self._h:
+            raise _lib.NeuroKmerError(_lib.NK_E_INVALID, _lib.last_error())
+
+    def close(self):
+        if self._h:
+            self._L.nk_loop_group_free(self._h)
             self._h = None
 
     def __del__(self):

@@ -1,0 +1,193 @@
+"""The library's multi-rank finish (nk_finalize_dist / nk_finalize_sliced_dist)
+at world 2..4 on ONE GPU, through the loopback transport (nk_loop_group_new,
+nk_comm_new_loopback): every rank is a host thread of this process with its
+own handle, stream and communicator, the collectives real exchanges between
+the ranks' buffers.  RCCL refuses two ranks on one device, so before this the
+in-library finish had run only in 1-rank groups, where every collective is the
+identity (the merge-set emptying keyed on the world size, the top
+k-mer union exchange and its redo, the reduce-scatter's slice padding were
+unchecked past one rank).
+
+Each case shards the records over the ranks, runs the N-rank steps, and
+compares every rank's finished state bit-exactly with one handle counting all
+the records (and, for the plain finish, with oracle/nk_oracle.c).
+
+Reference: src/spiking_hash.rs:84-201 (process_parallel: the rayon reduce of
+per-record currents the all-reduce replaces), :661-673 (top rows).
+"""
+import threading
+import traceback
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+
+def _input(total, seed, recs):
+    from neurokmer_amd import synth
+    return synth.make_records(total, recs, seed=seed, repeats_per_mb=20_000, motif_len=90,
+                              n_rate=0.002, mixed_case=True)
+
+
+def _shards(bases, offs, world):
+    """Records dealt round-robin to the ranks: (host bases, offsets) per rank."""
+    out = []
+    for r in range(world):
+        idx = list(range(r, offs.size - 1, world))
+        parts = [bases[int(offs[i]):int(offs[i + 1])] for i in idx]
+        b = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+        o = np.zeros(len(parts) + 1, np.uint64)
+        np.cumsum([p.size for p in parts], out=o[1:])
+        out.append((b, o))
+    return out
+
+
+def _run_ranks(world, body):
+    """body(rank, comm) on `world` threads sharing one loopback group."""
+    from neurokmer_amd import dist as nkdist
+    grp = nkdist.LoopbackGroup(world)
+    comms = [nkdist.Comm.loopback(grp, r, 0) for r in range(world)]
+    errs = [None] * world
+    out = [None] * world
+
+    def run(r):
+        try:
+            torch.cuda.set_device(0)
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                out[r] = body(r, comms[r])
+            st.synchronize()
+        except Exception:
+            errs[r] = traceback.format_exc()
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=240)
+    alive = any(t.is_alive() for t in ts)
+    if not alive:
+        for c in comms:
+            c.close()
+        grp.close()
+    assert not alive, "a rank thread did not finish"
+    for e in errs:
+        assert e is None, e
+    return out
+
+
+def _dev(b, o):
+    d_b = torch.from_numpy(np.concatenate([b, np.zeros(16, np.uint8)])).cuda()
+    d_o = torch.from_numpy(o.view(np.int64)).cuda()
+    return d_b, d_o
+
+
+def _state(c):
+    return {"currents": c.currents(), "spike_counts": c.spike_counts(),
+            "voltages": c.voltages().view(np.uint32), "refractory": c.refractory(),
+            "total_spikes": c.energy.total_spikes(), "energy_used": c.energy_used(),
+            "top": c.top_abundant_neurons(20)}
+
+
+def _assert_same(a, b, lo=0, hi=None):
+    for name in ("currents", "spike_counts", "voltages", "refractory"):
+        np.testing.assert_array_equal(a[name][lo:hi], b[name][lo:hi], err_msg=name)
+    assert a["total_spikes"] == b["total_spikes"]
+    assert a["energy_used"] == b["energy_used"]
+    assert a["top"] == b["top"]
+
+
+@pytest.mark.parametrize("world,wire,cap", [(2, "u32", 4096), (3, "u64", 4096), (4, "u32", 4),
+                                            (2, "u64", 1)])
+def test_loopback_finalize_dist(world, wire, cap):
+    """nk_finalize_dist: u32 / u64 wire all-reduce, export + all-gather + merge;
+    cap 4 and 1 overflow the export segments, so the redo and the two-pass
+    top k-mer union exchange run too."""
+    from neurokmer_amd import SpikingKmerCounter
+    from neurokmer_amd import dist as nkdist
+    from oracle import cbind
+    k, pool = 31, 2_000_000
+    bases, offs = _input(1_200_000, 71 + world, 9)
+    shards = _shards(bases, offs, world)
+    tk = int(offs[-1]) if wire == "u32" else None
+    steps = 2
+
+    def body(r, comm):
+        b, o = shards[r]
+        d_b, d_o = _dev(b, o)
+        c = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, True)
+        for _ in range(steps):  # state carries over between steps
+            c.accumulate_device(d_b.data_ptr(), d_o.data_ptr(), o.size - 1, b.size)
+            nkdist.finalize_step(c, total_kmers=tk, cap=cap, comm=comm)
+        torch.cuda.current_stream().synchronize()
+        st = _state(c)
+        comm.forget(c)
+        c.close()
+        return st
+
+    got = _run_ranks(world, body)
+    ref = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, True)
+    for _ in range(steps):
+        ref.process_parallel_arrays(bases, offs, 4)
+    want = {"currents": ref.currents(), "spike_counts": ref.spike_counts(),
+            "voltages": ref.voltages().view(np.uint32), "refractory": ref.refractory(),
+            "total_spikes": ref.total_spikes, "energy_used": ref.energy_used(),
+            "top": ref.top_abundant_neurons(20)}
+    for r in range(world):
+        _assert_same(got[r], want)
+
+
+@pytest.mark.parametrize("world,width", [(2, 64), (3, 128), (4, 64)])
+def test_loopback_finalize_sliced_dist(world, width):
+    """nk_finalize_sliced_dist: reduce-scatter of a zero-padded wire (a pool
+    not divisible by the world), LIF of each rank's slice, all-gather of the
+    slices' top rows, union of the shards' top k-mers."""
+    from neurokmer_amd import SpikingKmerCounter
+    from neurokmer_amd import dist as nkdist
+    k, pool = 63, (1 << 22) + 5
+    bases, offs = _input(900_000, 81 + world, 7)
+    shards = _shards(bases, offs, world)
+    tk = int(offs[-1]) if width == 64 else None
+
+    def body(r, comm):
+        b, o = shards[r]
+        d_b, d_o = _dev(b, o)
+        c = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, True, kmer_width=width)
+        for _ in range(2):
+            c.accumulate_device(d_b.data_ptr(), d_o.data_ptr(), o.size - 1, b.size)
+            nkdist.finalize_step_sliced(c, total_kmers=tk, comm=comm)
+        torch.cuda.current_stream().synchronize()
+        st = _state(c)
+        comm.forget(c)
+        c.close()
+        return st
+
+    got = _run_ranks(world, body)
+    one = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, True, kmer_width=width)
+    for _ in range(2):
+        one.process_parallel_arrays(bases, offs)
+    want = _state(one)
+    one.close()
+    for r in range(world):
+        lo, hi, _ = nkdist.slice_bounds(pool, world, r)
+        _assert_same(got[r], want, lo, hi)  # each rank owns its slice of the pool
+
+
+def test_loopback_group_errors():
+    """A bad world or rank fails loudly; a group whose ranks never all arrive
+    is not exercised here (its 120 s timeout is the guard)."""
+    from neurokmer_amd import dist as nkdist
+    from neurokmer_amd._lib import NeuroKmerError
+    with pytest.raises(NeuroKmerError):
+        nkdist.LoopbackGroup(0)
+    with pytest.raises(NeuroKmerError):
+        nkdist.LoopbackGroup(17)
+    g = nkdist.LoopbackGroup(2)
+    with pytest.raises(NeuroKmerError):
+        nkdist.Comm.loopback(g, 2, 0)
+    g.close()

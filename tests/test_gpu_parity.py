@@ -519,13 +519,37 @@ def test_full_size_properties(shape):
         h.accumulate_device(sub.data_ptr(), so.data_ptr(), 1, hi - lo)
         acc += h.currents()
     np.testing.assert_array_equal(acc, cur1)
-    # bit-exact vs the oracle on a 2 Mbase prefix of every record
+    # bit-exact vs the oracle on 2.1 Mbases: the first 300 kbases of each record
+    # (the whole input is compared in test_config2_full_parity)
     per = 300_000
     segs = [bases[int(offs[i]):int(offs[i]) + per] for i in range(7)]
     po = np.arange(8, dtype=np.uint64) * per
     pb = np.concatenate(segs)
     gg, rr = run_both(pb, po, 31, 2_000_000, True)
     assert_same(gg, rr)
+
+
+def test_config2_full_parity():
+    """BASELINE.json configs[1] at its full size: 115,000,000 bases in 7
+    records, k=31, pool=2M, canonical.  The GPU's process_parallel over the
+    whole input against oracle/nk_oracle.c's process_parallel restatement
+    (one thread per record like rayon, src/spiking_hash.rs:84-201), every
+    output bit-exact: currents, spike counts, voltages (bitwise), refractory,
+    total spikes, energy, top-20 rows with their uniques.  The same input
+    bench.py times (synth seed, 64 x 200-bp planted repeats per MB)."""
+    bases, offs = synth.make_records(115_000_000, 7, repeats_per_mb=64, motif_len=200)
+    d_b = torch.from_numpy(np.concatenate([bases, np.zeros(16, np.uint8)])).cuda()
+    d_o = torch.from_numpy(offs.view(np.int64)).cuda()
+    torch.cuda.synchronize()
+    g = SpikingKmerCounter(31, 1.0, 0.95, 2, 1.0, 2_000_000, True)
+    g.process_parallel_device(d_b.data_ptr(), d_o.data_ptr(), 7, bases.size)
+    del d_b
+    r = cbind.OracleCounter(31, 1.0, 0.95, 2, 1.0, 2_000_000, True)
+    r.process_parallel_arrays(bases, offs, 7)
+    assert_same(g, r)
+    nk = int(np.clip(np.diff(offs.astype(np.int64)) - 30, 0, None).sum())
+    assert int(g.currents().sum()) == nk == 114_999_790
+    g.close()
 
 
 # ---- exact k-mer table (SURVEY.md §8f-1) and process_sequence (§8f-3) --------
