@@ -792,7 +792,7 @@ static int build_sorted(nk_counter *c, const KmerInput &in0, hipStream_t s) {
   return NK_OK;
 }
 
-static uint64_t count_chunk(uint64_t n_bases = 0, uint64_t pool = 0);
+static uint64_t count_chunk(uint64_t n_bases = 0, uint64_t pool = 0, bool wide = false);
 static uint32_t env_u32(const char *name, uint32_t dflt);
 
 // neurons per K1a<KEYS> bucket (log2): kXMinBinBits; NK_XBIN_BITS (A/B,
@@ -1018,20 +1018,22 @@ static bool atomic_forced() {
 #ifndef NK_COUNT_CHUNK_DEFAULT
 #define NK_COUNT_CHUNK_DEFAULT (1ull << 31)
 #endif
-constexpr uint64_t kKeepBytesPerBase = 10;  // arena bytes per position, upper bound (wide path + slack)
-constexpr double kKeepFrac = 0.45;
+constexpr double kKeepFrac = 0.6;
 // (pool: a bucket region of one launch stays below 2^31 records, so K1b's u32
 // bins and partials cannot wrap whatever the input)
-static uint64_t count_chunk(uint64_t n_bases, uint64_t pool) {
+static uint64_t count_chunk(uint64_t n_bases, uint64_t pool, bool wide) {
   const char *e = getenv("NK_COUNT_CHUNK");
   uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
   if (!v) {
     v = NK_COUNT_CHUNK_DEFAULT;
     const uint64_t B = std::max<uint64_t>(1, (pool + kBinsPerBucket - 1) >> kBinBits);
+    // arena bytes per position: Part u16 offset + u16 position; Gen/Wide u32
+    // coarse + u16 fine records; x1.25 region slack, + segment descriptors
+    const double per = (wide || B > (uint64_t)kMaxBuckets) ? 8.5 : 5.5;
     size_t fr = 0, tot = 0;
     if (n_bases > v && pool && n_bases / B * 5 / 4 < (1ull << 31) - (1ull << 24) &&
         !getenv("NK_COUNT_BATCHED") && hipMemGetInfo(&fr, &tot) == hipSuccess &&
-        (double)n_bases * kKeepBytesPerBase <= kKeepFrac * (double)fr)
+        (double)n_bases * per <= kKeepFrac * (double)fr)
       v = (n_bases + kPartTile - 1) / kPartTile * kPartTile;
   }
   return std::max<uint64_t>(kPartTile, v / kPartTile * kPartTile);
@@ -1216,13 +1218,22 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
   // bucket regions: 1.25x the fair share + one tile of slack (overflow is
   // still exact: the excess is counted with direct atomics); past
   // count_chunk() positions the regions hold one batch at a time
-  const uint64_t chunk = count_chunk(n_bases, c->pool);
-  const uint64_t est = std::min<uint64_t>(n_bases, chunk);
+  uint64_t chunk = count_chunk(n_bases, c->pool, c->w128 || c->k > 32);
+  uint64_t est = std::min<uint64_t>(n_bases, chunk);
   // the exact table grouped by neuron from this count's own records (K1a also
   // writes each record's key, nk_table.hip), in 4096-neuron buckets
   const bool want_keyed = c->opts.exact_counts && grouped_ok(c, n_bases);
   int rc = plan_count(c, est, kPartTile, n_tiles_for(est, kPartTile), cp, z,
                      /*keep_gen=*/n_bases <= chunk, want_keyed ? xbin_bits() : 0);
+  if (rc == NK_E_OOM && chunk > count_chunk()) {
+    // the one-launch arena did not fit after all (other handles took the
+    // memory since the estimate): count in batches instead
+    z = ZeroList{};
+    chunk = count_chunk();
+    est = std::min<uint64_t>(n_bases, chunk);
+    rc = plan_count(c, est, kPartTile, n_tiles_for(est, kPartTile), cp, z, n_bases <= chunk,
+                    want_keyed ? xbin_bits() : 0);
+  }
   if (rc) return rc;
   in.n_tiles = n_tiles_for(n_bases, cp.tile);
   const bool batched = cp.path != CountPath::Atomic && n_bases > chunk;
@@ -2119,16 +2130,24 @@ int nk_top_kmers_padded(nk_counter *c, uint64_t *d_out, size_t cap, void *stream
     HIPCHK(hipMemsetAsync(d_out, 0, 8, s));
     return NK_OK;
   }
-  int rc;
-  if ((rc = c->top_keys.ensure(c->w128 ? 2 * c->set_cap : c->set_cap + 1))) return rc;
-  HIPCHK(hipMemsetAsync(c->top_keys_n.p, 0, 8, s));
-  if (c->w128)
-    HIPCHK(launch_set_compact128(c->set_keys.p, c->set_cap, c->top_keys.p, c->top_keys_n.p, s));
-  else
-    HIPCHK(launch_set_compact(c->set_keys.p, c->set_cap, c->special.p, m, c->cand.p, c->pool,
-                              c->top_keys.p, c->top_keys_n.p, s));
+  // Compact this shard's keys once per finish: a later exchange (the second,
+  // exact-size pass of the union) must re-pad the SAME list -- the merge of a
+  // truncated first pass has by then refilled the set with the union
+  // (nk_merge_top_kmers_padded merges into it), so a second compaction would
+  // export the truncated union instead of this shard's keys (found by the
+  // world-4 loopback run, tests/test_gpu_loopback.py).
+  if (!c->top_keys_ready) {
+    int rc;
+    if ((rc = c->top_keys.ensure(c->w128 ? 2 * c->set_cap : c->set_cap + 1))) return rc;
+    HIPCHK(hipMemsetAsync(c->top_keys_n.p, 0, 8, s));
+    if (c->w128)
+      HIPCHK(launch_set_compact128(c->set_keys.p, c->set_cap, c->top_keys.p, c->top_keys_n.p, s));
+    else
+      HIPCHK(launch_set_compact(c->set_keys.p, c->set_cap, c->special.p, m, c->cand.p, c->pool,
+                                c->top_keys.p, c->top_keys_n.p, s));
+    c->top_keys_ready = true;  // kept for the variable-length fallback (nk_top_kmers)
+  }
   HIPCHK(launch_pad_keys(c->top_keys.p, c->top_keys_n.p, cap, c->w128 ? 2 : 1, d_out, s));
-  c->top_keys_ready = true;  // kept for the variable-length fallback (nk_top_kmers)
   return NK_OK;
 }
 
@@ -2591,7 +2610,7 @@ static int acc_begin(nk_counter *c, uint64_t est_bases, uint64_t batch_bases, St
   z.ptr[z.n] = c->cur.p; z.bytes[z.n++] = c->pool * 8;
   const uint64_t B = (c->pool + kBinsPerBucket - 1) >> kBinBits;
   const bool part_like = !c->w128 && c->k <= 32 && B <= (uint64_t)kMaxBuckets &&
-                         !wide_bits_forced() && est_bases <= count_chunk(est_bases, c->pool);
+                         !wide_bits_forced() && est_bases <= count_chunk(est_bases, c->pool, c->w128 || c->k > 32);
   const uint64_t est = part_like ? est_bases : std::min(est_bases, batch_bases);
   // segments per bucket: one per tile per launch; chunk-straddling tiles add a few
   const uint64_t max_segs = n_tiles_for(std::max<uint64_t>(est, 1), kPartTile) + 4096;
