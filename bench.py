@@ -355,21 +355,11 @@ def main() -> int:
     # All handles count on ONE stream: one hardware queue, so the counts queue
     # back to back and the count queue never idles while a finish is awaited
     # (the library orders each handle's finish on the end of its own count).
-    # A stream per handle measured slower with 3 in flight: the third count's
-    # queue was not served until the finish queue went idle (0.529-0.537 vs
-    # 0.507-0.514 ms, profiles/r02_s31; NK_BENCH_COUNT_STREAM_PER_HANDLE=1).
-    # NK_BENCH_COUNT_STREAMS=2 (A/B): handles alternate between two count
-    # streams, so one batch's K1a may start while the previous batch's K1b
-    # runs: measured slower (0.5166 vs 0.5026 ms, five interleaved pairs,
-    # profiles/r03_cs2), not the default.
-    n_cs = int(os.environ.get("NK_BENCH_COUNT_STREAMS", "1"))
-    if os.environ.get("NK_BENCH_COUNT_STREAM_PER_HANDLE") == "1":
-        count_streams = [torch.cuda.Stream(device=dev) for _ in range(args.inflight)]
-    elif n_cs > 1:
-        pool_cs = [torch.cuda.Stream(device=dev) for _ in range(n_cs)]
-        count_streams = [pool_cs[j % n_cs] for j in range(args.inflight)]
-    else:
-        count_streams = [torch.cuda.Stream(device=dev)] * args.inflight
+    # Measured slower and not kept: a stream per handle with 3 in flight (the
+    # third count's queue was not served until the finish queue went idle,
+    # 0.529-0.537 vs 0.507-0.514 ms, profiles/r02_s31); handles alternating
+    # between two count streams (0.5166 vs 0.5026 ms, profiles/r03_cs2).
+    count_streams = [torch.cuda.Stream(device=dev)] * args.inflight
     run_stream = count_streams[0]
     fin_stream = (torch.cuda.Stream(device=dev, priority=torch.cuda.Stream.priority_range()[1])
                   if args.inflight > 1 else run_stream)
@@ -377,6 +367,7 @@ def main() -> int:
     s_handle = run_stream.cuda_stream
 
     start_host_s = []  # host time of each start() (the enqueue of a count)
+    settle_each = [False]
     # side lines (configs 4/5): hipEvents on the count stream around each
     # step's whole count (a multi-GB input runs several batches per count)
     side = args.workload in ("config4", "config5")
@@ -409,6 +400,8 @@ def main() -> int:
             if between is not None:
                 between()
             c.finalize(False, st.cuda_stream)
+            if settle_each[0]:  # write out v / refractory / spike counts too (nk_settle)
+                c.settle(st.cuda_stream)
             return
         with torch.cuda.stream(st):
             if args.workload == "config5":
@@ -460,9 +453,9 @@ def main() -> int:
             settle = int(t.item())
         run(settle, args.inflight)
         torch.cuda.synchronize()
-    # timed steps record no events at all (stage_timing 3; NK_BENCH_TIMED_LEVEL
-    # for A/B runs); K1a's duration comes from its in-kernel stamps
-    timed_level = int(os.environ.get("NK_BENCH_TIMED_LEVEL", "3"))
+    # timed steps record no events at all (stage_timing 3); K1a's duration
+    # comes from its in-kernel stamps
+    timed_level = 3
     for c in ctrs:
         c.set_stage_timing(timed_level)
     # one more untimed round in the timed mode: the first step after the switch
@@ -512,6 +505,15 @@ def main() -> int:
     # handle 1's steps in the overlapped run (the other batch's finish beside it)
     spans = ctr.count_spans(args.steps)
     spans2 = ctrs[1].count_spans(args.steps // args.inflight) if args.inflight > 1 else []
+    # the same steps writing the per-neuron state out in each (the reference
+    # writes v, refractory and spike counts in every call, src/spiking_hash.rs:
+    # 186-200; the step above leaves them derived from the currents until a
+    # reader asks, nk_settle): what that write costs per step
+    dt_settle = None
+    if not dist_on:
+        settle_each[0] = True
+        _, dt_settle = timed(args.steps, args.inflight, [])
+        settle_each[0] = False
     total_spikes = ctr.energy.total_spikes()
     # cross-check: K1a between hipEvents in 5 extra (untimed) steps
     ctr.set_stage_timing(0)
@@ -574,6 +576,13 @@ def main() -> int:
             "ms_per_step": round(ms_step, 4),
             "inflight": args.inflight,
             "ms_per_step_one_in_flight": round(dt1 / args.steps * 1e3, 4),
+            "ms_per_step_state_written": (round(dt_settle / args.steps * 1e3, 4)
+                                          if dt_settle is not None else None),
+            "state_written_note": ("the same steps (same batches in flight) with nk_settle after "
+                                   "each finish: v, refractory and spike counts written to HBM "
+                                   "as the reference does every call; `value` is the step "
+                                   "without that write (the state is derived on demand, "
+                                   "bit-identical when read)"),
             "inflight_handles_same_results": same_inflight,
             "start_host_ms_median_max": start_ms,
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "u64",

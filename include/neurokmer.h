@@ -359,6 +359,14 @@ int nk_copy_refractory(nk_counter *c, uint32_t *out, size_t n);
  * last call that passed one; after a call on the handle's own stream (NULL)
  * this waits for that stream, so any stream may read it.  NULL on error. */
 uint64_t *nk_device_currents(nk_counter *c);
+/* Write out the per-neuron state (voltages, refractory counters, spike counts)
+ * that the last finish left derived.  A finish from the reset state leaves
+ * them as a function of the currents (nothing reads them in a typical step);
+ * every reader (nk_copy_*, a further process call) writes them out first, so
+ * results never differ.  The reference writes them in every call
+ * (src/spiking_hash.rs:186-200): bench.py times a step plus this call to show
+ * what that costs.  Enqueued on `stream` (NULL: the handle's stream). */
+int nk_settle(nk_counter *c, void *stream);
 /* Resets neurons, currents and energy to the state nk_new() left them in. */
 int nk_reset(nk_counter *c);
 /* Same, enqueued on `stream` (hipStream_t or NULL for the handle's stream)

@@ -47,7 +47,7 @@ EXPORTS = (
     "nk_exact_owner", "nk_exact_partition", "nk_exact_adopt", "nk_device_kmer_per_neuron",
     "nk_set_stage_timing", "nk_diag_hash_ms", "nk_diag_hash_ms_w", "nk_count_spans", "nk_simulate_spikes_auto",
     "nk_comm_unique_id", "nk_comm_new", "nk_comm_free", "nk_finalize_dist", "nk_finalize_sliced_dist",
-    "nk_comm_forget", "nk_loop_group_new", "nk_loop_group_free", "nk_comm_new_loopback",
+    "nk_settle", "nk_comm_forget", "nk_loop_group_new", "nk_loop_group_free", "nk_comm_new_loopback",
     "nk_last_error",
     "nk_version",
 )
@@ -142,6 +142,7 @@ def load(share_torch: bool = True):
         "nk_copy_voltages": (C.c_int, [vp, vp, sz]),
         "nk_copy_refractory": (C.c_int, [vp, vp, sz]),
         "nk_device_currents": (vp, [vp]),
+        "nk_settle": (C.c_int, [vp, vp]),
         "nk_exact_owner": (u32, [u64, u32]),
         "nk_exact_partition": (C.c_int, [vp, u32, P(u64), P(vp), P(vp), vp]),
         "nk_exact_adopt": (C.c_int, [vp, vp, vp, sz, vp]),

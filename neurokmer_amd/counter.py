@@ -195,6 +195,10 @@ class SpikingKmerCounter:
     def finalize_redo(self, stream: int = 0) -> None:
         check(self._L.nk_finalize_redo(self._h, stream or None))
 
+    def settle(self, stream: int = 0) -> None:
+        """Write out the derived per-neuron state (nk_settle)."""
+        check(self._L.nk_settle(self._h, stream))
+
     def device_currents_ptr(self) -> int:
         return self._L.nk_device_currents(self._h) or 0
 

@@ -3082,6 +3082,13 @@ uint64_t nk_get_steps(const nk_counter *c) { return c ? c->steps : 0; }
 size_t nk_pool_size(const nk_counter *c) { return c ? c->pool : 0; }
 size_t nk_k(const nk_counter *c) { return c ? c->k : 0; }
 int nk_use_canonical(const nk_counter *c) { return c ? c->canonical : 0; }
+int nk_settle(nk_counter *c, void *stream) {
+  if (!c) return fail(NK_E_INVALID, "null counter");
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  return settle_state(c, s);
+}
+
 uint64_t *nk_device_currents(nk_counter *c) {
   if (!c) return nullptr;
   if (c->cur_in_wire) {

@@ -4,18 +4,21 @@
 // every process call (src/spiking_hash.rs:157-172).  Equal keys hash to the
 // same neuron, so the table is built from the count's own partition instead of
 // a global sort of every key:
-//   K1a<KEYS>  (nk_kernels.hip) each record of a bucket region (32768 neurons)
-//              carries its key beside its bin offset;
+//   K1a<KEYS>  (nk_kernels.hip) each record of a bucket region (2^13 neurons,
+//              kXMinBinBits; NK_XBIN_BITS 14/15 for tests) carries its key
+//              beside its bin offset;
 //   k_xcount   per (bucket, slice of kXSlice records): records per group of
-//              128 neurons (LDS histogram), one row per slice;
+//              2^ggbits neurons (32 at config 2) in an LDS histogram, one row
+//              per slice;
 //   k_xscan    per bucket: the rows -> the offset of every (slice, group) in
 //              group-major order, and each group's start;
 //   k_xbase    the buckets' table bases (their records before them);
-//   k_xscatter per (bucket, slice): 4096-record sub-tiles counting-sorted by
-//              group in LDS, then written as contiguous runs (one radix pass of
-//              at most 256 digits: a slice's run of a group is one stretch);
-//   k_xgroup   per group of 128 neurons, 2^gbits neurons per pass (the group's
-//              records re-read from L2): an LDS hash table (key -> u32 count,
+//   k_xscatter per (bucket, slice), one workgroup per CU, XCD-aware order:
+//              8192-record sub-tiles counting-sorted by group in LDS, then
+//              written as contiguous runs (one radix pass of at most 256
+//              digits: a slice's run of a group is one stretch);
+//   k_xgroup   per group, 2^gbits neurons per pass (the group's records re-read
+//              from L2): an LDS hash table of 4096 slots (key -> u32 count,
 //              wrapping like the reference's AtomicU32), distinct keys per
 //              neuron = kmer_per_neuron, entries written neuron by neuron
 //              (ent[n] = start | len << 40) into the group's own range (its
@@ -26,6 +29,8 @@
 // sorts that list (rocPRIM) and appends its run-length encoding as a key-sorted
 // part (ent = kSideEnt for those neurons).  get_count scans the neuron's
 // entries (grouped) or binary-searches the side part.
+// (Measured and not kept, profiles/r03_*: 2048-slot tables, 4096-record
+// sub-tiles, three scatter workgroups per CU, the plain workgroup order.)
 #include <stdlib.h>
 
 #include "nk_device.h"
@@ -143,22 +148,18 @@ __global__ __launch_bounds__(512) void k_xbase(XGroupArgs t) {
 // XCD-aware order: workgroups are placed on the 8 XCDs round-robin by their
 // linear index, so linear index L runs on XCD L % 8; bucket b's slices all go
 // to XCD b % 8, one after another, so the adjacent pieces of a group's runs
-// that consecutive slices write meet in one L2 (NK_XS_XCD=0: plain order)
-template <int kSub>  // records per LDS sub-tile
-__global__ __launch_bounds__(kXsBlock) void k_xscatter(XGroupArgs t, int xcd_order) {
+// that consecutive slices write meet in one L2
+constexpr int kSub = 8192;  // records per LDS sub-tile
+__global__ __launch_bounds__(kXsBlock) void k_xscatter(XGroupArgs t) {
   constexpr int kSubPer = kSub / kXsBlock;  // per thread
   __shared__ unsigned long long s_key[kSub];
   __shared__ uint8_t s_bin[kSub], s_grp[kSub];
   __shared__ uint32_t cnt[kXMaxGroups], st[kXMaxGroups], gcur[kXMaxGroups], s_w[4];
   __shared__ unsigned long long s_at;
   __shared__ uint32_t s_n;
-  uint32_t sl = blockIdx.x, b = blockIdx.y;
-  if (xcd_order) {
-    const uint32_t L = blockIdx.x, x = L & 7u, kk = L >> 3;
-    b = x + 8u * (kk / t.n_slices);
-    sl = kk % t.n_slices;
-    if (b >= t.n_buckets) return;
-  }
+  const uint32_t L = blockIdx.x, x = L & 7u, kk = L >> 3;
+  const uint32_t b = x + 8u * (kk / t.n_slices), sl = kk % t.n_slices;
+  if (b >= t.n_buckets) return;
   const uint32_t NG = t.n_groups, tid = threadIdx.x;
   const uint64_t fill = region_fill(t, b);
   const uint64_t r0 = (uint64_t)sl * kXSlice;
@@ -307,11 +308,9 @@ __device__ __forceinline__ void xg_load(const uint64_t *kp, const uint8_t *bp, u
   }
 }
 
-// HB: log2 of the LDS table's slots (12: 48 KB, three workgroups per CU; 11:
-// 24 KB, six, with half the neurons per pass)
-template <int HB, int WPE>
-__global__ __launch_bounds__(kXsBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void k_xgroup(XGroupArgs t) {
-  constexpr int kHashBits = HB, kHashSlots = 1 << HB, kSlotsPer = kHashSlots / kXsBlock;
+// 4096-slot LDS table (48 KB with its counts): three workgroups per CU
+__global__ __launch_bounds__(kXsBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_xgroup(XGroupArgs t) {
+  constexpr int kHashBits = 12, kHashSlots = 1 << kHashBits, kSlotsPer = kHashSlots / kXsBlock;
   constexpr uint32_t kHashMax = kHashSlots * 5 / 8;
   __shared__ unsigned long long hk[kHashSlots];
   __shared__ uint32_t hc[kHashSlots];
@@ -488,15 +487,7 @@ __global__ __launch_bounds__(256) void k_xfinish(XGroupArgs t, unsigned long lon
 
 }  // namespace
 
-static int env_int(const char *name, int dflt) {
-  const char *e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-
-uint32_t xgroup_hash_bits() {
-  static const int hb = env_int("NK_XG_HB", 12) == 11 ? 11 : 12;  // A/B: 11 = 2048-slot tables
-  return (uint32_t)hb;
-}
+uint32_t xgroup_hash_bits() { return 12; }
 
 uint32_t xgroup_bits(uint64_t n_records, uint64_t pool) {
   // about (table slots) / 2 distinct keys per pass at most (a neuron's records
@@ -528,23 +519,10 @@ hipError_t xgroup_build(const XGroupArgs &t, hipStream_t s) {
   // XCD's L2 with them (exact step 2.97-2.99 ms with 3 per CU, 2.98-3.06 with
   // 2, 2.92-2.94 with 1 -- 80 KB of unused dynamic LDS --, profiles/r03_xspad);
   // the LDS one workgroup per CU may use holds 8192-record sub-tiles, runs
-  // twice as long (2.92-2.94 vs 2.94-2.95 ms, profiles/r03_xssub).  A/B:
-  // NK_XS_SUB=4096 (+ NK_XS_LDS_PAD bytes of padding; 0: three per CU).
-  static const int xcd = env_int("NK_XS_XCD", 1), xs_sub = env_int("NK_XS_SUB", 8192),
-                   xs_pad = env_int("NK_XS_LDS_PAD", xs_sub == 8192 ? 0 : 80000);
-  const dim3 gx = xcd ? dim3(8u * ((t.n_buckets + 7u) / 8u) * t.n_slices) : gs;
-  if (xs_sub == 8192)
-    hipLaunchKernelGGL(k_xscatter<8192>, gx, dim3(kXsBlock), (unsigned)xs_pad, s, t, xcd);
-  else
-    hipLaunchKernelGGL(k_xscatter<4096>, gx, dim3(kXsBlock), (unsigned)xs_pad, s, t, xcd);
-  static const int wpe = env_int("NK_XG_WPE", 4);  // 2048-slot tables: waves per SIMD (A/B: 4 or 5)
-  const dim3 gg(t.n_groups, t.n_buckets);
-  if (t.hash_bits == 11 && wpe == 5)
-    hipLaunchKernelGGL((k_xgroup<11, 5>), gg, dim3(kXsBlock), 0, s, t);
-  else if (t.hash_bits == 11)
-    hipLaunchKernelGGL((k_xgroup<11, 4>), gg, dim3(kXsBlock), 0, s, t);
-  else
-    hipLaunchKernelGGL((k_xgroup<12, 3>), gg, dim3(kXsBlock), 0, s, t);
+  // twice as long (2.92-2.94 vs 2.94-2.95 ms, profiles/r03_xssub)
+  hipLaunchKernelGGL(k_xscatter, dim3(8u * ((t.n_buckets + 7u) / 8u) * t.n_slices), dim3(kXsBlock),
+                     0, s, t);
+  hipLaunchKernelGGL(k_xgroup, dim3(t.n_groups, t.n_buckets), dim3(kXsBlock), 0, s, t);
   return hipGetLastError();
 }
 
