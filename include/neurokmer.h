@@ -186,6 +186,25 @@ int nk_finalize_slice(nk_counter *c, int streaming_semantics, const void *d_slic
                       size_t lo, size_t hi, uint64_t *d_seg, size_t seg_rows, void *stream);
 int nk_adopt_slices(nk_counter *c, const uint64_t *d_all, size_t world, size_t stride,
                     void *stream);
+/* The same pool-sliced finish with no host wait until nk_merge_export (u32
+ * slices; world * top_n <= 2048):
+ *   nk_slice_export  LIF of [lo, hi) from the reduce-scattered u32 slice and
+ *                    the slice's top rows into d_seg (3 + 3*seg_rows words),
+ *                    by kernels;
+ *   <all-gather of the d_seg segments>
+ *   nk_adopt_export  the global rows picked on the device from the gathered
+ *                    segments, this shard's uniques pass for them, its new
+ *                    keys appended to d_keyseg (1 + key_words*cap words, the
+ *                    layout of nk_finalize_export);
+ *   <all-gather of the key segments>
+ *   nk_merge_export  as after nk_finalize_export; on *redo = 1 the blocking
+ *                    path follows (a slice's spike counts past 4095 need the
+ *                    exact refine; the set or a bucket overflowed; a segment
+ *                    was truncated).  nk_finalize_sliced_dist runs all of it. */
+int nk_slice_export(nk_counter *c, int streaming_semantics, const uint32_t *d_slice, size_t lo,
+                    size_t hi, uint64_t *d_seg, size_t seg_rows, void *stream);
+int nk_adopt_export(nk_counter *c, const uint64_t *d_all, size_t world, size_t stride,
+                    uint64_t *d_keyseg, size_t cap, void *stream);
 /* ---- multi-GPU step with the collectives inside the library ---------------
  * One communicator per rank (RCCL over xGMI; one process per GPU): rank 0
  * makes an id, the caller broadcasts it (e.g. torch.distributed), every rank

@@ -40,7 +40,7 @@ EXPORTS = (
     "nk_copy_refractory", "nk_device_currents", "nk_reset", "nk_reset_async", "nk_last_timings",
     "nk_count_history", "nk_wire32", "nk_finalize_export", "nk_merge_export", "nk_finalize_redo",
     "nk_top_kmers_padded", "nk_merge_top_kmers_padded",
-    "nk_finalize_slice", "nk_adopt_slices", "nk_accumulate_device_from",
+    "nk_finalize_slice", "nk_adopt_slices", "nk_slice_export", "nk_adopt_export", "nk_accumulate_device_from",
     "nk_willshaw_new", "nk_willshaw_free", "nk_willshaw_store", "nk_willshaw_recall",
     "nk_willshaw_stored", "nk_assoc_new", "nk_assoc_free", "nk_assoc_pattern_size",
     "nk_assoc_store_kmers", "nk_assoc_find_similar",
@@ -118,6 +118,8 @@ def load(share_torch: bool = True):
         "nk_assoc_find_similar": (C.c_long, [vp, u64, sz, vp, vp, sz]),
         "nk_finalize_slice": (C.c_int, [vp, C.c_int, vp, C.c_int, sz, sz, vp, sz, vp]),
         "nk_adopt_slices": (C.c_int, [vp, vp, sz, sz, vp]),
+        "nk_slice_export": (C.c_int, [vp, C.c_int, vp, sz, sz, vp, sz, vp]),
+        "nk_adopt_export": (C.c_int, [vp, vp, sz, sz, vp, sz, vp]),
         "nk_accumulate_device_from": (C.c_int, [vp, vp, vp, sz, sz, sz, vp]),
         "nk_top_kmers": (C.c_int, [vp, P(vp), P(sz)]),
         "nk_merge_top_kmers": (C.c_int, [vp, vp, sz, vp]),

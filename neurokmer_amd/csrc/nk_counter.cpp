@@ -2333,47 +2333,51 @@ int nk_finalize_redo(nk_counter *c, void *stream) {
 // ---------------------------------------------------------------------------
 static constexpr size_t kSliceHdr = 3;  // [rows, new spikes, max spike count]
 
-int nk_finalize_slice(nk_counter *c, int streaming, const void *d_slice, int slice_bits,
-                      size_t lo, size_t hi, uint64_t *d_seg, size_t seg_rows, void *stream) {
-  if (!c || !d_seg) return fail(NK_E_INVALID, "null argument");
+// run_lif = false: the slice's LIF already ran (nk_slice_export); only the
+// selection is redone, blocking, exact (a redo of the device-side finish)
+static int finalize_slice_impl(nk_counter *c, int streaming, const void *d_slice, int slice_bits,
+                               size_t lo, size_t hi, uint64_t *d_seg, size_t seg_rows,
+                               hipStream_t s, bool run_lif) {
   if (lo > hi || hi > c->pool) return fail(NK_E_INVALID, "slice [%zu, %zu) outside the pool", lo, hi);
-  if (slice_bits != 32 && slice_bits != 64) return fail(NK_E_INVALID, "slice_bits must be 32 or 64");
-  if (hi > lo && !d_slice) return fail(NK_E_INVALID, "null slice");
-  c->k1b_lif = false;  // the slice's LIF runs on the reduced slice
+  if (run_lif && slice_bits != 32 && slice_bits != 64)
+    return fail(NK_E_INVALID, "slice_bits must be 32 or 64");
+  if (run_lif && hi > lo && !d_slice) return fail(NK_E_INVALID, "null slice");
   const uint64_t want = std::min<uint64_t>(c->opts.top_n, c->pool);
   if (seg_rows < want) return fail(NK_E_INVALID, "seg_rows (%zu) < top_n rows (%llu)", seg_rows,
                                    (unsigned long long)want);
-  (void)hipSetDevice(c->device);
-  hipStream_t s = pick_stream(c, stream);
   HIPCHK(mark(c, 7, s));
   const uint64_t n = hi - lo;
   const uint64_t m = std::min<uint64_t>(want, n);
-  LifParams lp;
-  int rc = settle_state(c, s);
-  if (rc || (rc = lif_prepare(c, streaming, lp, s))) return rc;
-  // the reduced slice replaces this shard's currents and pending partials
-  c->pend_slices = 0;
-  c->cur_in_wire = false;
-  c->cur_fresh = false;
+  int rc;
+  if (run_lif) {
+    c->k1b_lif = false;  // the slice's LIF runs on the reduced slice
+    LifParams lp;
+    rc = settle_state(c, s);
+    if (rc || (rc = lif_prepare(c, streaming, lp, s))) return rc;
+    // the reduced slice replaces this shard's currents and pending partials
+    c->pend_slices = 0;
+    c->cur_in_wire = false;
+    c->cur_fresh = false;
+    if ((rc = c->sc8.ensure(c->pool))) return rc;
+    if (n) {
+      if (slice_bits == 64)
+        HIPCHK(hipMemcpyAsync(c->cur.p + lo, d_slice, n * 8, hipMemcpyDeviceToDevice, s));
+      const bool w32 = slice_bits == 32;
+      HIPCHK(launch_lif_apply(c->cur.p + lo, w32 ? (const uint32_t *)d_slice : nullptr, w32 ? 1u : 0u,
+                              w32 ? 1 : 0, nullptr, (int)c->last_pa.bin_bits, c->state_fresh ? 1 : 0,
+                              /*derive=*/1, c->v.p + lo, c->r.p + lo, c->sc.p + lo, n, lp, c->lif_tbl.p,
+                              kLifTable, c->hist.p, c->stats.p, TopFuse{}, s, c->sc8.p + lo));
+    }
+    c->sc8_ok = true;  // on [lo, hi), the only range this rank's passes read
+    if (c->state_fresh) {  // derived on [lo, hi) (the rest of the pool is not this rank's)
+      c->state_derived = true;
+      c->derived_lp = lp;
+    }
+    c->state_fresh = false;
+    c->sliced = true;  // only [lo, hi) of v / r / spike counts / currents is this rank's now
+  }
   c->top_valid = false;
   c->top_keys_ready = false;
-  if ((rc = c->sc8.ensure(c->pool))) return rc;
-  if (n) {
-    if (slice_bits == 64)
-      HIPCHK(hipMemcpyAsync(c->cur.p + lo, d_slice, n * 8, hipMemcpyDeviceToDevice, s));
-    const bool w32 = slice_bits == 32;
-    HIPCHK(launch_lif_apply(c->cur.p + lo, w32 ? (const uint32_t *)d_slice : nullptr, w32 ? 1u : 0u,
-                            w32 ? 1 : 0, nullptr, (int)c->last_pa.bin_bits, c->state_fresh ? 1 : 0,
-                            /*derive=*/1, c->v.p + lo, c->r.p + lo, c->sc.p + lo, n, lp, c->lif_tbl.p,
-                            kLifTable, c->hist.p, c->stats.p, TopFuse{}, s, c->sc8.p + lo));
-  }
-  c->sc8_ok = true;  // on [lo, hi), the only range this rank's passes read
-  if (c->state_fresh) {  // derived on [lo, hi) (the rest of the pool is not this rank's)
-    c->state_derived = true;
-    c->derived_lp = lp;
-  }
-  c->state_fresh = false;
-  c->sliced = true;  // only [lo, hi) of v / r / spike counts / currents is this rank's now
   if (m) {
     HIPCHK(launch_topn_threshold(c->hist.p, m, n, c->topst.p, s));
     if ((rc = enqueue_select(c, m, s, lo, n))) return rc;
@@ -2381,7 +2385,8 @@ int nk_finalize_slice(nk_counter *c, int streaming, const void *d_slice, int sli
   if ((rc = enqueue_readback(c, (uint32_t)m, false, s))) return rc;
   if ((rc = wait_readback(c, s))) return rc;
   const ResultHdr *h = reinterpret_cast<const ResultHdr *>(c->res_h);
-  const uint64_t new_spikes = h->stats[0], max_sc = h->stats[1];
+  // a redo counts no spikes: the LIF that produced them was accounted already
+  const uint64_t new_spikes = run_lif ? h->stats[0] : 0, max_sc = h->stats[1];
   if (m && h->st.refine) {  // spike counts >= 4095: exact radix refine over the slice
     TopState st = h->st;
     if ((rc = refine_threshold(c, m, max_sc, st, s, lo, n))) return rc;
@@ -2407,6 +2412,133 @@ int nk_finalize_slice(nk_counter *c, int streaming, const void *d_slice, int sli
   HIPCHK(hipMemcpyAsync(d_seg, seg.data(), seg.size() * 8, hipMemcpyHostToDevice, s));
   HIPCHK(hipStreamSynchronize(s));  // seg is host memory the copy reads
   c->slice_ready = true;
+  return NK_OK;
+}
+
+int nk_finalize_slice(nk_counter *c, int streaming, const void *d_slice, int slice_bits,
+                      size_t lo, size_t hi, uint64_t *d_seg, size_t seg_rows, void *stream) {
+  if (!c || !d_seg) return fail(NK_E_INVALID, "null argument");
+  (void)hipSetDevice(c->device);
+  return finalize_slice_impl(c, streaming, d_slice, slice_bits, lo, hi, d_seg, seg_rows,
+                             pick_stream(c, stream), true);
+}
+
+extern "C++" namespace nk {
+// the blocking selection of this rank's slice after nk_slice_export (its LIF
+// done): a redo of the device-side sliced finish (nk_dist.cpp)
+int slice_reselect(nk_counter *c, size_t lo, size_t hi, uint64_t *d_seg, size_t seg_rows,
+                   hipStream_t s) {
+  (void)hipSetDevice(c->device);
+  return finalize_slice_impl(c, 0, nullptr, 32, lo, hi, d_seg, seg_rows, pick_stream(c, s), false);
+}
+}  // namespace nk
+
+// The pool-sliced finish with no host wait before nk_merge_export:
+//   nk_slice_export  LIF of [lo, hi) from the reduce-scattered u32 slice, the
+//                    slice's top rows (exact unless a spike count passed
+//                    4095: flagged) into d_seg by a kernel;
+//   <all-gather of the slice segments>
+//   nk_adopt_export  the global rows picked on the device, this shard's
+//                    uniques pass for them with its new keys appended to the
+//                    key segment (nk_finalize_export's tail);
+//   <all-gather of the key segments>
+//   nk_merge_export  union -> uniques column, one readback; a redo (refine,
+//                    set, bucket, truncation) takes the blocking path.
+int nk_slice_export(nk_counter *c, int streaming, const uint32_t *d_slice, size_t lo, size_t hi,
+                    uint64_t *d_seg, size_t seg_rows, void *stream) {
+  if (!c || !d_seg) return fail(NK_E_INVALID, "null argument");
+  if (lo > hi || hi > c->pool) return fail(NK_E_INVALID, "slice [%zu, %zu) outside the pool", lo, hi);
+  if (hi > lo && !d_slice) return fail(NK_E_INVALID, "null slice");
+  const uint64_t want = std::min<uint64_t>(c->opts.top_n, c->pool);
+  if (seg_rows < want) return fail(NK_E_INVALID, "seg_rows (%zu) < top_n rows (%llu)", seg_rows,
+                                   (unsigned long long)want);
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  HIPCHK(mark(c, 7, s));
+  c->k1b_lif = false;
+  const uint64_t n = hi - lo;
+  const uint64_t m = std::min<uint64_t>(want, n);
+  LifParams lp;
+  int rc = settle_state(c, s);
+  if (rc || (rc = lif_prepare(c, streaming, lp, s))) return rc;
+  c->pend_slices = 0;
+  c->cur_in_wire = false;
+  c->cur_fresh = false;
+  c->top_valid = false;
+  c->top_keys_ready = false;
+  c->redo_ready = false;
+  if ((rc = c->sc8.ensure(c->pool))) return rc;
+  if (n)
+    HIPCHK(launch_lif_apply(c->cur.p + lo, d_slice, 1u, 1, nullptr, (int)c->last_pa.bin_bits,
+                            c->state_fresh ? 1 : 0, /*derive=*/1, c->v.p + lo, c->r.p + lo,
+                            c->sc.p + lo, n, lp, c->lif_tbl.p, kLifTable, c->hist.p, c->stats.p,
+                            TopFuse{}, s, c->sc8.p + lo));
+  c->sc8_ok = true;
+  if (c->state_fresh) {
+    c->state_derived = true;
+    c->derived_lp = lp;
+  }
+  c->state_fresh = false;
+  c->sliced = true;
+  if (m) {
+    HIPCHK(launch_topn_threshold(c->hist.p, m, n, c->topst.p, s));
+    if ((rc = enqueue_select(c, m, s, lo, n))) return rc;
+  }
+  HIPCHK(launch_slice_seg(c->cand.p, c->top_cur.p, c->topst.p, c->stats.p, (uint32_t)m, lo, d_seg, s));
+  c->slice_ready = true;
+  return NK_OK;
+}
+
+int nk_adopt_export(nk_counter *c, const uint64_t *d_all, size_t world, size_t stride,
+                    uint64_t *d_keyseg, size_t cap, void *stream) {
+  if (!c || !d_all || !d_keyseg) return fail(NK_E_INVALID, "null argument");
+  if (!c->slice_ready) return fail(NK_E_INVALID, "nk_slice_export first");
+  if (cap > (1ull << 40)) return fail(NK_E_INVALID, "cap too large");
+  const uint64_t want = std::min<uint64_t>(c->opts.top_n, c->pool);
+  if (!world || stride < kSliceHdr + 3 * want)
+    return fail(NK_E_INVALID, "bad all-gather layout (world %zu, stride %zu)", world, stride);
+  if ((uint64_t)world * want > (uint64_t)kAdoptMax)
+    return fail(NK_E_UNSUPPORTED, "world * top_n > %d: nk_adopt_slices", kAdoptMax);
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  c->slice_ready = false;
+  int rc;
+  // every rank's slice yields min(top_n, its size) rows: together >= min(top_n, pool) = want
+  HIPCHK(launch_slice_adopt(d_all, (uint32_t)world, stride, (uint32_t)want, c->cand.p, c->top_cur.p,
+                            c->topst.p, c->stats.p, s));
+  const bool uniq = want && c->have_input && c->last_in.n_tiles;
+  if ((rc = c->export_n.ensure(1))) return rc;
+  if (!c->export_n_zeroed) {
+    HIPCHK(hipMemsetAsync(c->export_n.p, 0, 8, s));
+    c->export_n_zeroed = true;
+  }
+  c->xport_dst = d_keyseg;  // the uniques pass appends each new key to the segment
+  c->xport_cap = cap;
+  rc = uniq ? enqueue_uniques(c, (uint32_t)want, false, false, s) : NK_OK;
+  c->xport_dst = nullptr;
+  if (rc) return rc;
+  MergePrep mp{};
+  c->merge_prepped = 0;
+  if (want && !getenv("NK_NO_MERGE_PREP_FUSE")) {
+    const uint64_t mcap = merge_cap((uint64_t)world * cap);
+    if (mcap > c->mset_alloc) {
+      if ((rc = c->mset_keys.ensure(c->w128 ? 3 * mcap : mcap))) return rc;
+      c->mset_alloc = mcap;
+    }
+    if ((rc = c->trunc_d.ensure(1)) || (rc = c->mset_mask_d.ensure(1)) ||
+        (rc = c->muniq.ensure(kMaxTopN)) || (rc = c->mspecial.ensure(kMaxTopN)))
+      return rc;
+    mp = MergePrep{c->mset_keys.p, c->mset_mask_d.p, mcap, c->muniq.p, c->mspecial.p, (uint32_t)want,
+                   c->trunc_d.p};
+    c->merge_prepped = mcap;
+  }
+  HIPCHK(launch_export(c->set_keys.p, c->set_mask_d.p, c->set_alloc, c->w128 ? 1 : 0, uniq,
+                       /*appended=*/true, c->special.p, (uint32_t)want, want ? c->topst.p : nullptr,
+                       c->post_flags.p, cap, d_keyseg, c->export_n.p, s, mp));
+  c->export_pending = true;
+  c->export_blocking = false;
+  c->export_want = (uint32_t)want;
+  c->export_uniq = uniq;
   return NK_OK;
 }
 

@@ -24,6 +24,7 @@
 
 #include "neurokmer.h"
 #include "nk_internal.h"
+#include "nk_kernels.h"
 
 namespace {
 
@@ -364,6 +365,25 @@ int nk_finalize_sliced_dist(nk_counter *c, nk_comm *m, int streaming, uint64_t t
   const uint64_t rows = nk::counter_rows(c);
   const size_t stride = 3 + 3 * rows;
   OOM(b.sseg.ensure(stride) && b.sall.ensure(W * stride), "slice row segments");
+  if (small && W * rows <= (uint64_t)nk::kAdoptMax) {
+    // no host wait before the merge: the slice's LIF + top rows, the global
+    // rows and this shard's uniques all on the device (nk_slice_export ..
+    // nk_merge_export); a redo takes the blocking selection without the LIF
+    const size_t kstride = 1 + (size_t)nk::counter_key_words(c) * cap;
+    OOM(b.seg.ensure(kstride) && b.all.ensure(W * kstride), "export segments");
+    RC(nk_slice_export(c, streaming, hi > lo ? (const uint32_t *)slice : nullptr, lo, hi, b.sseg.p,
+                       rows, stream));
+    RC(all_gather(m, b.sseg.p, b.sall.p, stride, true, s));
+    RC(nk_adopt_export(c, b.sall.p, W, stride, b.seg.p, cap, stream));
+    RC(all_gather(m, b.seg.p, b.all.p, kstride, true, s));
+    int redo = 0;
+    RC(nk_merge_export(c, b.all.p, W, kstride, cap, &redo, stream));
+    if (!redo) return NK_OK;
+    RC(nk::slice_reselect(c, lo, hi, b.sseg.p, rows, s));
+    RC(all_gather(m, b.sseg.p, b.sall.p, stride, true, s));
+    RC(nk_adopt_slices(c, b.sall.p, W, stride, stream));
+    return union_top_kmers(c, m, b, cap, s);
+  }
   RC(nk_finalize_slice(c, streaming, hi > lo ? slice : nullptr, small ? 32 : 64, lo, hi, b.sseg.p,
                        rows, stream));
   RC(all_gather(m, b.sseg.p, b.sall.p, stride, true, s));

@@ -23,6 +23,10 @@ bool counter_kpn_global(const nk_counter *c);
 // then emptied by the export's header kernel)
 void counter_merge_hint(nk_counter *c, uint32_t world);
 uint64_t *counter_currents_on(nk_counter *c, hipStream_t s);
+// after nk_slice_export + nk_merge_export asked for a redo: the blocking,
+// exact selection of this rank's slice [lo, hi) into d_seg (its LIF not rerun)
+int slice_reselect(nk_counter *c, size_t lo, size_t hi, uint64_t *d_seg, size_t seg_rows,
+                   hipStream_t s);
 // a per-process id of the handle, never reused after nk_free
 uint64_t counter_uid(const nk_counter *c);
 // the loopback transport (nk_loop.hip)

@@ -299,6 +299,16 @@ struct MergePrep {
   uint32_t m = 0;
   uint32_t *trunc = nullptr;
 };
+// the device-side sliced finish (nk_slice.hip): a slice's top rows into its
+// all-gather segment, and the global rows picked from the gathered segments
+// (world * want <= kAdoptMax)
+constexpr int kAdoptMax = 2048;
+hipError_t launch_slice_seg(const TopCand *cand, const uint64_t *top_cur, const TopState *st,
+                            const uint64_t *stats, uint32_t m, uint64_t lo, uint64_t *seg,
+                            hipStream_t s);
+hipError_t launch_slice_adopt(const uint64_t *all, uint32_t world, uint64_t stride, uint32_t want,
+                              TopCand *cand, uint64_t *top_cur, TopState *st, uint64_t *stats,
+                              hipStream_t s);
 hipError_t launch_export(const unsigned long long *set_keys, const uint64_t *set_mask,
                          uint64_t set_alloc, int w128, bool uniq, bool appended,
                          const uint32_t *special, uint32_t n_top, const TopState *st,

@@ -142,14 +142,22 @@ def test_loopback_finalize_dist(world, wire, cap):
         _assert_same(got[r], want)
 
 
-@pytest.mark.parametrize("world,width", [(2, 64), (3, 128), (4, 64)])
-def test_loopback_finalize_sliced_dist(world, width):
+@pytest.mark.parametrize("world,width,pool,steps,cap", [
+    (2, 64, (1 << 22) + 5, 1000, 4096),   # u32 wire: the device-side finish (nk_slice_export)
+    (3, 128, (1 << 22) + 5, 1000, 4096),  # u64 wire: the blocking finish (nk_finalize_slice)
+    (4, 64, (1 << 22) + 5, 1000, 4),      # truncated key segments: redo through nk_adopt_slices
+    (3, 64, 2_000_000, 1000, 4096),       # the metric's pool
+    (2, 64, 2_000_000, 20000, 4096),      # spike counts past 4095 in a slice: the refine redo
+])
+def test_loopback_finalize_sliced_dist(world, width, pool, steps, cap):
     """nk_finalize_sliced_dist: reduce-scatter of a zero-padded wire (a pool
-    not divisible by the world), LIF of each rank's slice, all-gather of the
-    slices' top rows, union of the shards' top k-mers."""
+    not divisible by the world), LIF of each rank's slice, the slices' top
+    rows gathered and the global rows picked, union of the shards' top k-mers.
+    With the u32 wire all of it stays on the device until the merge's
+    readback; the redo cases fall back to the blocking selection."""
     from neurokmer_amd import SpikingKmerCounter
     from neurokmer_amd import dist as nkdist
-    k, pool = 63, (1 << 22) + 5
+    k = 63 if pool > 2_000_000 else 31
     bases, offs = _input(900_000, 81 + world, 7)
     shards = _shards(bases, offs, world)
     tk = int(offs[-1]) if width == 64 else None
@@ -158,9 +166,10 @@ def test_loopback_finalize_sliced_dist(world, width):
         b, o = shards[r]
         d_b, d_o = _dev(b, o)
         c = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, True, kmer_width=width)
+        c.set_steps(steps)
         for _ in range(2):
             c.accumulate_device(d_b.data_ptr(), d_o.data_ptr(), o.size - 1, b.size)
-            nkdist.finalize_step_sliced(c, total_kmers=tk, comm=comm)
+            nkdist.finalize_step_sliced(c, total_kmers=tk, cap=cap, comm=comm)
         torch.cuda.current_stream().synchronize()
         st = _state(c)
         comm.forget(c)
@@ -169,10 +178,13 @@ def test_loopback_finalize_sliced_dist(world, width):
 
     got = _run_ranks(world, body)
     one = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, True, kmer_width=width)
+    one.set_steps(steps)
     for _ in range(2):
         one.process_parallel_arrays(bases, offs)
     want = _state(one)
     one.close()
+    if steps > 1000:
+        assert int(want["spike_counts"].max()) > 4095  # the case this parameter exists for
     for r in range(world):
         lo, hi, _ = nkdist.slice_bounds(pool, world, r)
         _assert_same(got[r], want, lo, hi)  # each rank owns its slice of the pool
