@@ -216,6 +216,10 @@ def main() -> int:
     # step itself the plain one-GPU step (what RCCL's presence alone costs)
     ap.add_argument("--dist-init-only", action="store_true")
     ap.add_argument("--nk-comm", action="store_true", help="the library's communicator under gloo too")
+    ap.add_argument("--finish", choices=("plain", "sliced"), default=None,
+                    help="N > 1: all-reduce + the whole pool's LIF on every rank (plain), or "
+                         "reduce-scatter + each rank's 1/N of the pool (sliced; default with the "
+                         "in-library communicator, and always for config5)")
     ap.add_argument("--inflight", type=int, default=None, choices=(1, 2, 3, 4),
                     help="batches in flight (default: 3 on one GPU, 1 across ranks and for "
                          "config5): > 1 "
@@ -255,6 +259,10 @@ def main() -> int:
     # slowed K1a by 5-20 % even when unused (1-rank rehearsal: 0.599-0.628 vs
     # 0.576-0.577 ms per step with gloo, plain 0.546-0.549, profiles/r03_s10..s12)
     lib_comm = dist_on and not shared and not args.dist_python
+    if args.workload == "config5":
+        args.finish = "sliced"
+    elif args.finish is None:
+        args.finish = "sliced" if lib_comm else "plain"
     backend = args.dist_backend or ("gloo" if shared or lib_comm else "nccl")
     if args.inflight is None:
         # config 5 (P = 256 M): its finish is a 256 M-neuron LIF + top-N pass
@@ -308,8 +316,8 @@ def main() -> int:
         scaling = "weak"
         workload = (f"config {args.workload[-1]}: {n_bases:,} bases in {RECS} records per GPU, "
                     f"k={k}, kmer_width={args.kmer_width}, pool_size={pool:,}, --canonical, "
-                    + ("process_parallel" if args.workload == "config2" or world == 1 else
-                       "pool-sliced finish"))
+                    + ("process_parallel" if world == 1 and not dist_on else
+                       f"{args.finish} multi-GPU finish"))
     else:
         T = args.total_bases
         n_shards = args.shard_of or world
@@ -404,7 +412,7 @@ def main() -> int:
                 c.settle(st.cuda_stream)
             return
         with torch.cuda.stream(st):
-            if args.workload == "config5":
+            if args.finish == "sliced":
                 if between is not None:
                     between()
                 nkdist.finalize_step_sliced(c, total_kmers=total_kmers, comm=comm)
@@ -594,7 +602,9 @@ def main() -> int:
                        "kmers_rank0": nk_rank, "kmers_total": total_kmers,
                        "parallelism": f"dp{world}" + (f" (rehearsal: {world} ranks on {ndev} GPU, "
                                                       f"{backend})" if shared else ""),
-                       "collectives": ((f"in-library RCCL communicator (nk_finalize_dist); "
+                       "finish": args.finish if dist_on else None,
+                       "collectives": ((f"in-library RCCL communicator ("
+                                        f"{'nk_finalize_sliced_dist' if args.finish == 'sliced' else 'nk_finalize_dist'}); "
                                         f"torch.distributed {backend} for bootstrap and timing")
                                        if comm is not None
                                        else (f"torch.distributed {backend} from Python" if dist_on
@@ -653,7 +663,7 @@ def parity_ranks(args, ctr, world, rank, dev_idx, nkdist, Counter, synth, total_
     records is the N-rank answer (bit-identical currents at 1,
     2, 4 and 8 GPUs).  Pool-sliced state (config5) is gathered first."""
     import torch
-    st = nkdist.gather_state(ctr) if args.workload == "config5" else None
+    st = nkdist.gather_state(ctr) if args.finish == "sliced" else None
     if rank != 0:
         return None
     k, pool = args.k, args.pool

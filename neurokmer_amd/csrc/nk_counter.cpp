@@ -792,7 +792,8 @@ static int build_sorted(nk_counter *c, const KmerInput &in0, hipStream_t s) {
   return NK_OK;
 }
 
-static uint64_t count_chunk(uint64_t n_bases = 0, uint64_t pool = 0, bool wide = false);
+static uint64_t count_chunk(uint64_t n_bases = 0, uint64_t pool = 0, bool wide = false,
+                            uint64_t held = 0);
 static uint32_t env_u32(const char *name, uint32_t dflt);
 
 // neurons per K1a<KEYS> bucket (log2): kXMinBinBits; NK_XBIN_BITS (A/B,
@@ -1020,8 +1021,11 @@ static bool atomic_forced() {
 #endif
 constexpr double kKeepFrac = 0.6;
 // (pool: a bucket region of one launch stays below 2^31 records, so K1b's u32
-// bins and partials cannot wrap whatever the input)
-static uint64_t count_chunk(uint64_t n_bases, uint64_t pool, bool wide) {
+// bins and partials cannot wrap whatever the input; held: the arena bytes
+// this handle already holds, free for it to reuse -- without them a handle's
+// second count of the same input measured its own arena as taken and fell
+// back to batches, profiles/r04_t3)
+static uint64_t count_chunk(uint64_t n_bases, uint64_t pool, bool wide, uint64_t held) {
   const char *e = getenv("NK_COUNT_CHUNK");
   uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
   if (!v) {
@@ -1033,10 +1037,15 @@ static uint64_t count_chunk(uint64_t n_bases, uint64_t pool, bool wide) {
     size_t fr = 0, tot = 0;
     if (n_bases > v && pool && n_bases / B * 5 / 4 < (1ull << 31) - (1ull << 24) &&
         !getenv("NK_COUNT_BATCHED") && hipMemGetInfo(&fr, &tot) == hipSuccess &&
-        (double)n_bases * per <= kKeepFrac * (double)fr)
+        (double)n_bases * per <= kKeepFrac * (double)(fr + held))
       v = (n_bases + kPartTile - 1) / kPartTile * kPartTile;
   }
   return std::max<uint64_t>(kPartTile, v / kPartTile * kPartTile);
+}
+
+// device bytes of the partition arena this handle holds (reused by a count)
+static uint64_t arena_bytes(const nk_counter *c) {
+  return c->p_off.n * 2 + c->p_pos.n * 2 + c->p_desc.n * 8 + c->w_rec.n * 4;
 }
 
 // Sizes the buffers for a batch of about est_bases bases (slack: extra
@@ -1218,7 +1227,7 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
   // bucket regions: 1.25x the fair share + one tile of slack (overflow is
   // still exact: the excess is counted with direct atomics); past
   // count_chunk() positions the regions hold one batch at a time
-  uint64_t chunk = count_chunk(n_bases, c->pool, c->w128 || c->k > 32);
+  uint64_t chunk = count_chunk(n_bases, c->pool, c->w128 || c->k > 32, arena_bytes(c));
   uint64_t est = std::min<uint64_t>(n_bases, chunk);
   // the exact table grouped by neuron from this count's own records (K1a also
   // writes each record's key, nk_table.hip), in 4096-neuron buckets
@@ -1615,10 +1624,17 @@ static int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, bool post_don
     if (genk) {
       // the tiles holding the top rows' records, then the rescan of those only;
       // a full list sets post flag 1 (-> settle_top redoes a full rescan)
-      const uint32_t kTileList = [] {  // NK_UNIQ_TILE_LIST (tests): a small list overflows
+      // list capacity: 2^20 entries, or 1/16 of the input's lanes when that is
+      // more (a 12.5 Gbase config-5 input: planted repeats give the top rows
+      // ~800 k records each, 16 M lanes, past 2^20 -> the full rescan, 70 ms,
+      // profiles/r04_t3); a list past 1/16 of the lanes would hash as much as
+      // half a rescan anyway.  NK_UNIQ_TILE_LIST (tests): a small list overflows.
+      const uint32_t kTileList = [&] {
         const char *e = getenv("NK_UNIQ_TILE_LIST");
         const unsigned long v = e ? strtoul(e, nullptr, 10) : 0;
-        return v ? (uint32_t)v : (1u << 20);
+        const uint64_t lanes16 = in.n_tiles * kPartBlock / 16;  // k_part_gen: one lane per 16 positions
+        return v ? (uint32_t)v
+                 : (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 20, lanes16), 1u << 30);
       }();
       if ((rc = c->u_tiles.ensure(kTileList)) || (rc = c->u_nt.ensure(1))) return rc;
       if (c->u_mark.n < in.n_tiles || c->u_mark_zeroed < in.n_tiles || ++c->u_epoch == 0) {
@@ -2742,7 +2758,7 @@ static int acc_begin(nk_counter *c, uint64_t est_bases, uint64_t batch_bases, St
   z.ptr[z.n] = c->cur.p; z.bytes[z.n++] = c->pool * 8;
   const uint64_t B = (c->pool + kBinsPerBucket - 1) >> kBinBits;
   const bool part_like = !c->w128 && c->k <= 32 && B <= (uint64_t)kMaxBuckets &&
-                         !wide_bits_forced() && est_bases <= count_chunk(est_bases, c->pool, c->w128 || c->k > 32);
+                         !wide_bits_forced() && est_bases <= count_chunk(est_bases, c->pool, c->w128 || c->k > 32, arena_bytes(c));
   const uint64_t est = part_like ? est_bases : std::min(est_bases, batch_bases);
   // segments per bucket: one per tile per launch; chunk-straddling tiles add a few
   const uint64_t max_segs = n_tiles_for(std::max<uint64_t>(est, 1), kPartTile) + 4096;

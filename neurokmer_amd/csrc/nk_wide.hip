@@ -203,10 +203,15 @@ __global__ __launch_bounds__(kPartBlock) void k_split(GenPartArgs ga, PartArgs p
   __shared__ __align__(16) uint16_t s_rec[S::kSlots];
   __shared__ S::GMap s_gmap[S::kGroups];
   const int tid = threadIdx.x;
-  const uint32_t cb = blockIdx.y;
+  // workgroup L takes tile L / nb of coarse bucket L % nb: the workgroups in
+  // flight spread over every coarse bucket (bucket-major order put ~1000 of
+  // them on one bucket's 32 fine fill counters at a time: 131 ms at a 12.5
+  // Gbase config-5 input, profiles/r04_t3), and bucket b stays on XCD b % 8
+  // (nb a multiple of 8), its fine regions' partial lines in one L2
+  const uint32_t cb = blockIdx.x % ga.n_buckets;
   uint64_t n = ga.fill[cb] & ((1ull << 40) - 1);  // (bits 40..: kept segments)
   if (n > ga.cap) n = ga.cap;
-  const uint64_t t0 = (uint64_t)blockIdx.x * kPartTile;
+  const uint64_t t0 = (uint64_t)(blockIdx.x / ga.n_buckets) * kPartTile;
   if (t0 >= n) return;  // uniform
   const uint32_t F = 1u << (ga.bin_bits - kBinBits);
   const uint32_t cmask = (uint32_t)((1ull << ga.bin_bits) - 1ull);
@@ -296,7 +301,32 @@ __global__ __launch_bounds__(kHistBlock) void k_uniq_tiles(GenPartArgs ga, UniqA
     return h;
   };
   auto entry = [&](uint64_t i, uint32_t rec) -> uint32_t {
-    uint64_t a = 0, z = n_seg;  // last segment with first record <= i
+    // last segment with first record <= i: every tile adds about the same
+    // number of records to a bucket, so i * n_seg / n is within a few segments
+    // (a gallop from there, then a binary search: ~4 dependent loads instead
+    // of ~21 over 1.5 M segments at a 12.5 Gbase input)
+    uint64_t a = 0, z = n_seg;
+    if (n_seg > 1) {
+      uint64_t g = (uint64_t)((double)i * (double)n_seg / (double)(n ? n : 1));
+      if (g >= n_seg) g = n_seg - 1;
+      if (d[g].y <= i) {  // gallop up: [g, z)
+        a = g;
+        for (uint64_t st = 1;; st <<= 1) {
+          const uint64_t t = a + st;
+          if (t >= n_seg) { z = n_seg; break; }
+          if (d[t].y > i) { z = t; break; }
+          a = t;
+        }
+      } else {  // gallop down: [a, g)
+        z = g;
+        for (uint64_t st = 1;; st <<= 1) {
+          if (z <= st) { a = 0; break; }
+          const uint64_t t = z - st;
+          if (d[t].y <= i) { a = t; break; }
+          z = t;
+        }
+      }
+    }
     while (z - a > 1) {
       const uint64_t m = (a + z) >> 1;
       if (d[m].y <= i) a = m;
@@ -511,8 +541,9 @@ hipError_t launch_uniq_tiles(const GenPartArgs &ga, int wide, const UniqArgs &u,
 hipError_t launch_split(const GenPartArgs &ga, const PartArgs &pa, hipStream_t s) {
   if (!ga.n_buckets) return hipSuccess;
   if (ga.bin_bits < kBinBits || ga.bin_bits - kBinBits > kMaxSplitBits) return hipErrorInvalidValue;
-  const unsigned tx = (unsigned)((ga.cap + kPartTile - 1) / kPartTile);
-  hipLaunchKernelGGL(k_split, dim3(tx, ga.n_buckets), dim3(kPartBlock), 0, s, ga, pa);
+  const uint64_t tx = (ga.cap + kPartTile - 1) / kPartTile;
+  if (tx * ga.n_buckets > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_split, dim3((unsigned)(tx * ga.n_buckets)), dim3(kPartBlock), 0, s, ga, pa);
   return hipGetLastError();
 }
 
