@@ -1711,7 +1711,31 @@ __global__ __launch_bounds__(kLifBlock) void k_lif_apply(uint64_t *__restrict__ 
     // neurons that never spiked (most of a large pool) are counted in a
     // register: same-address LDS atomics of a whole wave serialise
     if (sc == 0) ++n_zero;
-    else atomicAdd(&sh[sc < (uint64_t)(kHistBins - 1) ? (uint32_t)sc : (uint32_t)(kHistBins - 1)], 1u);
+  }
+  // the histogram: bins the lanes of a wave share are added once per bin for
+  // the two most common ones (a uniform pool -- a 12.5 Gbase config-4 shard,
+  // every neuron spiking 333-334 times -- sent all 64 lanes to one LDS bin:
+  // k_lif_apply 5 ms against 0.02 ms at config 2, profiles/r04_t3); the rest
+  // one atomic per lane
+#pragma unroll
+  for (int j = 0; j < kLifPerThread; ++j) {
+    const uint64_t sc = scv[j];
+    const uint32_t bin = sc < (uint64_t)(kHistBins - 1) ? (uint32_t)sc : (uint32_t)(kHistBins - 1);
+    bool pend = sc != 0;  // (i >= pool: scv 0)
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const uint64_t m = __ballot(pend);
+      if (!m) break;
+      const uint32_t v = (uint32_t)__shfl((int)bin, __ffsll((long long)m) - 1, 64);
+      const bool mine = pend && bin == v;
+      const uint64_t same = __ballot(mine);
+      if (mine) {
+        if ((threadIdx.x & 63) == (uint32_t)(__ffsll((long long)same) - 1))
+          atomicAdd(&sh[v], (uint32_t)__popcll(same));
+        pend = false;
+      }
+    }
+    if (pend) atomicAdd(&sh[bin], 1u);
   }
   // wave reductions
   for (int o = 32; o > 0; o >>= 1) {

@@ -146,6 +146,59 @@ __device__ __forceinline__ void sort_and_store(const uint32_t (&E)[PER], const u
 
 }  // namespace
 
+// --kmer-width=128, canonical, 48 < k <= 64 (config 5: k = 63): the lane's 16
+// windows from 6 forward and 6 complement code words read once from LDS, each
+// window's two 128-bit strands by funnel shifts of constant (2j) and uniform
+// (128 - 2k) amounts -- no per-window LDS reads, 64-bit variable shifts or
+// dynamically indexed registers (the generic loop's cost: K1g at 0.57 of its
+// 128-bit hash-only floor at a 12.5 Gbase input, profiles/r04_t3).  The same
+// keys as window_key128<CANON> (nk_tile.h); every position is hashed, the
+// ones that start no k-mer go to the no-record bucket nb.
+__device__ __forceinline__ void gen_rolled128(const TileLds<kPartTile, false> &L, const KmerInput &in,
+                                              uint64_t T0, int q0, int k, const FastMod &fm,
+                                              bool small_pool, uint32_t nb, int bb, uint32_t omask,
+                                              uint32_t ltag, uint32_t *s_cnt, uint32_t (&E)[kPer],
+                                              uint32_t (&O)[kPer]) {
+  const int w = q0 >> 4;  // q0 is 16-aligned
+  uint32_t Fw[6], Rw[6];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    Fw[c] = L.F[w + c];
+    Rw[c] = L.R[w + c];
+  }
+  // windows that start a k-mer of some record, in [pos_lo, pos_hi)
+  uint32_t ok = ~(L.WIN[q0 >> 5] >> (q0 & 31)) & 0xFFFFu;
+  const uint64_t rem = in.n_bases - T0;
+  const uint64_t nrange = rem >= (uint64_t)k ? rem - (uint64_t)k + 1 : 0;
+  if (nrange < (uint64_t)q0 + kPer) ok &= nrange > (uint64_t)q0 ? (1u << (uint32_t)(nrange - q0)) - 1u : 0u;
+  const uint64_t p0 = T0 + (uint64_t)q0;
+  if (in.pos_lo > p0) ok &= in.pos_lo - p0 >= (uint64_t)kPer ? 0u : ~((1u << (uint32_t)(in.pos_lo - p0)) - 1u);
+  if (in.pos_hi < p0 + kPer) ok &= in.pos_hi > p0 ? (1u << (uint32_t)(in.pos_hi - p0)) - 1u : 0u;
+  const uint32_t sh = (uint32_t)(128 - 2 * k);  // 0 .. 30
+  const uint64_t hmask = k >= 64 ? ~0ull : ((1ull << (2 * k - 64)) - 1ull);
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    uint32_t W[4], Y[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      W[c] = j ? __builtin_amdgcn_alignbit(Fw[c], Fw[c + 1], 32 - 2 * j) : Fw[c];
+      Y[c] = j ? __builtin_amdgcn_alignbit(Rw[c + 1], Rw[c], 2 * j) : Rw[c];
+    }
+    Key128 fwd, rev;
+    fwd.lo = ((uint64_t)__builtin_amdgcn_alignbit(W[1], W[2], sh) << 32) |
+             __builtin_amdgcn_alignbit(W[2], W[3], sh);
+    fwd.hi = ((uint64_t)(W[0] >> sh) << 32) | __builtin_amdgcn_alignbit(W[0], W[1], sh);
+    rev.lo = ((uint64_t)Y[1] << 32) | Y[0];
+    rev.hi = (((uint64_t)Y[3] << 32) | Y[2]) & hmask;
+    const Key128 key = key128_less(rev, fwd) ? rev : fwd;
+    const uint64_t h = sip13_u128(key.lo, key.hi);
+    const uint32_t idx = small_pool ? fastmod32(h, fm) : (uint32_t)fastmod(h, fm);
+    const uint32_t b = ((ok >> j) & 1u) ? (idx >> bb) : nb;
+    E[j] = (b << 16) | atomicAdd(&s_cnt[b], 1u);
+    O[j] = (idx & omask) | ltag;
+  }
+}
+
 // K1g: hash + partition for key modes KM 0/1/2 (see the file comment).
 // Lane = 16 consecutive positions of an 8192-position tile.
 template <int KM, bool CANON, bool WIDE>
@@ -173,9 +226,18 @@ __global__ __launch_bounds__(kPartBlock) void k_part_gen(KmerInput in, int k, Fa
   stage_tile<kPartTile, kPartBlock, kRaw>(L, in, tile, k);  // syncs
 
   const int q0 = tid * kPer;
+  uint32_t E[kPer], O[kPer];
+  if constexpr (KM == 2 && CANON) {
+    if (k > 48) {  // (uniform) the lane's 16 windows rolled from registers
+      gen_rolled128(L, in, T0, q0, k, fm, small_pool, nb, bb, omask, ltag, s_cnt, E, O);
+      sort_and_store<WIDE, kPer>(E, O, nb, s_cnt, s_start, s_base, s_fit, s_rec, s_gmap, ga.fill,
+                                 ga.overflow, ga.cap, reinterpret_cast<typename S::Rec *>(ga.rec),
+                                 0, bb, ga.currents, ga.desc, ga.max_segs, (uint32_t)tile);
+      return;
+    }
+  }
   RecCursor rc;
   rec_cursor_init<KM>(rc, in, T0 + (uint64_t)q0, blockIdx.x);
-  uint32_t E[kPer], O[kPer];
 #pragma unroll 2
   for (int j = 0; j < kPer; ++j) {
     const int q = q0 + j;

@@ -367,7 +367,7 @@ def test_wide_partition_streaming_ingest(tmp_path, k):
 
 # ---- --kmer-width=128 (the build's true k <= 64 mode) -------
 @pytest.mark.parametrize("canon", [True, False])
-@pytest.mark.parametrize("k", [1, 17, 32, 33, 47, 63, 64])
+@pytest.mark.parametrize("k", [1, 17, 32, 33, 47, 49, 56, 63, 64])
 def test_width128_parity(k, canon):
     bases, offs = ragged_records(n_rate=0.01, mixed_case=True, seed=211 + k)
     g, r = run_both(bases, offs, k, 5003, canon, width=128)
