@@ -263,7 +263,9 @@ def _config3_run(args, path, fsize, n_reads, nk, k, pool, L, dev, Counter, synth
     offs = np.arange(n_reads + 1, dtype=np.uint64) * np.uint64(L)
     d_o = torch.from_numpy(offs.view(np.int64)).to(dev)
     r = Counter(k, 1.0, 0.95, 2, 1.0, pool, True, device=0)
-    s = torch.cuda.current_stream()
+    # a real stream: torch's default one is handle 0, which the library reads
+    # as "the handle's own stream" (the events would then bracket nothing)
+    s = torch.cuda.Stream(device=dev)
     cms, tot = [], []
     for i in range(1 + steps):
         r.reset()

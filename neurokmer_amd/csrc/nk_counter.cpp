@@ -2394,7 +2394,7 @@ static int finalize_slice_impl(nk_counter *c, int streaming, const void *d_slice
   }
   c->top_valid = false;
   c->top_keys_ready = false;
-  if (m) {
+  if (m && run_lif) {
     HIPCHK(launch_topn_threshold(c->hist.p, m, n, c->topst.p, s));
     if ((rc = enqueue_select(c, m, s, lo, n))) return rc;
   }
@@ -2403,7 +2403,10 @@ static int finalize_slice_impl(nk_counter *c, int streaming, const void *d_slice
   const ResultHdr *h = reinterpret_cast<const ResultHdr *>(c->res_h);
   // a redo counts no spikes: the LIF that produced them was accounted already
   const uint64_t new_spikes = run_lif ? h->stats[0] : 0, max_sc = h->stats[1];
-  if (m && h->st.refine) {  // spike counts >= 4095: exact radix refine over the slice
+  // a redo selects by the exact radix passes: nk_slice_export's fused LIF
+  // wrote no spike histogram (max_sc: the largest count of any slice, an
+  // upper bound of this one's)
+  if (m && (h->st.refine || !run_lif)) {  // spike counts >= 4095: exact radix refine over the slice
     TopState st = h->st;
     if ((rc = refine_threshold(c, m, max_sc, st, s, lo, n))) return rc;
     HIPCHK(hipMemcpyAsync(c->topst.p, &st, sizeof st, hipMemcpyHostToDevice, s));
@@ -2484,19 +2487,40 @@ int nk_slice_export(nk_counter *c, int streaming, const uint32_t *d_slice, size_
   c->top_keys_ready = false;
   c->redo_ready = false;
   if ((rc = c->sc8.ensure(c->pool))) return rc;
+  // the slice's top rows selected inside its LIF kernel (+ k_top_final), as the
+  // plain finish does, when they fit: 2 kernels instead of the LIF, the
+  // threshold and three select passes (a 1-rank rehearsal measured the
+  // unfused form +0.04 ms per step, profiles/r04_s2)
+  const bool fuse = m && m <= kFuseMaxTopN && lif_blocks(n) <= kFuseMaxBlocks && n <= (1ull << 24);
+  TopFuse tf{};
+  if (fuse) {
+    const uint32_t nbk = lif_blocks(n);
+    if ((rc = c->bcand.ensure((uint64_t)nbk * m)) || (rc = c->bcnt.ensure(nbk)) ||
+        (rc = c->tbuckets.ensure(m)))
+      return rc;
+    tf.want = (uint32_t)m;
+    tf.bcand = c->bcand.p;
+    tf.bcnt = c->bcnt.p;
+    tf.st = c->topst.p;
+    tf.cand = c->cand.p;
+    tf.top_cur = c->top_cur.p;
+    // (its uniques bookkeeping is redone for the global rows by nk_adopt_export)
+    tf.post = PostArgs{c->set_alloc, nullptr, 0, c->set_mask_d.p, c->tbuckets.p, c->post_flags.p,
+                       c->uniq.p, c->special.p, c->n_hits.p, c->last_pa.bin_bits};
+  }
   if (n)
     HIPCHK(launch_lif_apply(c->cur.p + lo, d_slice, 1u, 1, nullptr, (int)c->last_pa.bin_bits,
                             c->state_fresh ? 1 : 0, /*derive=*/1, c->v.p + lo, c->r.p + lo,
                             c->sc.p + lo, n, lp, c->lif_tbl.p, kLifTable, c->hist.p, c->stats.p,
-                            TopFuse{}, s, c->sc8.p + lo));
-  c->sc8_ok = true;
+                            tf, s, fuse ? nullptr : c->sc8.p + lo));
+  c->sc8_ok = !fuse;
   if (c->state_fresh) {
     c->state_derived = true;
     c->derived_lp = lp;
   }
   c->state_fresh = false;
   c->sliced = true;
-  if (m) {
+  if (m && !fuse) {
     HIPCHK(launch_topn_threshold(c->hist.p, m, n, c->topst.p, s));
     if ((rc = enqueue_select(c, m, s, lo, n))) return rc;
   }

@@ -313,7 +313,7 @@ __global__ __launch_bounds__(kPartBlock) void k_split(GenPartArgs ga, PartArgs p
 // tiles only (and, tagged, hashes only the marked lanes): at config 5 (0.45
 // k-mers per neuron) a fraction of the 14,000 tiles.
 constexpr int kTileSeen = 256;
-constexpr int kHitQueue = 4096;
+constexpr int kHitQueue = 8192;
 template <bool WIDE>
 __global__ __launch_bounds__(kHistBlock) void k_uniq_tiles(GenPartArgs ga, UniqArgs u,
                                                            const uint32_t *__restrict__ tbuckets,
@@ -423,10 +423,17 @@ __global__ __launch_bounds__(kHistBlock) void k_uniq_tiles(GenPartArgs ga, UniqA
     if (g < max_list) tiles[g] = ent;
     else atomicOr(flag, 1u);  // list full: the caller rescans everything
   };
-  // 4 records per lane per load (16 B wide, 8 B narrow), 4 loads in flight
+  // 4 records per lane per load (16 B wide, 8 B narrow), 4 loads in flight;
+  // the block steps through its range together, so the queue can be resolved
+  // whenever it is half full (a planted-repeat top row of ~800 k records gave
+  // a slice ~16 k hits: past the queue they were resolved in place, one
+  // dependent chain per lane -- k_uniq_tiles 19 ms at a 12.5 Gbase config-5
+  // input, profiles/r04_t4)
   constexpr int kU = 4;
   constexpr uint64_t kStep = 4ull * kHistBlock;
-  for (uint64_t i0 = lo + 4ull * threadIdx.x; i0 < hi; i0 += kU * kStep) {
+  const uint32_t flush_at = qcap > (uint32_t)kHitQueue / 2 ? (uint32_t)kHitQueue / 2 : 0u;
+  for (uint64_t base = lo; base < hi; base += kU * kStep) {
+    const uint64_t i0 = base + 4ull * threadIdx.x;
     uint32_t v[kU][4];
 #pragma unroll
     for (int q = 0; q < kU; ++q) {
@@ -462,6 +469,16 @@ __global__ __launch_bounds__(kHistBlock) void k_uniq_tiles(GenPartArgs ga, UniqA
           }
         }
       }
+    __syncthreads();
+    const uint32_t nh = h_n;
+    __syncthreads();  // every lane has read h_n before the next round adds to it
+    if (nh > flush_at) {  // (block-uniform) resolve the queued hits, all lanes together
+      const uint32_t nq = nh < qcap ? nh : qcap;
+      for (uint32_t j = threadIdx.x; j < nq; j += kHistBlock) append(entry(h_i[j], h_rec[j]));
+      __syncthreads();
+      if (threadIdx.x == 0) h_n = 0;
+      __syncthreads();
+    }
   }
   __syncthreads();
   const uint32_t nq = h_n < qcap ? h_n : qcap;
