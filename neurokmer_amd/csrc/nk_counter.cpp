@@ -163,6 +163,9 @@ struct nk_counter {
   // GPU FASTX ingest buffers, kept between file calls
   PinnedBuf ing_hb[2];
   DevBuf<uint8_t> ing_draw, ing_scratch;
+  DevBuf<uint8_t> ing_draw2;              // the second raw-chunk buffer (H2D of the next chunk)
+  hipStream_t ing_cs = nullptr;           // the ingest's copy stream
+  hipEvent_t ing_ev[4] = {};              // copied[0..1], parsed[0..1]
   DevBuf<IngestState> ing_dst;
   // LIF table cache key
   bool lif_valid = false;
@@ -621,7 +624,11 @@ void nk_free(nk_counter *c) {
   c->rk_keys.release(); c->rk_idx.release(); c->rk_tmp.release(); c->rk_cand.release();
   c->rk_uniq.release();
   c->ing_hb[0].release(); c->ing_hb[1].release(); c->ing_draw.release();
-  c->ing_scratch.release(); c->ing_dst.release();
+  c->ing_draw2.release(); c->ing_scratch.release(); c->ing_dst.release();
+  if (c->ing_cs) (void)hipStreamSynchronize(c->ing_cs);
+  for (hipEvent_t &e : c->ing_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->ing_cs) (void)hipStreamDestroy(c->ing_cs);
   c->special.release(); c->stats.release(); c->lif_tbl.release(); c->topst.release();
   c->cand.release(); c->top_cur.release(); c->set_keys.release(); c->top_keys.release();
   c->top_keys_n.release(); c->radix_h.release(); c->set_mask_d.release();
@@ -2898,11 +2905,23 @@ static int ingest_file(nk_counter *c, const char *path, bool *fallback) {
   const uint64_t fsize = src.file_size();
   uint64_t cap_bases = (src.gz() ? 4 * fsize : fsize) + 64;
   if ((rc = c->in_bases.ensure(cap_bases + 16)) || (rc = c->in_offs.ensure(1025))) return rc;
-  DevBuf<uint8_t> &draw = c->ing_draw, &scratch = c->ing_scratch;
+  DevBuf<uint8_t> *draws[2] = {&c->ing_draw, &c->ing_draw2};
+  DevBuf<uint8_t> &scratch = c->ing_scratch;
   DevBuf<IngestState> &dst = c->ing_dst;
-  if ((rc = draw.ensure(chunk)) || (rc = scratch.ensure(ingest_scratch_bytes(chunk))) ||
-      (rc = dst.ensure(1)))
+  if ((rc = draws[0]->ensure(chunk)) || (rc = draws[1]->ensure(chunk)) ||
+      (rc = scratch.ensure(ingest_scratch_bytes(chunk))) || (rc = dst.ensure(1)))
     return rc;
+  // the raw chunks go up on a copy stream into two device buffers, so chunk
+  // c+1's H2D runs beside chunk c's count (on s, one stream: parse and count
+  // stay ordered); the H2D into a buffer waits for the parse that last read it
+  if (!c->ing_cs) {
+    HIPCHK(hipStreamCreateWithFlags(&c->ing_cs, hipStreamNonBlocking));
+    for (hipEvent_t &e : c->ing_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  hipStream_t cs = c->ing_cs;
+  hipEvent_t *ev_copied = c->ing_ev, *ev_parsed = c->ing_ev + 2;
+  bool parsed_once[2] = {false, false};
+  int db = 0;
   IngestState st{};
   st.at_line_start = 1;
   HIPCHK(hipMemcpyAsync(dst.p, &st, sizeof st, hipMemcpyHostToDevice, s));
@@ -2933,15 +2952,25 @@ static int ingest_file(nk_counter *c, const char *path, bool *fallback) {
         no.release();
       }
     }
+    DevBuf<uint8_t> &draw = *draws[db];
     if (len > draw.n) {
       HIPCHK(hipStreamSynchronize(s));
+      HIPCHK(hipStreamSynchronize(cs));
       if ((rc = draw.ensure(len)) || (rc = scratch.ensure(ingest_scratch_bytes(len)))) return rc;
     }
-    HIPCHK(hipMemcpyAsync(draw.p, data, len, hipMemcpyHostToDevice, s));
+    if (parsed_once[db]) HIPCHK(hipStreamWaitEvent(cs, ev_parsed[db], 0));
+    HIPCHK(hipMemcpyAsync(draw.p, data, len, hipMemcpyHostToDevice, cs));
+    HIPCHK(hipEventRecord(ev_copied[db], cs));
+    HIPCHK(hipStreamWaitEvent(s, ev_copied[db], 0));
     IngestBufs ib{c->in_bases.p, c->in_offs.p, c->in_bases.n, c->in_offs.n - 1, scratch.p};
     HIPCHK(fastq ? ingest_fastq(draw.p, len, eof, ib, dst.p, s)
                  : ingest_fasta(draw.p, len, eof, ib, dst.p, s));
+    HIPCHK(hipEventRecord(ev_parsed[db], s));
+    parsed_once[db] = true;
+    db ^= 1;
     HIPCHK(hipMemcpyAsync(&st, dst.p, sizeof st, hipMemcpyDeviceToHost, s));
+    // (the host buffer `data` is free again once this returns: its H2D
+    // preceded the parse on s)
     HIPCHK(hipStreamSynchronize(s));
     if (fastq && st.blank) {
       if (next.valid()) next.get();

@@ -55,8 +55,14 @@ size_t ChunkSource::read(uint8_t *dst, size_t want) {
   }
   // plain file: split the read over threads (page-cache copies run at the
   // memory bandwidth of several cores, one core copies ~5-10 GB/s)
-  const size_t part = (size_t)8 << 20;
-  const int nt = (int)std::min<size_t>(8, (want + part - 1) / part);
+  // up to 16 threads (a one-GPU box's CPU share; 8 read a 10 GB FASTQ from
+  // the page cache at ~24 GB/s, the limiter of config 3, profiles/r04_s2)
+  const size_t part = (size_t)4 << 20;
+  static const int kMaxThreads = [] {
+    const unsigned hc = std::thread::hardware_concurrency();
+    return (int)std::max<unsigned>(1, std::min<unsigned>(16, hc ? hc : 8));
+  }();
+  const int nt = (int)std::min<size_t>((size_t)kMaxThreads, (want + part - 1) / part);
   std::vector<size_t> got(nt > 0 ? nt : 1, 0);
   auto work = [&](int t) {
     const size_t lo = want * t / nt, hi = want * (t + 1) / nt;
