@@ -48,7 +48,7 @@ struct GenShape {
 // (tile, bucket), 16-B stores of 8-record groups (shared by k_part_gen and
 // k_split).  E[j] = bucket << 16 | rank (bucket == nb: no record), O[j] = the
 // record.  Ends the kernel.
-template <bool WIDE, int PER>
+template <bool WIDE, int PER, int BLOCK = kPartBlock>
 __device__ __forceinline__ void sort_and_store(const uint32_t (&E)[PER], const uint32_t (&O)[PER],
                                                uint32_t nb, uint32_t *s_cnt, uint32_t *s_start,
                                                uint32_t *s_base, uint32_t *s_fit,
@@ -80,7 +80,7 @@ __device__ __forceinline__ void sort_and_store(const uint32_t (&E)[PER], const u
     }
     if (tid == 0) s_start[nb] = carry;
   }
-  for (uint32_t b = tid; b < nb; b += kPartBlock) {
+  for (uint32_t b = tid; b < nb; b += BLOCK) {
     const uint32_t c = (s_cnt[b] + 7u) & ~7u;
     uint32_t fit = 0, base = 0;
     if (c) {
@@ -112,7 +112,7 @@ __device__ __forceinline__ void sort_and_store(const uint32_t (&E)[PER], const u
       if (slot < (uint32_t)S::kSlots) s_rec[slot] = (Rec)O[j];  // the no-record bucket may run past
     }
   }
-  for (uint32_t b = tid; b < nb; b += kPartBlock) {
+  for (uint32_t b = tid; b < nb; b += BLOCK) {
     const uint32_t c = s_cnt[b], st = s_start[b], cp = (c + 7u) & ~7u;
     for (uint32_t i = c; i < cp; ++i) s_rec[st + i] = (Rec)S::kPad;
     for (uint32_t g = st >> 3; g < (st + cp) >> 3; ++g) s_gmap[g] = (typename S::GMap)b;
@@ -120,8 +120,8 @@ __device__ __forceinline__ void sort_and_store(const uint32_t (&E)[PER], const u
   __syncthreads();
   const uint32_t n_groups = s_start[nb] >> 3;
 #pragma unroll
-  for (int it = 0; it < S::kGroupIters; ++it) {
-    const uint32_t g = (uint32_t)tid + (uint32_t)it * kPartBlock;
+  for (int it = 0; it < (S::kGroups + BLOCK - 1) / BLOCK; ++it) {
+    const uint32_t g = (uint32_t)tid + (uint32_t)it * BLOCK;
     if (g >= n_groups) break;
     const uint32_t b = s_gmap[g];
     const uint32_t j8 = g * 8 - s_start[b];
@@ -256,7 +256,11 @@ __global__ __launch_bounds__(kPartBlock) void k_part_gen(KmerInput in, int k, Fa
 
 // K1s: one 8192-record tile of a coarse bucket (u32 offsets of 2^S bins) ->
 // its 2^(S-15) fine buckets (u16 offsets), the layout k_bucket_hist reads.
-__global__ __launch_bounds__(kPartBlock) void k_split(GenPartArgs ga, PartArgs pa) {
+// 512 threads x 16 records (256 x 32 needs 119 VGPRs: the same 32 waves of
+// 16-B loads in flight per CU, no gain)
+constexpr int kSplitBlock = kPartBlock;
+constexpr int kSplitPer = kPartTile / kSplitBlock;  // 16
+__global__ __launch_bounds__(kSplitBlock) void k_split(GenPartArgs ga, PartArgs pa) {
   using S = GenShape<false>;
   __shared__ uint32_t s_cnt[kMaxSplit + 1];
   __shared__ uint32_t s_start[kMaxSplit + 1];
@@ -277,21 +281,22 @@ __global__ __launch_bounds__(kPartBlock) void k_split(GenPartArgs ga, PartArgs p
   if (t0 >= n) return;  // uniform
   const uint32_t F = 1u << (ga.bin_bits - kBinBits);
   const uint32_t cmask = (uint32_t)((1ull << ga.bin_bits) - 1ull);
-  for (uint32_t f = tid; f <= F; f += kPartBlock) s_cnt[f] = 0;
+  for (uint32_t f = tid; f <= F; f += kSplitBlock) s_cnt[f] = 0;
   __syncthreads();
   const uint32_t *src = reinterpret_cast<const uint32_t *>(ga.rec) + (uint64_t)cb * ga.cap;
-  // 16 records per lane: four 16-B loads (the region is a multiple of 8 records
-  // and 64-record aligned; records past n are ignored)
-  uint4 v[4];
-  const uint64_t i0 = t0 + (uint64_t)tid * kPer;
+  // 16 records per lane: four 16-B loads (the region is a multiple of 8
+  // records and 64-record aligned; records past n are ignored)
+  constexpr int kL = kSplitPer / 4;
+  uint4 v[kL];
+  const uint64_t i0 = t0 + (uint64_t)tid * kSplitPer;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
+  for (int t = 0; t < kL; ++t) {
     const uint64_t i = i0 + 4 * t;
     v[t] = i < n ? *reinterpret_cast<const uint4 *>(src + i) : make_uint4(~0u, ~0u, ~0u, ~0u);
   }
-  uint32_t E[kPer], O[kPer];
+  uint32_t E[kSplitPer], O[kSplitPer];
 #pragma unroll
-  for (int j = 0; j < kPer; ++j) {
+  for (int j = 0; j < kSplitPer; ++j) {
     const uint4 &w = v[j >> 2];
     const uint32_t o = (j & 3) == 0 ? w.x : (j & 3) == 1 ? w.y : (j & 3) == 2 ? w.z : w.w;
     const bool ok = o != 0xFFFFFFFFu && i0 + j < n;
@@ -299,9 +304,9 @@ __global__ __launch_bounds__(kPartBlock) void k_split(GenPartArgs ga, PartArgs p
     E[j] = (f << 16) | atomicAdd(&s_cnt[f], 1u);
     O[j] = o & (kBinsPerBucket - 1);
   }
-  sort_and_store<false, kPer>(E, O, F, s_cnt, s_start, s_base, s_fit, s_rec, s_gmap, pa.fill,
-                              pa.overflow, pa.cap, pa.off, (uint64_t)cb * F, kBinBits,
-                              pa.currents);
+  sort_and_store<false, kSplitPer, kSplitBlock>(E, O, F, s_cnt, s_start, s_base, s_fit, s_rec, s_gmap,
+                                                pa.fill, pa.overflow, pa.cap, pa.off, (uint64_t)cb * F,
+                                                kBinBits, pa.currents);
 }
 
 // U1g: the tiles that hold records of the top rows in the kept Gen/Wide
@@ -622,7 +627,7 @@ hipError_t launch_split(const GenPartArgs &ga, const PartArgs &pa, hipStream_t s
   if (ga.bin_bits < kBinBits || ga.bin_bits - kBinBits > kMaxSplitBits) return hipErrorInvalidValue;
   const uint64_t tx = (ga.cap + kPartTile - 1) / kPartTile;
   if (tx * ga.n_buckets > 0x7FFFFFFFull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_split, dim3((unsigned)(tx * ga.n_buckets)), dim3(kPartBlock), 0, s, ga, pa);
+  hipLaunchKernelGGL(k_split, dim3((unsigned)(tx * ga.n_buckets)), dim3(kSplitBlock), 0, s, ga, pa);
   return hipGetLastError();
 }
 
