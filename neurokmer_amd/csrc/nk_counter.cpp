@@ -2928,7 +2928,30 @@ static int ingest_file(nk_counter *c, const char *path, bool *fallback) {
   StreamAcc sa;
   if ((rc = acc_begin(c, fastq ? cap_bases / 2 : cap_bases, chunk + room + 64, sa, s))) return rc;
   uint64_t counted = 0;  // windows below this start were counted
+  // NK_INGEST_PROFILE=1: host time per phase, printed to stderr at the end
+  // (parse = H2D + the device parse, waited for; count = the count enqueue;
+  // read = waiting for the reader thread; carry = the FASTQ carry copy)
+  static const bool prof = getenv("NK_INGEST_PROFILE") != nullptr;
+  using clk = std::chrono::steady_clock;
+  double t_parse = 0, t_count = 0, t_read = 0, t_carry = 0;
+  uint64_t n_chunks = 0;
+  auto since = [](clk::time_point a) {
+    return std::chrono::duration<double, std::milli>(clk::now() - a).count();
+  };
+  struct ProfOut {
+    bool on;
+    double *p, *c, *r, *y;
+    uint64_t *n;
+    ~ProfOut() {
+      if (on)
+        fprintf(stderr, "[nk ingest] chunks %llu  parse+H2D %.1f ms  count enqueue %.1f ms  "
+                        "read wait %.1f ms  carry %.1f ms\n",
+                (unsigned long long)*n, *p, *c, *r, *y);
+    }
+  } prof_out{prof, &t_parse, &t_count, &t_read, &t_carry, &n_chunks};
   for (;;) {
+    const clk::time_point t0 = clk::now();
+    ++n_chunks;
     const uint8_t *data = hb[cur].p + start;
     const size_t len = have;
     // capacity of the resident buffers for this chunk (grow: wait, copy, free)
@@ -2972,6 +2995,8 @@ static int ingest_file(nk_counter *c, const char *path, bool *fallback) {
     // (the host buffer `data` is free again once this returns: its H2D
     // preceded the parse on s)
     HIPCHK(hipStreamSynchronize(s));
+    if (prof) t_parse += since(t0);
+    const clk::time_point t1 = clk::now();
     if (fastq && st.blank) {
       if (next.valid()) next.get();
       *fallback = true;
@@ -2991,6 +3016,7 @@ static int ingest_file(nk_counter *c, const char *path, bool *fallback) {
       if ((rc = acc_batch(c, sa, whole, counted, hi, s))) return rc;
       counted = hi;
     }
+    if (prof) t_count += since(t1);
     if (last) {
       if (next.valid()) next.get();
       if ((rc = acc_end(c, sa, whole, s))) return rc;
@@ -2998,7 +3024,10 @@ static int ingest_file(nk_counter *c, const char *path, bool *fallback) {
     }
     // next chunk: the prefetched bytes, behind this chunk's FASTQ carry
     const int nxt = cur ^ 1;
+    const clk::time_point t2 = clk::now();
     const size_t got = next.get();
+    if (prof) t_read += since(t2);
+    const clk::time_point t3 = clk::now();
     const size_t carry = fastq ? len - (size_t)st.consumed : 0;
     size_t nstart = room;
     if (carry) {
@@ -3015,6 +3044,7 @@ static int ingest_file(nk_counter *c, const char *path, bool *fallback) {
         nstart = 0;
       }
     }
+    if (prof) t_carry += since(t3);
     eof = got < chunk;
     cur = nxt;
     start = nstart;
