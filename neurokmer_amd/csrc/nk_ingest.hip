@@ -7,10 +7,15 @@
 // the base counts, the new totals and the carried line state; E per block:
 // scatter of the bases and of the record offsets.
 //
-// FASTQ (the chunk starts at a record boundary): A newline counts; B scan; C
-// newline positions; D per record: the four lines' validity and the sequence
-// length; E one block: first bad record, sequence offsets, new totals; F one
-// wave per record: copy of the sequence bytes.
+// FASTQ (the chunk starts at a record boundary): A newline counts (16-B loads);
+// B scan; C newline positions; D per record: the four lines' validity and the
+// sequence length, the first bad record (atomicMin) and per-1024-record sums
+// of the sequence lengths; E one block: the scan of those sums, the first bad
+// record's block, the new totals; G per 1024 records: the sequence offsets; F
+// one wave per record: copy of the sequence bytes.  (Round 3's E was one block
+// walking every record of the chunk, ~200 k per 64 MB, and A/C loaded bytes one
+// at a time: the parse took ~1.3 ms per 64 MB, the limiter of a streamed 10 GB
+// FASTQ, profiles/r04_s6.)
 #include "nk_ingest.h"
 
 namespace nk {
@@ -242,16 +247,36 @@ struct FqScratch {
   uint32_t *seqlen;          // [records]
   uint8_t *flag;             // [records] 0 ok, 1 bad, 2 blank header
   unsigned long long *pos;   // [records] output offset of the sequence
+  unsigned long long *bsum;  // [record blocks] sum of seqlen -> exclusive prefix
   unsigned long long out_base, rec_base, n_good;
+  unsigned long long first_bad;  // min index of a flagged record (~0: none)
 };
+constexpr int kRecBlock = 1024;  // records per block of the D/G passes
+
+// 0x80 in each byte of t that is '\n'
+__device__ __forceinline__ uint32_t nl_bytes(uint32_t t) {
+  const uint32_t z = t ^ 0x0A0A0A0Au;
+  return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u;
+}
+
+// newlines in the 16 bytes at b0 (one 16-B load when whole and aligned)
+__device__ __forceinline__ uint32_t nl16(const uint8_t *R, uint64_t b0, uint64_t L) {
+  if (b0 + 16 <= L && !((uintptr_t)(R + b0) & 15)) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(R + b0);
+    return __popc(nl_bytes(v.x)) + __popc(nl_bytes(v.y)) + __popc(nl_bytes(v.z)) +
+           __popc(nl_bytes(v.w));
+  }
+  uint32_t n = 0;
+  for (int j = 0; j < kIPer; ++j)
+    if (b0 + j < L) n += R[b0 + j] == '\n';
+  return n;
+}
 
 __global__ __launch_bounds__(kIB) void k_fq_a(const uint8_t *__restrict__ R, uint64_t L,
                                               FqScratch f) {
   __shared__ unsigned long long s_n[kIB / 64];
   const uint64_t b0 = (uint64_t)blockIdx.x * kIS + (uint64_t)threadIdx.x * kIPer;
-  unsigned long long n = 0;
-  for (int j = 0; j < kIPer; ++j)
-    if (b0 + j < L) n += R[b0 + j] == '\n';
+  const unsigned long long n = nl16(R, b0, L);
   unsigned long long tn;
   block_scan_excl<unsigned long long>(n, 0ull, OpAdd(), s_n, &tn);
   if (threadIdx.x == 0) f.nl[blockIdx.x] = tn;
@@ -269,14 +294,25 @@ __global__ __launch_bounds__(kIB) void k_fq_c(const uint8_t *__restrict__ R, uin
                                               FqScratch f) {
   __shared__ unsigned long long s_n[kIB / 64];
   const uint64_t b0 = (uint64_t)blockIdx.x * kIS + (uint64_t)threadIdx.x * kIPer;
+  uint8_t by[kIPer];
+  if (b0 + 16 <= L && !((uintptr_t)(R + b0) & 15)) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(R + b0);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < kIPer; ++j) by[j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+  } else {
+#pragma unroll
+    for (int j = 0; j < kIPer; ++j) by[j] = b0 + j < L ? R[b0 + j] : 0;
+  }
   unsigned long long n = 0;
-  for (int j = 0; j < kIPer; ++j)
-    if (b0 + j < L) n += R[b0 + j] == '\n';
+#pragma unroll
+  for (int j = 0; j < kIPer; ++j) n += by[j] == '\n';
   unsigned long long tn;
   unsigned long long at = block_scan_excl<unsigned long long>(n, 0ull, OpAdd(), s_n, &tn);
   at += f.nl[blockIdx.x];
+#pragma unroll
   for (int j = 0; j < kIPer; ++j)
-    if (b0 + j < L && R[b0 + j] == '\n') f.nlpos[at++] = (uint32_t)(b0 + j);
+    if (by[j] == '\n') f.nlpos[at++] = (uint32_t)(b0 + j);
 }
 
 // line l of the chunk: [start, end) without its '\n'
@@ -286,11 +322,17 @@ __device__ __forceinline__ void fq_line(const FqScratch &f, uint64_t l, uint64_t
   *e = l < nl_total ? (uint64_t)f.nlpos[l] : L;
 }
 
-__global__ void k_fq_d(const uint8_t *__restrict__ R, uint64_t L, uint64_t n_rec,
-                       const unsigned long long *__restrict__ nl_total_p, FqScratch f) {
+// one thread per record: validity, sequence length; per block of kRecBlock
+// records the sum of the lengths (bsum) and the first flagged record
+__global__ __launch_bounds__(kRecBlock) void k_fq_d(const uint8_t *__restrict__ R, uint64_t L,
+                                                    uint64_t n_rec,
+                                                    const unsigned long long *__restrict__ nl_total_p,
+                                                    FqScratch *__restrict__ fs, FqScratch f) {
+  __shared__ unsigned long long s_w[kRecBlock / 64];
   const uint64_t nl_total = *nl_total_p;
-  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_rec;
-       r += (uint64_t)gridDim.x * blockDim.x) {
+  const uint64_t r = (uint64_t)blockIdx.x * kRecBlock + threadIdx.x;
+  uint32_t len = 0;
+  if (r < n_rec) {
     uint64_t s[4], e[4];
     for (int q = 0; q < 4; ++q) {
       fq_line(f, 4 * r + q, nl_total, L, &s[q], &e[q]);
@@ -302,41 +344,37 @@ __global__ void k_fq_d(const uint8_t *__restrict__ R, uint64_t L, uint64_t n_rec
     else if (e[2] == s[2] || R[s[2]] != '+') fl = 1;       // '+' line missing or empty
     else if (e[3] - s[3] != e[1] - s[1]) fl = 1;           // quality length != sequence
     f.flag[r] = fl;
-    f.seqlen[r] = (uint32_t)(e[1] - s[1]);
+    len = (uint32_t)(e[1] - s[1]);
+    f.seqlen[r] = len;
+    if (fl) atomicMin(&fs->first_bad, (unsigned long long)r);
   }
+  unsigned long long tot;
+  block_scan_excl<unsigned long long>((unsigned long long)len, 0ull, OpAdd(), s_w, &tot);
+  if (threadIdx.x == 0) f.bsum[blockIdx.x] = tot;
 }
 
-__global__ __launch_bounds__(kScanT) void k_fq_e(uint64_t n_rec, bool eof, uint64_t L,
+// one block: the first bad record fixes the good prefix; the record blocks'
+// length sums scanned; the totals of the chunk's good records
+__global__ __launch_bounds__(kScanT) void k_fq_e(uint64_t n_rec, uint64_t L,
                                                  const unsigned long long *__restrict__ nl_total_p,
                                                  IngestState *__restrict__ st,
                                                  FqScratch *__restrict__ fs,
                                                  uint64_t *__restrict__ offsets) {
   __shared__ unsigned long long s_w[kScanT / 64];
-  __shared__ unsigned long long s_first;
-  if (threadIdx.x == 0) s_first = n_rec;
-  __syncthreads();
   const FqScratch f = *fs;
-  const uint64_t per = (n_rec + kScanT - 1) / kScanT;
-  const uint64_t lo = threadIdx.x * per, hi = lo + per < n_rec ? lo + per : n_rec;
-  for (uint64_t r = lo; r < hi; ++r)
-    if (f.flag[r]) {
-      atomicMin(&s_first, (unsigned long long)r);
-      break;
-    }
-  __syncthreads();
-  const uint64_t ng = s_first;
-  // exclusive scan of the sequence lengths of the good records
-  unsigned long long loc = 0;
-  for (uint64_t r = lo; r < hi && r < ng; ++r) loc += f.seqlen[r];
-  unsigned long long tot;
-  unsigned long long run = block_scan_excl<unsigned long long>(loc, 0ull, OpAdd(), s_w, &tot);
-  IngestState S = *st;
-  for (uint64_t r = lo; r < hi && r < ng; ++r) {
-    f.pos[r] = S.data_end + run;
-    offsets[S.n_rec + r] = S.data_end + run;
-    run += f.seqlen[r];
-  }
+  const uint64_t ng = f.first_bad < n_rec ? f.first_bad : n_rec;
+  const uint64_t nrb = (n_rec + kRecBlock - 1) / kRecBlock;
+  unsigned long long tn;
+  scan_array_excl<unsigned long long>(f.bsum, nrb, 0ull, OpAdd(), s_w, &tn);
+  // the good records' total: the blocks before ng's, plus ng's block up to ng
+  const uint64_t gb = ng / kRecBlock;
+  unsigned long long part = 0;
+  for (uint64_t r = gb * kRecBlock + threadIdx.x; r < ng; r += kScanT) part += f.seqlen[r];
+  unsigned long long ptot;
+  block_scan_excl<unsigned long long>(part, 0ull, OpAdd(), s_w, &ptot);
   if (threadIdx.x != 0) return;
+  const unsigned long long tot = (gb < nrb ? f.bsum[gb] : tn) + ptot;
+  IngestState S = *st;
   const uint64_t nl_total = *nl_total_p;
   fs->out_base = S.data_end;
   fs->rec_base = S.n_rec;
@@ -352,9 +390,27 @@ __global__ __launch_bounds__(kScanT) void k_fq_e(uint64_t n_rec, bool eof, uint6
   S.consumed = ng == 0 ? 0 : (last_nl <= nl_total ? (uint64_t)f.nlpos[last_nl - 1] + 1 : L);
   *st = S;
   offsets[S.n_rec] = S.data_end;
-  (void)eof;
 }
 
+// per block of kRecBlock records: the good records' output offsets
+__global__ __launch_bounds__(kRecBlock) void k_fq_g(uint64_t n_rec, const FqScratch *__restrict__ fs,
+                                                    uint64_t *__restrict__ offsets) {
+  __shared__ unsigned long long s_w[kRecBlock / 64];
+  const FqScratch f = *fs;
+  const uint64_t r = (uint64_t)blockIdx.x * kRecBlock + threadIdx.x;
+  const uint64_t ng = f.n_good;
+  if ((uint64_t)blockIdx.x * kRecBlock >= ng) return;  // uniform
+  const unsigned long long len = r < ng ? f.seqlen[r] : 0ull;
+  unsigned long long tot;
+  const unsigned long long at = block_scan_excl<unsigned long long>(len, 0ull, OpAdd(), s_w, &tot) +
+                                f.bsum[blockIdx.x] + f.out_base;
+  if (r < ng) {
+    f.pos[r] = at;
+    offsets[f.rec_base + r] = at;
+  }
+}
+
+// one wave per record: the sequence bytes to their resident offset
 __global__ void k_fq_f(const uint8_t *__restrict__ R, uint64_t L,
                        const unsigned long long *__restrict__ nl_total_p,
                        const FqScratch *__restrict__ fs, uint8_t *__restrict__ bases) {
@@ -379,7 +435,8 @@ size_t ingest_scratch_bytes(size_t chunk_cap) {
   const size_t NB = (chunk_cap + kIS - 1) / kIS + 1;
   const size_t fa = NB * (8 + 8 + 8) + sizeof(FaScratch);
   const size_t recs = chunk_cap / 4 + 2;
-  const size_t fq = NB * 8 + (chunk_cap + 1) * 4 + recs * (4 + 1 + 8) + sizeof(FqScratch) + 64;
+  const size_t fq = NB * 8 + (chunk_cap + 1) * 4 + recs * (4 + 1 + 8) + (recs / kRecBlock + 2) * 8 +
+                    sizeof(FqScratch) + 64 + 64;
   return (fa > fq ? fa : fq) + 1024;
 }
 
@@ -431,9 +488,12 @@ hipError_t ingest_fastq(const uint8_t *raw, size_t len, bool eof, const IngestBu
   const uint64_t max_rec = len / 4 + 2;
   f.pos = (unsigned long long *)p;
   p += max_rec * 8;
+  f.bsum = (unsigned long long *)p;
+  p += (max_rec / kRecBlock + 2) * 8;
   f.seqlen = (uint32_t *)p;
   p += max_rec * 4;
   f.flag = (uint8_t *)p;
+  f.first_bad = ~0ull;
   hipError_t e = hipMemcpyAsync(fs, &f, sizeof f, hipMemcpyHostToDevice, s);
   if (e != hipSuccess) return e;
   // newline count first: the number of candidate records follows from it
@@ -454,13 +514,14 @@ hipError_t ingest_fastq(const uint8_t *raw, size_t len, bool eof, const IngestBu
   }
   const uint64_t n_rec = lines / 4;  // complete 4-line records
   hipLaunchKernelGGL(k_fq_c, dim3((unsigned)NB), dim3(kIB), 0, s, raw, (uint64_t)len, f);
+  const uint64_t nrb = (n_rec + kRecBlock - 1) / kRecBlock;
+  if (n_rec)
+    hipLaunchKernelGGL(k_fq_d, dim3((unsigned)nrb), dim3(kRecBlock), 0, s, raw, (uint64_t)len, n_rec,
+                       nl_total, fs, f);
+  hipLaunchKernelGGL(k_fq_e, dim3(1), dim3(kScanT), 0, s, n_rec, (uint64_t)len, nl_total, st, fs,
+                     bufs.offsets);
   if (n_rec) {
-    const unsigned g = (unsigned)((n_rec + 255) / 256 < 65535 ? (n_rec + 255) / 256 : 65535);
-    hipLaunchKernelGGL(k_fq_d, dim3(g), dim3(256), 0, s, raw, (uint64_t)len, n_rec, nl_total, f);
-  }
-  hipLaunchKernelGGL(k_fq_e, dim3(1), dim3(kScanT), 0, s, n_rec, eof, (uint64_t)len, nl_total,
-                     st, fs, bufs.offsets);
-  if (n_rec) {
+    hipLaunchKernelGGL(k_fq_g, dim3((unsigned)nrb), dim3(kRecBlock), 0, s, n_rec, fs, bufs.offsets);
     const uint64_t waves = n_rec < 65536 ? n_rec : 65536;
     hipLaunchKernelGGL(k_fq_f, dim3((unsigned)((waves * 64 + 255) / 256)), dim3(256), 0, s, raw,
                        (uint64_t)len, nl_total, fs, bufs.bases);
