@@ -161,11 +161,11 @@ struct nk_counter {
   DevBuf<uint8_t> in_bases;
   DevBuf<uint64_t> in_offs;
   // GPU FASTX ingest buffers, kept between file calls
-  PinnedBuf ing_hb[2];
+  PinnedBuf ing_hb[3];                    // chunk i of a file in ing_hb[i % 3]
   DevBuf<uint8_t> ing_draw, ing_scratch;
   DevBuf<uint8_t> ing_draw2;              // the second raw-chunk buffer (H2D of the next chunk)
   hipStream_t ing_cs = nullptr;           // the ingest's copy stream
-  hipEvent_t ing_ev[4] = {};              // copied[0..1], parsed[0..1]
+  hipEvent_t ing_ev[4] = {};              // copied[0..1], free[0..1]
   DevBuf<IngestState> ing_dst;
   // LIF table cache key
   bool lif_valid = false;
@@ -623,7 +623,8 @@ void nk_free(nk_counter *c) {
   c->span.release();
   c->rk_keys.release(); c->rk_idx.release(); c->rk_tmp.release(); c->rk_cand.release();
   c->rk_uniq.release();
-  c->ing_hb[0].release(); c->ing_hb[1].release(); c->ing_draw.release();
+  for (PinnedBuf &b : c->ing_hb) b.release();
+  c->ing_draw.release();
   c->ing_draw2.release(); c->ing_scratch.release(); c->ing_dst.release();
   if (c->ing_cs) (void)hipStreamSynchronize(c->ing_cs);
   for (hipEvent_t &e : c->ing_ev)
@@ -2879,49 +2880,68 @@ static int ingest_file(nk_counter *c, const char *path, bool *fallback) {
   if (rc) return fail(rc, "%s", err.c_str());
   (void)hipSetDevice(c->device);
   hipStream_t s = pick_stream(c, nullptr);
-  // two pinned host buffers: [room for a FASTQ carry | chunk]; the reader
-  // thread fills one while the device copies and parses the other
+  // Three stages overlap: the reader thread fills pinned host buffer (c+2) % 3
+  // with chunk c+2 while the copy stream moves chunk c+1 up and the count
+  // stream parses and counts chunk c.  A FASTQ chunk's unfinished last record
+  // (the carry) is copied on the device in front of the next chunk's bytes.
   size_t chunk = ingest_chunk_bytes();
   size_t room = std::max<size_t>(chunk / 8, 1 << 16);
-  // (kept by the handle: pinning ~150 MB of host memory per call cost more
+  // (kept by the handle: pinning ~200 MB of host memory per call cost more
   // than reading a 100 MB file from the page cache)
   PinnedBuf *hb = c->ing_hb;
-  if ((rc = hb[0].ensure(room + chunk)) || (rc = hb[1].ensure(room + chunk))) return rc;
-  int cur = 0;
-  size_t start = room, have = src.read(hb[0].p + room, chunk);
+  for (int i = 0; i < 3; ++i)
+    if ((rc = hb[i].ensure(chunk))) return rc;
+  size_t have = src.read(hb[0].p, chunk);
   bool eof = have < chunk;
   if (!have) return fail(NK_E_PARSE, "empty file");
-  const bool fastq = hb[0].p[room] == '@';
-  if (hb[0].p[room] != '>' && !fastq)
+  const bool fastq = hb[0].p[0] == '@';
+  if (hb[0].p[0] != '>' && !fastq)
     return fail(NK_E_PARSE, "unknown format: first byte is neither '>' nor '@'");
   std::future<size_t> next;
   auto prefetch = [&](int b) {
-    next = std::async(std::launch::async, [&src, hb, b, room, chunk] {
-      return src.read(hb[b].p + room, chunk);
-    });
+    next = std::async(std::launch::async, [&src, hb, b, chunk] { return src.read(hb[b].p, chunk); });
   };
   if (!eof) prefetch(1);
   // resident input: the file size bounds the bases of a plain file
   const uint64_t fsize = src.file_size();
   uint64_t cap_bases = (src.gz() ? 4 * fsize : fsize) + 64;
   if ((rc = c->in_bases.ensure(cap_bases + 16)) || (rc = c->in_offs.ensure(1025))) return rc;
+  // device chunk buffers: [room for the carry | chunk | 16 B the parse's
+  // aligned 16-B groups may read past the end]
   DevBuf<uint8_t> *draws[2] = {&c->ing_draw, &c->ing_draw2};
   DevBuf<uint8_t> &scratch = c->ing_scratch;
   DevBuf<IngestState> &dst = c->ing_dst;
-  if ((rc = draws[0]->ensure(chunk)) || (rc = draws[1]->ensure(chunk)) ||
-      (rc = scratch.ensure(ingest_scratch_bytes(chunk))) || (rc = dst.ensure(1)))
+  if ((rc = draws[0]->ensure(room + chunk + 16)) || (rc = draws[1]->ensure(room + chunk + 16)) ||
+      (rc = scratch.ensure(ingest_scratch_bytes(room + chunk))) || (rc = dst.ensure(1)))
     return rc;
-  // the raw chunks go up on a copy stream into two device buffers, so chunk
-  // c+1's H2D runs beside chunk c's count (on s, one stream: parse and count
-  // stay ordered); the H2D into a buffer waits for the parse that last read it
   if (!c->ing_cs) {
     HIPCHK(hipStreamCreateWithFlags(&c->ing_cs, hipStreamNonBlocking));
     for (hipEvent_t &e : c->ing_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
   hipStream_t cs = c->ing_cs;
-  hipEvent_t *ev_copied = c->ing_ev, *ev_parsed = c->ing_ev + 2;
-  bool parsed_once[2] = {false, false};
-  int db = 0;
+  hipEvent_t *ev_copied = c->ing_ev, *ev_free = c->ing_ev + 2;
+  // every exit leaves no copy in flight into the handle's buffers
+  struct CsDrain {
+    hipStream_t cs;
+    std::future<size_t> *next;
+    ~CsDrain() {
+      (void)hipStreamSynchronize(cs);
+      if (next->valid()) next->wait();
+    }
+  } drain{cs, &next};
+  bool used[2] = {false, false};
+  // chunk bytes -> draws[b] + room on the copy stream, once the carry out of
+  // that buffer and its parse are done
+  auto upload = [&](int b, const uint8_t *h, size_t n) -> int {
+    if (used[b]) HIPCHK(hipStreamWaitEvent(cs, ev_free[b], 0));
+    HIPCHK(hipMemcpyAsync(draws[b]->p + room, h, n, hipMemcpyHostToDevice, cs));
+    HIPCHK(hipEventRecord(ev_copied[b], cs));
+    return NK_OK;
+  };
+  if ((rc = upload(0, hb[0].p, have))) return rc;
+  int db = 0;        // the device buffer of this chunk
+  uint64_t ci = 0;   // this chunk's number (host buffer ci % 3)
+  size_t carry = 0;  // bytes of the previous chunk in front of this one
   IngestState st{};
   st.at_line_start = 1;
   HIPCHK(hipMemcpyAsync(dst.p, &st, sizeof st, hipMemcpyHostToDevice, s));
@@ -2929,8 +2949,8 @@ static int ingest_file(nk_counter *c, const char *path, bool *fallback) {
   if ((rc = acc_begin(c, fastq ? cap_bases / 2 : cap_bases, chunk + room + 64, sa, s))) return rc;
   uint64_t counted = 0;  // windows below this start were counted
   // NK_INGEST_PROFILE=1: host time per phase, printed to stderr at the end
-  // (parse = H2D + the device parse, waited for; count = the count enqueue;
-  // read = waiting for the reader thread; carry = the FASTQ carry copy)
+  // (parse = the device parse, waited for; count = the count enqueue; read =
+  // waiting for the reader thread; carry = the carry copy's enqueue)
   static const bool prof = getenv("NK_INGEST_PROFILE") != nullptr;
   using clk = std::chrono::steady_clock;
   double t_parse = 0, t_count = 0, t_read = 0, t_carry = 0;
@@ -2944,16 +2964,24 @@ static int ingest_file(nk_counter *c, const char *path, bool *fallback) {
     uint64_t *n;
     ~ProfOut() {
       if (on)
-        fprintf(stderr, "[nk ingest] chunks %llu  parse+H2D %.1f ms  count enqueue %.1f ms  "
+        fprintf(stderr, "[nk ingest] chunks %llu  parse %.1f ms  count enqueue %.1f ms  "
                         "read wait %.1f ms  carry %.1f ms\n",
                 (unsigned long long)*n, *p, *c, *r, *y);
     }
   } prof_out{prof, &t_parse, &t_count, &t_read, &t_carry, &n_chunks};
   for (;;) {
-    const clk::time_point t0 = clk::now();
     ++n_chunks;
-    const uint8_t *data = hb[cur].p + start;
-    const size_t len = have;
+    // the next chunk: wait for its bytes, send them up, start reading the one after
+    size_t got = 0;
+    if (!eof) {
+      const clk::time_point t2 = clk::now();
+      got = next.get();
+      if (prof) t_read += since(t2);
+      if ((rc = upload(db ^ 1, hb[(ci + 1) % 3].p, got))) return rc;
+      if (got == chunk) prefetch((int)((ci + 2) % 3));  // chunk ci - 1's buffer: its H2D is done
+    }
+    const clk::time_point t0 = clk::now();
+    const size_t len = carry + have;
     // capacity of the resident buffers for this chunk (grow: wait, copy, free)
     const uint64_t need_b = st.data_end + len + 64, need_r = st.n_rec + len / 2 + 4;
     if (need_b > c->in_bases.n || need_r + 1 > c->in_offs.n) {
@@ -2975,41 +3003,59 @@ static int ingest_file(nk_counter *c, const char *path, bool *fallback) {
         no.release();
       }
     }
-    DevBuf<uint8_t> &draw = *draws[db];
-    if (len > draw.n) {
-      HIPCHK(hipStreamSynchronize(s));
-      HIPCHK(hipStreamSynchronize(cs));
-      if ((rc = draw.ensure(len)) || (rc = scratch.ensure(ingest_scratch_bytes(len)))) return rc;
-    }
-    if (parsed_once[db]) HIPCHK(hipStreamWaitEvent(cs, ev_parsed[db], 0));
-    HIPCHK(hipMemcpyAsync(draw.p, data, len, hipMemcpyHostToDevice, cs));
-    HIPCHK(hipEventRecord(ev_copied[db], cs));
+    const uint8_t *raw = draws[db]->p + room - carry;
     HIPCHK(hipStreamWaitEvent(s, ev_copied[db], 0));
     IngestBufs ib{c->in_bases.p, c->in_offs.p, c->in_bases.n, c->in_offs.n - 1, scratch.p};
-    HIPCHK(fastq ? ingest_fastq(draw.p, len, eof, ib, dst.p, s)
-                 : ingest_fasta(draw.p, len, eof, ib, dst.p, s));
-    HIPCHK(hipEventRecord(ev_parsed[db], s));
-    parsed_once[db] = true;
-    db ^= 1;
+    HIPCHK(fastq ? ingest_fastq(raw, len, eof, ib, dst.p, s) : ingest_fasta(raw, len, eof, ib, dst.p, s));
     HIPCHK(hipMemcpyAsync(&st, dst.p, sizeof st, hipMemcpyDeviceToHost, s));
-    // (the host buffer `data` is free again once this returns: its H2D
-    // preceded the parse on s)
     HIPCHK(hipStreamSynchronize(s));
     if (prof) t_parse += since(t0);
-    const clk::time_point t1 = clk::now();
     if (fastq && st.blank) {
-      if (next.valid()) next.get();
       *fallback = true;
       return NK_OK;
     }
+    // the carry goes in front of the next chunk's bytes (they sit at + room);
+    // enqueued before this chunk's count so the next H2D into this buffer can start
+    const bool last = eof || st.stop;
+    size_t nc = 0;
+    if (!last) {
+      const clk::time_point t3 = clk::now();
+      nc = fastq ? len - (size_t)st.consumed : 0;
+      const uint8_t *from = raw + st.consumed;
+      if (nc > room) {  // a record longer than the carry room: regrow both buffers
+        HIPCHK(hipStreamSynchronize(cs));
+        HIPCHK(hipStreamSynchronize(s));
+        const size_t nroom = 2 * nc;
+        DevBuf<uint8_t> nb[2];
+        if ((rc = nb[0].ensure(nroom + chunk + 16)) || (rc = nb[1].ensure(nroom + chunk + 16)) ||
+            (rc = scratch.ensure(ingest_scratch_bytes(nroom + chunk))))
+          return rc;
+        HIPCHK(hipMemcpy(nb[db ^ 1].p + nroom, draws[db ^ 1]->p + room, got, hipMemcpyDeviceToDevice));
+        HIPCHK(hipMemcpy(nb[db ^ 1].p + nroom - nc, from, nc, hipMemcpyDeviceToDevice));
+        for (int i = 0; i < 2; ++i) {
+          std::swap(nb[i].p, draws[i]->p);
+          std::swap(nb[i].n, draws[i]->n);
+          nb[i].release();
+        }
+        room = nroom;
+        used[0] = used[1] = false;
+        HIPCHK(hipEventRecord(ev_copied[db ^ 1], s));
+      } else {
+        if (nc)
+          HIPCHK(hipMemcpyAsync(draws[db ^ 1]->p + room - nc, from, nc, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipEventRecord(ev_free[db], s));  // this buffer's parse and carry are done
+        used[db] = true;
+      }
+      if (prof) t_carry += since(t3);
+    }
     // count what is complete: every window of a FASTQ chunk's records (they
     // are whole); FASTA: windows that end inside the bases parsed so far
+    const clk::time_point t1 = clk::now();
     KmerInput whole{};
     whole.bases = c->in_bases.p;
     whole.offsets = c->in_offs.p;
     whole.n_recs = st.n_rec;
     whole.n_bases = st.data_end;
-    const bool last = eof || st.stop;
     uint64_t hi = st.data_end;
     if (!fastq && !last) hi = st.data_end >= c->k - 1 ? st.data_end - (c->k - 1) : 0;
     if (st.n_rec && hi > counted) {
@@ -3018,38 +3064,14 @@ static int ingest_file(nk_counter *c, const char *path, bool *fallback) {
     }
     if (prof) t_count += since(t1);
     if (last) {
-      if (next.valid()) next.get();
       if ((rc = acc_end(c, sa, whole, s))) return rc;
       break;
     }
-    // next chunk: the prefetched bytes, behind this chunk's FASTQ carry
-    const int nxt = cur ^ 1;
-    const clk::time_point t2 = clk::now();
-    const size_t got = next.get();
-    if (prof) t_read += since(t2);
-    const clk::time_point t3 = clk::now();
-    const size_t carry = fastq ? len - (size_t)st.consumed : 0;
-    size_t nstart = room;
-    if (carry) {
-      if (carry <= room) {
-        nstart = room - carry;
-        memcpy(hb[nxt].p + nstart, data + st.consumed, carry);
-      } else {  // a record longer than the carry room: grow both buffers
-        std::vector<uint8_t> cv(data + st.consumed, data + len);
-        std::vector<uint8_t> tmp(hb[nxt].p + room, hb[nxt].p + room + got);
-        room = carry;
-        if ((rc = hb[nxt].ensure(room + chunk)) || (rc = hb[cur].ensure(room + chunk))) return rc;
-        memcpy(hb[nxt].p, cv.data(), carry);
-        memcpy(hb[nxt].p + room, tmp.data(), got);
-        nstart = 0;
-      }
-    }
-    if (prof) t_carry += since(t3);
+    db ^= 1;
+    ++ci;
+    carry = nc;
+    have = got;
     eof = got < chunk;
-    cur = nxt;
-    start = nstart;
-    have = carry + got;
-    if (!eof) prefetch(cur ^ 1);
   }
   return NK_OK;
 }

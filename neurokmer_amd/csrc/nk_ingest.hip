@@ -253,30 +253,33 @@ struct FqScratch {
 };
 constexpr int kRecBlock = 1024;  // records per block of the D/G passes
 
-// 0x80 in each byte of t that is '\n'
-__device__ __forceinline__ uint32_t nl_bytes(uint32_t t) {
-  const uint32_t z = t ^ 0x0A0A0A0Au;
-  return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u;
-}
-
-// newlines in the 16 bytes at b0 (one 16-B load when whole and aligned)
-__device__ __forceinline__ uint32_t nl16(const uint8_t *R, uint64_t b0, uint64_t L) {
-  if (b0 + 16 <= L && !((uintptr_t)(R + b0) & 15)) {
-    const uint4 v = *reinterpret_cast<const uint4 *>(R + b0);
-    return __popc(nl_bytes(v.x)) + __popc(nl_bytes(v.y)) + __popc(nl_bytes(v.z)) +
-           __popc(nl_bytes(v.w));
+// The newline passes read the chunk as 16-B groups aligned in memory (the
+// chunk may start anywhere: a FASTQ carry is copied in front of the new data
+// on the device): group g covers bytes [16 g - head, 16 g - head + 16) of the
+// chunk, head = its start's offset in its 16-B line; bytes outside [0, L) are
+// masked.  The buffer holds >= 16 readable bytes past the chunk.
+__device__ __forceinline__ void load_group(const uint8_t *R, uint64_t L, uint32_t head, uint64_t g,
+                                           uint8_t (&by)[kIPer]) {
+  const uint4 v = *reinterpret_cast<const uint4 *>(R - head + 16 * g);
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < kIPer; ++j) {
+    const long long i = (long long)(16 * g + j) - (long long)head;
+    by[j] = (i >= 0 && (uint64_t)i < L) ? (uint8_t)(w[j >> 2] >> (8 * (j & 3))) : (uint8_t)0;
   }
-  uint32_t n = 0;
-  for (int j = 0; j < kIPer; ++j)
-    if (b0 + j < L) n += R[b0 + j] == '\n';
-  return n;
 }
 
 __global__ __launch_bounds__(kIB) void k_fq_a(const uint8_t *__restrict__ R, uint64_t L,
-                                              FqScratch f) {
+                                              uint32_t head, FqScratch f) {
   __shared__ unsigned long long s_n[kIB / 64];
-  const uint64_t b0 = (uint64_t)blockIdx.x * kIS + (uint64_t)threadIdx.x * kIPer;
-  const unsigned long long n = nl16(R, b0, L);
+  const uint64_t g = (uint64_t)blockIdx.x * kIB + threadIdx.x;
+  unsigned long long n = 0;
+  if (16 * g < L + head) {
+    uint8_t by[kIPer];
+    load_group(R, L, head, g, by);
+#pragma unroll
+    for (int j = 0; j < kIPer; ++j) n += by[j] == '\n';
+  }
   unsigned long long tn;
   block_scan_excl<unsigned long long>(n, 0ull, OpAdd(), s_n, &tn);
   if (threadIdx.x == 0) f.nl[blockIdx.x] = tn;
@@ -291,18 +294,15 @@ __global__ __launch_bounds__(kScanT) void k_fq_b(uint64_t NB, FqScratch f,
 }
 
 __global__ __launch_bounds__(kIB) void k_fq_c(const uint8_t *__restrict__ R, uint64_t L,
-                                              FqScratch f) {
+                                              uint32_t head, FqScratch f) {
   __shared__ unsigned long long s_n[kIB / 64];
-  const uint64_t b0 = (uint64_t)blockIdx.x * kIS + (uint64_t)threadIdx.x * kIPer;
+  const uint64_t g = (uint64_t)blockIdx.x * kIB + threadIdx.x;
   uint8_t by[kIPer];
-  if (b0 + 16 <= L && !((uintptr_t)(R + b0) & 15)) {
-    const uint4 v = *reinterpret_cast<const uint4 *>(R + b0);
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int j = 0; j < kIPer; ++j) by[j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+  if (16 * g < L + head) {
+    load_group(R, L, head, g, by);
   } else {
 #pragma unroll
-    for (int j = 0; j < kIPer; ++j) by[j] = b0 + j < L ? R[b0 + j] : 0;
+    for (int j = 0; j < kIPer; ++j) by[j] = 0;
   }
   unsigned long long n = 0;
 #pragma unroll
@@ -312,7 +312,7 @@ __global__ __launch_bounds__(kIB) void k_fq_c(const uint8_t *__restrict__ R, uin
   at += f.nl[blockIdx.x];
 #pragma unroll
   for (int j = 0; j < kIPer; ++j)
-    if (by[j] == '\n') f.nlpos[at++] = (uint32_t)(b0 + j);
+    if (by[j] == '\n') f.nlpos[at++] = (uint32_t)(16 * g + j - head);
 }
 
 // line l of the chunk: [start, end) without its '\n'
@@ -432,7 +432,7 @@ unsigned blocks_for(uint64_t L) { return (unsigned)((L + kIS - 1) / kIS); }
 }  // namespace
 
 size_t ingest_scratch_bytes(size_t chunk_cap) {
-  const size_t NB = (chunk_cap + kIS - 1) / kIS + 1;
+  const size_t NB = (chunk_cap + 16 + kIS - 1) / kIS + 1;
   const size_t fa = NB * (8 + 8 + 8) + sizeof(FaScratch);
   const size_t recs = chunk_cap / 4 + 2;
   const size_t fq = NB * 8 + (chunk_cap + 1) * 4 + recs * (4 + 1 + 8) + (recs / kRecBlock + 2) * 8 +
@@ -473,7 +473,8 @@ hipError_t ingest_fasta(const uint8_t *raw, size_t len, bool eof, const IngestBu
 
 hipError_t ingest_fastq(const uint8_t *raw, size_t len, bool eof, const IngestBufs &bufs,
                         IngestState *st, hipStream_t s) {
-  const uint64_t NB = blocks_for(len ? len : 1);
+  const uint32_t head = (uint32_t)((uintptr_t)raw & 15);
+  const uint64_t NB = blocks_for(len + head ? len + head : 1);
   uint8_t *p = (uint8_t *)bufs.scratch;
   FqScratch *fs = (FqScratch *)p;
   p += 256;
@@ -497,7 +498,7 @@ hipError_t ingest_fastq(const uint8_t *raw, size_t len, bool eof, const IngestBu
   hipError_t e = hipMemcpyAsync(fs, &f, sizeof f, hipMemcpyHostToDevice, s);
   if (e != hipSuccess) return e;
   // newline count first: the number of candidate records follows from it
-  hipLaunchKernelGGL(k_fq_a, dim3((unsigned)NB), dim3(kIB), 0, s, raw, (uint64_t)len, f);
+  hipLaunchKernelGGL(k_fq_a, dim3((unsigned)NB), dim3(kIB), 0, s, raw, (uint64_t)len, head, f);
   hipLaunchKernelGGL(k_fq_b, dim3(1), dim3(kScanT), 0, s, NB, f, nl_total);
   unsigned long long nl = 0;
   e = hipMemcpyAsync(&nl, nl_total, 8, hipMemcpyDeviceToHost, s);
@@ -513,7 +514,7 @@ hipError_t ingest_fastq(const uint8_t *raw, size_t len, bool eof, const IngestBu
     if (last != '\n') ++lines;
   }
   const uint64_t n_rec = lines / 4;  // complete 4-line records
-  hipLaunchKernelGGL(k_fq_c, dim3((unsigned)NB), dim3(kIB), 0, s, raw, (uint64_t)len, f);
+  hipLaunchKernelGGL(k_fq_c, dim3((unsigned)NB), dim3(kIB), 0, s, raw, (uint64_t)len, head, f);
   const uint64_t nrb = (n_rec + kRecBlock - 1) / kRecBlock;
   if (n_rec)
     hipLaunchKernelGGL(k_fq_d, dim3((unsigned)nrb), dim3(kRecBlock), 0, s, raw, (uint64_t)len, n_rec,

@@ -714,6 +714,22 @@ def test_ingest_fastq_chunks(tmp_path, chunk, streaming):
     assert len(recs) == 403
 
 
+def test_ingest_fastq_record_longer_than_carry_room(tmp_path):
+    """A FASTQ record (~300 KB with its quality line) far past the carry room
+    in front of a device chunk buffer (max(chunk / 8, 64 KB)): the buffers
+    regrow, several times, while the next chunk's bytes are already up."""
+    reads, roffs = synth.make_reads(300, 150, seed=15, n_rate=0.005)
+    longr, loffs = synth.make_reads(2, 150_000, seed=16, n_rate=0.001)
+    allr = np.concatenate([reads[:int(roffs[100])], longr, reads[int(roffs[100]):]])
+    lens = np.concatenate([np.diff(roffs)[:100], np.diff(loffs), np.diff(roffs)[100:]])
+    offs = np.zeros(lens.size + 1, np.uint64)
+    np.cumsum(lens, out=offs[1:])
+    p = tmp_path / "long.fq"
+    synth.write_fastq(str(p), allr, offs)
+    recs = _ingest_check(str(p), 25, 6007, True, True, 50_001)
+    assert len(recs) == 302
+
+
 def test_ingest_fastq_stops_at_malformed_record(tmp_path):
     reads, roffs = synth.make_reads(300, 120, seed=7)
     p = tmp_path / "bad.fq"
