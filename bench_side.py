@@ -370,10 +370,14 @@ def _config3_run(args, path, fsize, n_reads, nk, k, pool, L, dev, Counter, synth
                        "page_cache_read_1thread_gb_per_s": round(read_gbps, 2),
                        "resident_step_ms": round(float(np.median(tot)), 3),
                        "resident_mkmers_per_s": round(nk / (float(np.median(tot)) * 1e-3) / 1e6, 1),
-                       "limiter": ("the file path: H2D of the FASTQ bytes + the device parse "
-                                   "(the step is %.1fx the resident count + LIF; the file moves "
-                                   "%.1fx the bases)" % (t * 1e3 / float(np.median(tot)),
-                                                         fsize / n_b))},
+                       "pcie_floor_ms": round(fsize / h2d * 1e3, 1),
+                       "limiter": ("the file path: three stages overlap (the host reads chunk c+2 "
+                                   "from the page cache into pinned memory, the copy stream moves "
+                                   "c+1 up, the device parses and counts c); the host read is the "
+                                   "slowest (NK_INGEST_PROFILE=1, profiles/r04_s8).  The step is "
+                                   "%.1fx the resident count + LIF and %.2fx the PCIe floor; the "
+                                   "file moves %.1fx the bases" % (t * 1e3 / float(np.median(tot)),
+                                                                   t / (fsize / h2d), fsize / n_b))},
         "roofline": {"bound": "hbm" if alg / (cm * 1e-3) / HBM_PEAK >= 0.6 else "latency",
                      "kernel": "the resident count of the reads (every batch's K1 + K1b)",
                      "achieved": round(alg / (cm * 1e-3) / 1e9, 2), "peak": HBM_PEAK / 1e9,

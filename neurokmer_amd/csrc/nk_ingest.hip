@@ -7,7 +7,8 @@
 // the base counts, the new totals and the carried line state; E per block:
 // scatter of the bases and of the record offsets.
 //
-// FASTQ (the chunk starts at a record boundary): A newline counts (16-B loads);
+// FASTQ (the chunk starts at a record boundary, at any address: A and C read
+// aligned 16-B groups and mask the bytes outside the chunk): A newline counts;
 // B scan; C newline positions; D per record: the four lines' validity and the
 // sequence length, the first bad record (atomicMin) and per-1024-record sums
 // of the sequence lengths; E one block: the scan of those sums, the first bad
