@@ -834,6 +834,11 @@ __device__ __forceinline__ uint64_t fresh_spikes(uint64_t cnt, const LifParams &
 #ifndef NK_HIST_KU
 #define NK_HIST_KU 4
 #endif
+constexpr int kK1bLifLds = 1024;  // counts whose fresh spikes the write-through K1b keeps in LDS
+// (u32 in LDS: every spike count fits below 2^32 steps)
+__device__ __forceinline__ int k1b_lds_entries(const K1bLif &L) {
+  return L.lp.steps >= (1ull << 32) ? 0 : L.tbl_n < kK1bLifLds ? L.tbl_n : kK1bLifLds;
+}
 // LIF: the write-through K1b also runs the LIF from the reset state (pa.lif)
 template <int BB, int KU = NK_HIST_KU, bool LIF = false>  // 2^BB bins per bucket (pa.bin_bits)
 __global__ __launch_bounds__(kHistBlock) void k_bucket_hist(PartArgs pa, uint64_t pool,
@@ -842,12 +847,17 @@ __global__ __launch_bounds__(kHistBlock) void k_bucket_hist(PartArgs pa, uint64_
   constexpr uint32_t kBins = 1u << BB;
   __shared__ uint32_t h[kBins + 1];  // + a spill bin for pad records
   __shared__ uint32_t s_sh[LIF ? kHistBins : 1];  // spike histogram of the bucket
+  __shared__ uint32_t s_tsp[LIF ? kK1bLifLds : 1];  // spikes of the small counts (pa.lif.tbl)
   __shared__ unsigned long long s_acc[2];
   const uint32_t b = blockIdx.x, r = blockIdx.y;  // buckets on x: up to 65536 of them
   for (int i = threadIdx.x; i <= (int)kBins; i += kHistBlock) h[i] = 0;
   if (LIF) {
     for (int i = threadIdx.x; i < kHistBins; i += kHistBlock) s_sh[i] = 0;
     if (threadIdx.x < 2) s_acc[threadIdx.x] = 0;
+    // the write-through's LIF reads these instead of a dependent global load
+    // per bin (fresh_spikes: tbl[count])
+    for (int i = threadIdx.x; i < k1b_lds_entries(pa.lif); i += kHistBlock)
+      s_tsp[i] = (uint32_t)pa.lif.tbl[i].spikes;
   }
   auto bin = [](uint32_t off) { return off < kBins ? off : kBins; };
   __syncthreads();
@@ -925,10 +935,13 @@ __global__ __launch_bounds__(kHistBlock) void k_bucket_hist(PartArgs pa, uint64_
     // lane, the currents as two 16-B stores and the u8 mirror as one 4-B store
     const K1bLif &L = pa.lif;
     unsigned long long my_sp = 0, my_mx = 0;
+    const uint64_t nt = (uint64_t)k1b_lds_entries(L);
     auto lif = [&](unsigned long long x) -> uint32_t {
       float v;
       uint32_t rr;
-      const uint64_t sp = fresh_spikes(x, L.lp, L.tbl, L.tbl_n, v, rr);
+      const uint64_t sp = (L.lp.skip_zero && x == 0) || L.lp.steps == 0 ? 0ull
+                          : x < nt ? (uint64_t)s_tsp[x]
+                                   : fresh_spikes(x, L.lp, L.tbl, L.tbl_n, v, rr);
       if (sp) {
         my_sp += sp;
         my_mx = sp > my_mx ? sp : my_mx;
