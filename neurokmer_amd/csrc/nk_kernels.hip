@@ -839,7 +839,9 @@ constexpr int kK1bLifLds = 1024;  // counts whose fresh spikes the write-through
 __device__ __forceinline__ int k1b_lds_entries(const K1bLif &L) {
   return L.lp.steps >= (1ull << 32) ? 0 : L.tbl_n < kK1bLifLds ? L.tbl_n : kK1bLifLds;
 }
-// LIF: the write-through K1b also runs the LIF from the reset state (pa.lif)
+// LIF: the write-through K1b also runs the LIF from the reset state (pa.lif).
+// (Measured and not kept, profiles/r04_s15: the bins and the spike histogram
+// as packed u16 pairs, 78 KB of LDS, two workgroups per CU -- equal.)
 template <int BB, int KU = NK_HIST_KU, bool LIF = false>  // 2^BB bins per bucket (pa.bin_bits)
 __global__ __launch_bounds__(kHistBlock) void k_bucket_hist(PartArgs pa, uint64_t pool,
                                                             uint32_t slices,
@@ -950,17 +952,22 @@ __global__ __launch_bounds__(kHistBlock) void k_bucket_hist(PartArgs pa, uint64_
       return sp < 255 ? (uint32_t)sp : 255u;
     };
     uint8_t *m8 = L.sc8 + nb0;
-    for (uint32_t t = 4 * threadIdx.x; t < nbins; t += 4 * kHistBlock) {
-      if (t + 4 <= nbins) {
-        const unsigned long long x0 = count(t), x1 = count(t + 1), x2 = count(t + 2), x3 = count(t + 3);
-        reinterpret_cast<ulonglong2 *>(o + t)[0] = make_ulonglong2(x0, x1);
-        reinterpret_cast<ulonglong2 *>(o + t)[1] = make_ulonglong2(x2, x3);
-        *reinterpret_cast<uint32_t *>(m8 + t) = lif(x0) | lif(x1) << 8 | lif(x2) << 16 | lif(x3) << 24;
-      } else {
-        for (uint32_t u = t; u < nbins; ++u) {
-          const unsigned long long x = count(u);
-          o[u] = x;
-          m8[u] = (uint8_t)lif(x);
+    // wave w of each 4096-bin span writes its 256 bins as two lane-contiguous
+    // 1 KB stores of currents (lane l: bins 2l, 2l+1 and 128+2l, 129+2l) and
+    // two 128-B stores of the u8 mirror
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (uint32_t s0 = wv * 256; s0 < nbins; s0 += 4 * kHistBlock) {
+#pragma unroll
+      for (uint32_t half = 0; half < 2; ++half) {
+        const uint32_t t = s0 + 128 * half + 2 * lane;
+        if (t + 2 <= nbins) {
+          const unsigned long long x0 = count(t), x1 = count(t + 1);
+          *reinterpret_cast<ulonglong2 *>(o + t) = make_ulonglong2(x0, x1);
+          *reinterpret_cast<uint16_t *>(m8 + t) = (uint16_t)(lif(x0) | lif(x1) << 8);
+        } else if (t < nbins) {
+          const unsigned long long x = count(t);
+          o[t] = x;
+          m8[t] = (uint8_t)lif(x);
         }
       }
     }
