@@ -608,6 +608,12 @@ void nk_free(nk_counter *c) {
   if (c->last_s) (void)hipStreamSynchronize(c->last_s);
   if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
   c->cur.release(); c->sc.release(); c->v.release(); c->r.release();
+  c->sc8.release(); c->ovf.release();
+  c->w_rec.release(); c->w_over.release(); c->w_fill.release();
+  c->x_cs.release(); c->xp_keys.release(); c->xp_cnt.release(); c->xp_ctr.release();
+  c->xk_off.release(); c->xk_over.release(); c->xk_wrec.release(); c->xk_wover.release();
+  c->xk_part.release(); c->xk_fill.release(); c->xk_wfill.release(); c->xk_cur.release();
+  c->u_tiles.release(); c->u_nt.release(); c->u_mark.release(); c->u_lanes.release();
   c->p_off.release(); c->p_pos.release(); c->p_fill.release(); c->p_desc.release();
   c->p_over.release(); c->partials.release(); c->tbuckets.release();
   c->bcand.release(); c->bcnt.release();
@@ -1539,7 +1545,8 @@ static int enqueue_lif(nk_counter *c, int streaming, uint32_t fuse_want, bool pa
     tf.post = PostArgs{c->set_alloc, part ? (gk ? c->last_ga.overflow : c->p_over.p) : nullptr,
                        part ? 1 : 0, c->set_mask_d.p, c->tbuckets.p, c->post_flags.p, c->uniq.p,
                        c->special.p, c->n_hits.p,
-                       gk ? (uint32_t)c->last_ga.bin_bits : c->last_pa.bin_bits};
+                       gk ? (uint32_t)c->last_ga.bin_bits : c->last_pa.bin_bits,
+                       part ? (gk ? c->last_ga.n_buckets : c->last_pa.n_buckets) : 0u};
   }
   // steps == 0: the kernel leaves every neuron as it is (streaming returns early,
   // src/spiking_hash.rs:549-551; in-memory runs zero iterations)
@@ -1577,9 +1584,12 @@ static int enqueue_select(nk_counter *c, uint64_t want, hipStream_t s, uint64_t 
   const unsigned nb = (unsigned)((n + 2047) / 2048);
   int rc;
   if ((rc = c->tie_cnt.ensure(nb))) return rc;
+  // rows the passes leave unfilled (a threshold inconsistent with the counts)
+  // read back as index ~0, never as stale rows
+  HIPCHK(hipMemsetAsync(c->cand.p, 0xFF, want * sizeof(TopCand), s));
   HIPCHK(launch_topn_count(sc, n, c->topst.p, c->tie_cnt.p, c->cand.p, s));
   HIPCHK(launch_topn_emit(sc, n, c->topst.p, c->tie_cnt.p, c->cand.p, s));
-  HIPCHK(launch_topn_sort(c->cand.p, (uint32_t)want, cur, c->top_cur.p, s));
+  HIPCHK(launch_topn_sort(c->cand.p, (uint32_t)want, n, cur, c->top_cur.p, s));
   return NK_OK;
 }
 
@@ -1597,7 +1607,8 @@ static int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, bool post_don
                            part ? c->p_over.p : genk ? c->last_ga.overflow : nullptr,
                            (part || genk) ? 1 : 0, c->set_mask_d.p, c->tbuckets.p, c->post_flags.p,
                            c->uniq.p, c->special.p, c->n_hits.p,
-                           genk ? (uint32_t)c->last_ga.bin_bits : c->last_pa.bin_bits, s));
+                           genk ? (uint32_t)c->last_ga.bin_bits : c->last_pa.bin_bits, s,
+                           part ? c->last_pa.n_buckets : genk ? c->last_ga.n_buckets : 0u));
   // the set must be empty up to the pass's mask: after the count's prep it is
   c->dirty_before = c->set_clean ? 0 : c->set_alloc;
   if (!part || !c->set_clean)
@@ -2414,10 +2425,10 @@ static int finalize_slice_impl(nk_counter *c, int streaming, const void *d_slice
   // a redo selects by the exact radix passes: nk_slice_export's fused LIF
   // wrote no spike histogram (max_sc: the largest count of any slice, an
   // upper bound of this one's)
+  TopState sel = h->st;
   if (m && (h->st.refine || !run_lif)) {  // spike counts >= 4095: exact radix refine over the slice
-    TopState st = h->st;
-    if ((rc = refine_threshold(c, m, max_sc, st, s, lo, n))) return rc;
-    HIPCHK(hipMemcpyAsync(c->topst.p, &st, sizeof st, hipMemcpyHostToDevice, s));
+    if ((rc = refine_threshold(c, m, max_sc, sel, s, lo, n))) return rc;
+    HIPCHK(hipMemcpyAsync(c->topst.p, &sel, sizeof sel, hipMemcpyHostToDevice, s));
     if ((rc = enqueue_select(c, m, s, lo, n))) return rc;
   }
   std::vector<TopCand> rows(m);
@@ -2427,6 +2438,14 @@ static int finalize_slice_impl(nk_counter *c, int streaming, const void *d_slice
     HIPCHK(hipMemcpyAsync(rcur.data(), c->top_cur.p, m * 8, hipMemcpyDeviceToHost, s));
   }
   HIPCHK(hipStreamSynchronize(s));
+  for (uint64_t i = 0; i < m; ++i)
+    if (rows[i].idx >= n)
+      return fail(NK_E_DEVICE,
+                  "slice [%zu, %zu) selection left row %llu unfilled (T %llu, rows above %llu, "
+                  "ties %llu, largest count %llu, redo %d)",
+                  lo, hi, (unsigned long long)i, (unsigned long long)sel.T,
+                  (unsigned long long)sel.n_above, (unsigned long long)sel.need,
+                  (unsigned long long)max_sc, run_lif ? 0 : 1);
   std::vector<uint64_t> seg(kSliceHdr + 3 * m);
   seg[0] = m;
   seg[1] = new_spikes;
@@ -2613,8 +2632,12 @@ int nk_adopt_slices(nk_counter *c, const uint64_t *d_all, size_t world, size_t s
     if (g[0] > want || kSliceHdr + 3 * g[0] > stride)
       return fail(NK_E_INVALID, "segment %zu holds %llu rows", r, (unsigned long long)g[0]);
     new_spikes += g[1];
-    for (uint64_t i = 0; i < g[0]; ++i)
+    for (uint64_t i = 0; i < g[0]; ++i) {
+      if (g[kSliceHdr + 3 * i] >= c->pool)
+        return fail(NK_E_DEVICE, "segment %zu row %llu: neuron %llu outside the pool", r,
+                    (unsigned long long)i, (unsigned long long)g[kSliceHdr + 3 * i]);
       cand.push_back(Row{g[kSliceHdr + 3 * i], g[kSliceHdr + 3 * i + 1], g[kSliceHdr + 3 * i + 2]});
+    }
   }
   const uint64_t m = std::min<uint64_t>(want, cand.size());
   std::partial_sort(cand.begin(), cand.begin() + m, cand.end(), [](const Row &a, const Row &b) {

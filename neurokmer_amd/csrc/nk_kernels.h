@@ -71,6 +71,7 @@ struct PostArgs {
   uint32_t *special;
   unsigned long long *n_hits;
   uint32_t bin_bits = kBinBits;  // of the partitioned count's buckets
+  uint32_t n_over = 0;           // entries of overflow (0: unchecked)
 };
 
 // Top-N selection fused into the LIF kernel (want <= kFuseMaxTopN): every LIF
@@ -254,7 +255,7 @@ hipError_t launch_topn_count(const SpikeSrc &sc, uint64_t pool, TopState *st,
                              uint32_t *tie_cnt, TopCand *cand, hipStream_t s);
 hipError_t launch_topn_emit(const SpikeSrc &sc, uint64_t pool, TopState *st,
                             const uint32_t *tie_cnt, TopCand *cand, hipStream_t s);
-hipError_t launch_topn_sort(TopCand *cand, uint32_t m, const uint64_t *currents,
+hipError_t launch_topn_sort(TopCand *cand, uint32_t m, uint64_t n, const uint64_t *currents,
                             uint64_t *top_cur, hipStream_t s);
 hipError_t launch_set_fill(unsigned long long *keys, const uint64_t *mask, uint64_t max_cap,
                            hipStream_t s);
@@ -262,7 +263,7 @@ hipError_t launch_top_post(const TopCand *top, const uint64_t *top_cur, uint32_t
                            uint64_t set_alloc, const uint32_t *overflow, int part,
                            uint64_t *set_mask, uint32_t *tbuckets, uint32_t *flags,
                            uint32_t *uniq, uint32_t *special, unsigned long long *n_hits,
-                           uint32_t bin_bits, hipStream_t s);
+                           uint32_t bin_bits, hipStream_t s, uint32_t n_over = 0);
 // --kmer-width=128 (k <= 64): the count, the top rows' uniques (set of 3
 // words per slot, u.set_keys), and the set helpers; keys outside the set are
 // (lo, hi) pairs of u64.

@@ -1290,7 +1290,7 @@ __device__ void top_post_block(const TopCand *top, const uint64_t *top_cur, uint
   __shared__ uint32_t s_bk[kMaxTopN];
   if (threadIdx.x == 0) { s_sum = 0; s_nb = 0; s_over = 0; *pa.n_hits = 0; }
   for (uint32_t i = threadIdx.x; i < m; i += blockDim.x)
-    s_bk[i] = (uint32_t)(top[i].idx >> pa.bin_bits);
+    s_bk[i] = top[i].idx == ~0ull ? 0u : (uint32_t)(top[i].idx >> pa.bin_bits);  // (an unfilled row)
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
     pa.uniq[i] = 0;
@@ -1298,6 +1298,12 @@ __device__ void top_post_block(const TopCand *top, const uint64_t *top_cur, uint
     atomicAdd(&s_sum, (unsigned long long)top_cur[i]);
     if (pa.part) {
       const uint32_t b = s_bk[i];
+      if (pa.n_over && b >= pa.n_over) {  // a row outside the count's buckets: never indexed
+        printf("nk top_post: row %u index %llu bucket %u outside %u buckets\n", i,
+               (unsigned long long)top[i].idx, b, pa.n_over);
+        s_over = 1;
+        continue;
+      }
       if (pa.overflow[b]) s_over = 1;
       bool first = true;  // first row of its bucket in the list
       for (uint32_t j = 0; j < i; ++j)
@@ -1914,8 +1920,10 @@ __global__ __launch_bounds__(kBlock) void k_topn_count(SpikeSrc sc,
     if (v[j] == T) ++c;
     if (v[j] > T && T != ~0ULL) {
       const unsigned long long pos = atomicAdd((unsigned long long *)&st->emit_above, 1ull);
-      cand[pos].idx = i;
-      cand[pos].sc = v[j];
+      if (pos < (unsigned long long)kMaxTopN) {  // (a threshold inconsistent with the counts
+        cand[pos].idx = i;                        // must not write past the candidates)
+        cand[pos].sc = v[j];
+      }
     }
   }
   for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
@@ -2001,7 +2009,7 @@ __global__ __launch_bounds__(kBlock) void k_topn_emit(SpikeSrc sc,
 
 
 // exact final order of the <= kMaxTopN candidates: bitonic sort in LDS
-__global__ __launch_bounds__(1024) void k_topn_sort(TopCand *__restrict__ cand, uint32_t m,
+__global__ __launch_bounds__(1024) void k_topn_sort(TopCand *__restrict__ cand, uint32_t m, uint64_t n,
                                                     const uint64_t *__restrict__ currents,
                                                     uint64_t *__restrict__ top_cur) {
   __shared__ TopCand s[kMaxTopN];
@@ -2028,7 +2036,7 @@ __global__ __launch_bounds__(1024) void k_topn_sort(TopCand *__restrict__ cand, 
   }
   for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
     cand[i] = s[i];
-    top_cur[i] = currents[s[i].idx];
+    top_cur[i] = s[i].idx < n ? currents[s[i].idx] : 0ull;  // (an unfilled row: the caller checks)
   }
 }
 
@@ -2359,10 +2367,10 @@ hipError_t launch_topn_emit(const SpikeSrc &sc, uint64_t pool, TopState *st,
   return hipGetLastError();
 }
 
-hipError_t launch_topn_sort(TopCand *cand, uint32_t m, const uint64_t *currents,
+hipError_t launch_topn_sort(TopCand *cand, uint32_t m, uint64_t n, const uint64_t *currents,
                             uint64_t *top_cur, hipStream_t s) {
   if (!m) return hipSuccess;
-  hipLaunchKernelGGL(k_topn_sort, dim3(1), dim3(1024), 0, s, cand, m, currents, top_cur);
+  hipLaunchKernelGGL(k_topn_sort, dim3(1), dim3(1024), 0, s, cand, m, n, currents, top_cur);
   return hipGetLastError();
 }
 
@@ -2590,8 +2598,9 @@ hipError_t launch_top_post(const TopCand *top, const uint64_t *top_cur, uint32_t
                            uint64_t set_alloc, const uint32_t *overflow, int part,
                            uint64_t *set_mask, uint32_t *tbuckets, uint32_t *flags,
                            uint32_t *uniq, uint32_t *special, unsigned long long *n_hits,
-                           uint32_t bin_bits, hipStream_t s) {
-  PostArgs pa{set_alloc, overflow, part, set_mask, tbuckets, flags, uniq, special, n_hits, bin_bits};
+                           uint32_t bin_bits, hipStream_t s, uint32_t n_over) {
+  PostArgs pa{set_alloc, overflow, part, set_mask, tbuckets, flags, uniq, special, n_hits, bin_bits,
+              n_over};
   hipLaunchKernelGGL(k_top_post, dim3(1), dim3(1024), 0, s, top, top_cur, m, pa);
   return hipGetLastError();
 }
