@@ -1299,9 +1299,7 @@ __device__ void top_post_block(const TopCand *top, const uint64_t *top_cur, uint
     if (pa.part) {
       const uint32_t b = s_bk[i];
       if (pa.n_over && b >= pa.n_over) {  // a row outside the count's buckets: never indexed
-        printf("nk top_post: row %u index %llu bucket %u outside %u buckets\n", i,
-               (unsigned long long)top[i].idx, b, pa.n_over);
-        s_over = 1;
+        s_over = 1;                          // (the host takes the rescan path)
         continue;
       }
       if (pa.overflow[b]) s_over = 1;
