@@ -2438,6 +2438,15 @@ static int finalize_slice_impl(nk_counter *c, int streaming, const void *d_slice
     HIPCHK(hipMemcpyAsync(rcur.data(), c->top_cur.p, m * 8, hipMemcpyDeviceToHost, s));
   }
   HIPCHK(hipStreamSynchronize(s));
+  if (getenv("NK_DEBUG_SELECT")) {  // (tests: the selection state of a slice)
+    uint64_t bad = 0;
+    for (uint64_t i = 0; i < m; ++i) bad += rows[i].idx >= n;
+    fprintf(stderr, "[nk select] slice [%zu, %zu) m %llu T %llu above %llu need %llu max_sc %llu "
+                    "redo %d refine %u unfilled %llu\n", lo, hi, (unsigned long long)m,
+            (unsigned long long)sel.T, (unsigned long long)sel.n_above,
+            (unsigned long long)sel.need, (unsigned long long)max_sc, run_lif ? 0 : 1,
+            (unsigned)h->st.refine, (unsigned long long)bad);
+  }
   for (uint64_t i = 0; i < m; ++i)
     if (rows[i].idx >= n)
       return fail(NK_E_DEVICE,

@@ -284,8 +284,8 @@ void nk_comm_free(nk_comm *m) {
   delete m;
 }
 
-int nk_finalize_dist(nk_counter *c, nk_comm *m, int streaming, uint64_t total_kmers, size_t cap,
-                     void *stream) {
+static int finalize_dist_impl(nk_counter *c, nk_comm *m, int streaming, uint64_t total_kmers,
+                              size_t cap, void *stream) {
   if (!c || !m) return failf(NK_E_INVALID, "null argument");
   if (!cap || cap > (1u << 24)) return failf(NK_E_INVALID, "cap must be in 1 .. 2^24");
   // the library's calls and the collectives share this stream's order (a NULL
@@ -325,8 +325,8 @@ int nk_finalize_dist(nk_counter *c, nk_comm *m, int streaming, uint64_t total_km
   return union_top_kmers(c, m, b, cap, s);
 }
 
-int nk_finalize_sliced_dist(nk_counter *c, nk_comm *m, int streaming, uint64_t total_kmers,
-                            size_t cap, void *stream) {
+static int finalize_sliced_dist_impl(nk_counter *c, nk_comm *m, int streaming,
+                                     uint64_t total_kmers, size_t cap, void *stream) {
   if (!c || !m) return failf(NK_E_INVALID, "null argument");
   if (!cap || cap > (1u << 24)) return failf(NK_E_INVALID, "cap must be in 1 .. 2^24");
   // the library's calls and the collectives share this stream's order (a NULL
@@ -389,6 +389,22 @@ int nk_finalize_sliced_dist(nk_counter *c, nk_comm *m, int streaming, uint64_t t
   RC(all_gather(m, b.sseg.p, b.sall.p, stride, true, s));
   RC(nk_adopt_slices(c, b.sall.p, W, stride, stream));
   return union_top_kmers(c, m, b, cap, s);
+}
+
+// (a loopback rank that fails releases the others at once instead of leaving
+// them at the next collective until the group's timeout)
+int nk_finalize_dist(nk_counter *c, nk_comm *m, int streaming, uint64_t total_kmers, size_t cap,
+                     void *stream) {
+  const int rc = finalize_dist_impl(c, m, streaming, total_kmers, cap, stream);
+  if (rc && m && m->loop) nk::loop_break(m->loop);
+  return rc;
+}
+
+int nk_finalize_sliced_dist(nk_counter *c, nk_comm *m, int streaming, uint64_t total_kmers,
+                            size_t cap, void *stream) {
+  const int rc = finalize_sliced_dist_impl(c, m, streaming, total_kmers, cap, stream);
+  if (rc && m && m->loop) nk::loop_break(m->loop);
+  return rc;
 }
 
 }  // extern "C"

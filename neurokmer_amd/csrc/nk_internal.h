@@ -31,6 +31,8 @@ int slice_reselect(nk_counter *c, size_t lo, size_t hi, uint64_t *d_seg, size_t 
 uint64_t counter_uid(const nk_counter *c);
 // the loopback transport (nk_loop.hip)
 int loop_join(nk_loop_group *g, int rank, int device);
+// a rank that failed between collectives releases the others (they fail too)
+void loop_break(nk_loop_group *g);
 int loop_world(const nk_loop_group *g);
 // kind 0 all-reduce (sum, n elements), 1 all-gather (n per rank), 2
 // reduce-scatter (sum, n per rank); elem 4 or 8 bytes; blocks until done

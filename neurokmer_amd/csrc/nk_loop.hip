@@ -95,6 +95,8 @@ namespace nk {
 
 int loop_world(const nk_loop_group *g) { return g->world; }
 
+void loop_break(nk_loop_group *g) { g->fail_all(); }
+
 int loop_join(nk_loop_group *g, int rank, int device) {
   std::lock_guard<std::mutex> lk(g->mu);
   if (rank < 0 || rank >= g->world) return failf(NK_E_INVALID, "rank out of range");

@@ -66,17 +66,25 @@ __global__ __launch_bounds__(kAdoptBlock) void k_slice_adopt(const uint64_t *__r
     if (g[0] & kSegRefine) atomicOr(&s_ref, 1u);
   }
   __syncthreads();
+  // a segment's row count, bounded by its stride and the LDS rows (a corrupt
+  // header must not drive the loops below past either)
+  const uint64_t seg_max = stride >= 3 ? (stride - 3) / 3 : 0;
+  auto rows_of = [&](const uint64_t *g) -> uint32_t {
+    const uint64_t nr = g[0] & kSegCount;
+    return (uint32_t)(nr < seg_max ? nr : seg_max);
+  };
   if (threadIdx.x == 0) {
     uint32_t n = 0;
-    for (uint32_t r = 0; r < W; ++r) n += (uint32_t)(all[(uint64_t)r * stride] & kSegCount);
-    s_n = n;
+    for (uint32_t r = 0; r < W; ++r) n += rows_of(all + (uint64_t)r * stride);
+    s_n = n < (uint32_t)kAdoptMax ? n : (uint32_t)kAdoptMax;
   }
   __syncthreads();
   // rows in segment order: prefix over segments (W is small), one row per thread
   uint32_t base = 0;
   for (uint32_t r = 0; r < W; ++r) {
     const uint64_t *g = all + (uint64_t)r * stride;
-    const uint32_t nr = (uint32_t)(g[0] & kSegCount);
+    uint32_t nr = rows_of(g);
+    if (base + nr > (uint32_t)kAdoptMax) nr = base < (uint32_t)kAdoptMax ? (uint32_t)kAdoptMax - base : 0u;
     for (uint32_t i = threadIdx.x; i < nr; i += blockDim.x) {
       s_idx[base + i] = g[3 + 3 * (uint64_t)i];
       s_sc[base + i] = g[4 + 3 * (uint64_t)i];
