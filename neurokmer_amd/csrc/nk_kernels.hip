@@ -1312,7 +1312,8 @@ __device__ void top_post_block(const TopCand *top, const uint64_t *top_cur, uint
   __syncthreads();
   if (threadIdx.x == 0) {
     uint64_t cap = 64;
-    while (cap < 2 * (uint64_t)s_sum + 2) cap <<= 1;
+    while (cap < 2 * (uint64_t)s_sum + 2 && cap < (1ull << 48)) cap <<= 1;  // (bounded: a row's
+    // current read before its selection was resolved must not spin the loop)
     pa.flags[0] = cap > pa.set_alloc ? 1u : 0u;  // set too small
     pa.flags[1] = s_over;                        // a top bucket overflowed
     pa.flags[2] = s_nb;                          // distinct top buckets
@@ -1577,10 +1578,14 @@ __device__ void final_top(uint64_t pool, const uint64_t *currents, uint32_t nb,
   const bool row = (uint32_t)lane < m;
   const uint64_t key = wave_sort64_desc(row ? s_fin[lane] : 0ull);
   const uint64_t idx = key_idx(key), sc = key_sc(key);
-  const uint64_t cur = row ? currents[idx] : 0ull;
+  // a row outside the pool (a selection the refine redoes) is never indexed;
+  // it counts as an overflowed bucket, which sends the host down the rescan
+  const bool in_pool = idx < pool;
+  const uint64_t cur = (row && in_pool) ? currents[idx] : 0ull;
   const PostArgs &pa = tf.post;
-  const uint32_t bk = (uint32_t)(idx >> pa.bin_bits);
-  const uint32_t over = (row && pa.part) ? pa.overflow[bk] : 0u;
+  const uint32_t bk = in_pool ? (uint32_t)(idx >> pa.bin_bits) : 0u;
+  const bool bk_ok = in_pool && (!pa.n_over || bk < pa.n_over);
+  const uint32_t over = (row && pa.part) ? (bk_ok ? pa.overflow[bk] : 1u) : 0u;
   if (row) {
     tf.cand[lane].idx = idx;
     tf.cand[lane].sc = sc;
@@ -1600,7 +1605,7 @@ __device__ void final_top(uint64_t pool, const uint64_t *currents, uint32_t nb,
   const bool any_over = __ballot(over != 0) != 0;
   if (lane == 0) {
     uint64_t cap = 64;
-    while (cap < 2 * (uint64_t)sum + 2) cap <<= 1;
+    while (cap < 2 * (uint64_t)sum + 2 && cap < (1ull << 48)) cap <<= 1;  // (bounded, as k_top_post)
     pa.flags[0] = cap > pa.set_alloc ? 1u : 0u;  // set too small
     pa.flags[1] = any_over ? 1u : 0u;            // a top bucket overflowed
     pa.flags[2] = (uint32_t)__popcll(fb);        // distinct top buckets
