@@ -189,7 +189,7 @@ def main() -> int:
                     help="config2/5: bases per rank (default 115e6 / 12.5e9)")
     ap.add_argument("--total-bases", type=int, default=C4_TOTAL, help="config4: bases in all")
     ap.add_argument("--shard-of", type=int, default=0,
-                    help="config4: split the input into this many shards (default: world size)")
+                    help="config4: split the input into this many shards (default: the world size; 8 on one GPU)")
     ap.add_argument("--no-side-parity", action="store_true",
                     help="side lines: skip the properties / prefix oracle compare")
     ap.add_argument("--fastq", default=None, help="config3: the FASTQ (default: generated in /dev/shm)")
@@ -320,7 +320,10 @@ def main() -> int:
                        f"{args.finish} multi-GPU finish"))
     else:
         T = args.total_bases
-        n_shards = args.shard_of or world
+        # one GPU holds the 12.5 Gbase shard of an 8-GPU run by default (the
+        # whole 100 Gbase input would not fit one GPU's arena); --shard-of 1
+        # asks for all of it
+        n_shards = args.shard_of or (8 if world == 1 and T == C4_TOTAL else world)
         if n_shards < world:
             print("bench.py: --shard-of must be >= the world size", file=sys.stderr)
             return 2
@@ -636,7 +639,9 @@ def main() -> int:
         }
         if pr is not None:
             out["parity_ranks"] = pr
-        if world == 1 and args.workload == "config2" and args.kmer_width == 64:
+        if world == 1 and args.workload == "config2" and args.kmer_width == 64 and bases is not None:
+            # (extras time the host-array and file paths from the host copy of
+            # the input: none past HOST_GEN_MAX, where it is generated on the device)
             out.update(extras(args, ctr, bases, offsets, nk_rank, d_bases, d_offs, s_handle,
                               dev_idx, SpikingKmerCounter, synth))
         if side:

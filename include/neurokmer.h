@@ -225,7 +225,10 @@ void nk_comm_forget(nk_comm *m, const nk_counter *c);
  * copies and a sum kernel between host barriers (a rank that does not arrive
  * within 120 s fails every rank's call).  RCCL refuses two ranks on one
  * device, so this is how nk_finalize_dist / nk_finalize_sliced_dist run at
- * world > 1 on a one-GPU box.  world: 1 .. 16. */
+ * world > 1 on a one-GPU box.  world: 1 .. 16.  Each rank joins once (a second
+ * communicator for a live rank fails; nk_comm_free leaves the group).  A
+ * group that broke (a rank failed or timed out) stays broken: every later
+ * collective fails, so free it and make a new one. */
 typedef struct nk_loop_group nk_loop_group;
 nk_loop_group *nk_loop_group_new(int world);
 void nk_loop_group_free(nk_loop_group *g);  /* after every member's nk_comm_free */

@@ -179,6 +179,13 @@ struct nk_counter {
   // wide partition (pool > 16.7 M or big-key modes past it): coarse buckets
   DevBuf<uint32_t> w_rec, w_over;
   DevBuf<unsigned long long> w_fill;
+  // pipelined split (split_pipelined): the coarse records of k_part_gen launch
+  // g are split on split_s while launch g + 1 hashes; w_snap[g][bucket] = the
+  // records reserved after launch g
+  static constexpr int kSplitMax = 32;
+  hipStream_t split_s = nullptr;
+  hipEvent_t split_ev[kSplitMax + 1] = {};
+  DevBuf<unsigned long long> w_snap;
   // overflow target of a write-through K1b (PartArgs::out), kept zero
   DevBuf<unsigned long long> ovf;
   size_t ovf_zeroed = 0;  // entries known zero
@@ -636,6 +643,11 @@ void nk_free(nk_counter *c) {
   for (hipEvent_t &e : c->ing_ev)
     if (e) (void)hipEventDestroy(e);
   if (c->ing_cs) (void)hipStreamDestroy(c->ing_cs);
+  if (c->split_s) (void)hipStreamSynchronize(c->split_s);
+  for (hipEvent_t &e : c->split_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->split_s) (void)hipStreamDestroy(c->split_s);
+  c->w_snap.release();
   c->special.release(); c->stats.release(); c->lif_tbl.release(); c->topst.release();
   c->cand.release(); c->top_cur.release(); c->set_keys.release(); c->top_keys.release();
   c->top_keys_n.release(); c->radix_h.release(); c->set_mask_d.release();
@@ -1173,9 +1185,59 @@ static hipError_t gen_hist(nk_counter *c, const CountPlan &cp, bool defer_partia
   return launch_bucket_hist(cp.pa, c->pool, 1, nullptr, s);
 }
 
+// k_part_gen launches of a pipelined wide count: G launches of at least
+// kSplitMinTiles tiles each (NK_SPLIT_LAUNCHES: tests / A/B; 1 = one launch,
+// the split after it)
+constexpr uint64_t kSplitMinTiles = 2048;
+static uint32_t split_launches(uint64_t n_tiles) {
+  const char *e = getenv("NK_SPLIT_LAUNCHES");
+  uint64_t g = e ? strtoull(e, nullptr, 10) : std::min<uint64_t>(16, n_tiles / kSplitMinTiles);
+  g = std::min<uint64_t>(std::min<uint64_t>(g, nk_counter::kSplitMax), n_tiles);
+  return (uint32_t)std::max<uint64_t>(g, 1);
+}
+
+// The wide count with its split pipelined: k_part_gen is VALU-bound (SipHash)
+// and k_split is bound by its bytes, so the input's tiles go in G launches on
+// s and the split of launch g's records (each coarse bucket's records reserved
+// between the fill snapshots after launches g - 1 and g) runs on split_s while
+// launch g + 1 hashes.  s waits for the last split before K1b.
+static hipError_t split_pipelined(nk_counter *c, const CountPlan &cp, const KmerInput &in, uint32_t G,
+                                  hipStream_t s) {
+  hipError_t e;
+  if (!c->split_s) {
+    if ((e = hipStreamCreateWithFlags(&c->split_s, hipStreamNonBlocking)) != hipSuccess) return e;
+    for (hipEvent_t &ev : c->split_ev)
+      if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+  }
+  const uint64_t nb = cp.ga.n_buckets;
+  if (c->w_snap.ensure(G * nb)) return hipErrorOutOfMemory;
+  const uint64_t per = (in.n_tiles + G - 1) / G;
+  const bool wide = true;
+  uint32_t g = 0;
+  for (uint64_t t0 = 0; t0 < in.n_tiles; t0 += per, ++g) {
+    KmerInput bi = in;
+    bi.tile_base = in.tile_base + t0;
+    bi.tile_rec = in.tile_rec + t0;
+    bi.n_tiles = std::min<uint64_t>(per, in.n_tiles - t0);
+    unsigned long long *hi = c->w_snap.p + (uint64_t)g * nb;
+    if ((e = launch_part_gen(bi, (int)c->k, c->canonical, cp.km, c->pool, cp.ga, wide ? 1 : 0, s)) ||
+        (e = launch_fill_snap(cp.ga, hi, s)) || (e = hipEventRecord(c->split_ev[g], s)) ||
+        (e = hipStreamWaitEvent(c->split_s, c->split_ev[g], 0)) ||
+        (e = launch_split(cp.ga, cp.pa, c->split_s, g ? hi - nb : nullptr, hi, bi.n_tiles * kPartTile)))
+      return e;
+  }
+  if ((e = hipEventRecord(c->split_ev[nk_counter::kSplitMax], c->split_s))) return e;
+  return hipStreamWaitEvent(s, c->split_ev[nk_counter::kSplitMax], 0);
+}
+
 // Gen/Wide count kernels of one batch (before K1b)
-static hipError_t gen_count(nk_counter *c, const CountPlan &cp, const KmerInput &in, hipStream_t s) {
+static hipError_t gen_count(nk_counter *c, const CountPlan &cp, const KmerInput &in, hipStream_t s,
+                            bool pipeline = false) {
   const bool wide = cp.path == CountPath::Wide;
+  if (wide && pipeline) {
+    const uint32_t G = split_launches(in.n_tiles);
+    if (G > 1) return split_pipelined(c, cp, in, G, s);
+  }
   hipError_t e = launch_part_gen(in, (int)c->k, c->canonical, cp.km, c->pool, cp.ga, wide ? 1 : 0, s);
   if (e != hipSuccess || !wide) return e;
   return launch_split(cp.ga, cp.pa, s);
@@ -1379,7 +1441,7 @@ static int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_o
       HIPCHK(launch_partials_add(c->partials.p, cp.slices, c->pool, c->cur.p, s));
     c->last_pa = cp.pa;
   } else if (counted) {
-    HIPCHK(gen_count(c, cp, in, s));
+    HIPCHK(gen_count(c, cp, in, s, /*pipeline=*/true));
     HIPCHK(mark(c, 2, s));
     HIPCHK(gen_hist(c, cp, defer_partials, s));
   } else {
@@ -2560,7 +2622,7 @@ int nk_slice_export(nk_counter *c, int streaming, const uint32_t *d_slice, size_
     HIPCHK(launch_topn_threshold(c->hist.p, m, n, c->topst.p, s));
     if ((rc = enqueue_select(c, m, s, lo, n))) return rc;
   }
-  HIPCHK(launch_slice_seg(c->cand.p, c->top_cur.p, c->topst.p, c->stats.p, (uint32_t)m, lo, d_seg, s));
+  HIPCHK(launch_slice_seg(c->cand.p, c->top_cur.p, c->topst.p, c->stats.p, (uint32_t)m, lo, n, d_seg, s));
   c->slice_ready = true;
   return NK_OK;
 }
@@ -2580,8 +2642,8 @@ int nk_adopt_export(nk_counter *c, const uint64_t *d_all, size_t world, size_t s
   c->slice_ready = false;
   int rc;
   // every rank's slice yields min(top_n, its size) rows: together >= min(top_n, pool) = want
-  HIPCHK(launch_slice_adopt(d_all, (uint32_t)world, stride, (uint32_t)want, c->cand.p, c->top_cur.p,
-                            c->topst.p, c->stats.p, s));
+  HIPCHK(launch_slice_adopt(d_all, (uint32_t)world, stride, (uint32_t)want, c->pool, c->cand.p,
+                            c->top_cur.p, c->topst.p, c->stats.p, s));
   const bool uniq = want && c->have_input && c->last_in.n_tiles;
   if ((rc = c->export_n.ensure(1))) return rc;
   if (!c->export_n_zeroed) {
@@ -2821,12 +2883,24 @@ static int acc_begin(nk_counter *c, uint64_t est_bases, uint64_t batch_bases, St
   ZeroList z{};
   z.ptr[z.n] = c->cur.p; z.bytes[z.n++] = c->pool * 8;
   const uint64_t B = (c->pool + kBinsPerBucket - 1) >> kBinBits;
-  const bool part_like = !c->w128 && c->k <= 32 && B <= (uint64_t)kMaxBuckets &&
-                         !wide_bits_forced() && est_bases <= count_chunk(est_bases, c->pool, c->w128 || c->k > 32, arena_bytes(c));
-  const uint64_t est = part_like ? est_bases : std::min(est_bases, batch_bases);
+  bool part_like = !c->w128 && c->k <= 32 && B <= (uint64_t)kMaxBuckets &&
+                   !wide_bits_forced() && est_bases <= count_chunk(est_bases, c->pool, c->w128 || c->k > 32, arena_bytes(c));
+  uint64_t est = part_like ? est_bases : std::min(est_bases, batch_bases);
   // segments per bucket: one per tile per launch; chunk-straddling tiles add a few
-  const uint64_t max_segs = n_tiles_for(std::max<uint64_t>(est, 1), kPartTile) + 4096;
-  if ((rc = plan_count(c, est, 4 * kPartTile, max_segs, sa.cp, z))) return rc;
+  uint64_t max_segs = n_tiles_for(std::max<uint64_t>(est, 1), kPartTile) + 4096;
+  rc = plan_count(c, est, 4 * kPartTile, max_segs, sa.cp, z);
+  if (rc == NK_E_OOM && part_like && est > batch_bases) {
+    // the one-launch arena (sized from an estimate of the file's bases) did
+    // not fit after all -- other handles took the memory since the check:
+    // histogram batch by batch instead, as accumulate() does
+    z = ZeroList{};
+    z.ptr[z.n] = c->cur.p; z.bytes[z.n++] = c->pool * 8;
+    part_like = false;
+    est = std::min(est_bases, batch_bases);
+    max_segs = n_tiles_for(std::max<uint64_t>(est, 1), kPartTile) + 4096;
+    rc = plan_count(c, est, 4 * kPartTile, max_segs, sa.cp, z);
+  }
+  if (rc) return rc;
   z.ptr[z.n] = c->hist.p;  z.bytes[z.n++] = kHistBins * kHistCopies * 4;
   z.ptr[z.n] = c->stats.p; z.bytes[z.n++] = 16;
   c->lif_zeroed = true;

@@ -281,6 +281,7 @@ void nk_comm_free(nk_comm *m) {
   (void)hipDeviceSynchronize();
   for (auto &kv : m->bufs) kv.second.release();
   if (m->comm) (void)rccl().comm_destroy(m->comm);
+  if (m->loop) nk::loop_leave(m->loop, m->rank);
   delete m;
 }
 

@@ -30,7 +30,8 @@ int slice_reselect(nk_counter *c, size_t lo, size_t hi, uint64_t *d_seg, size_t 
 // a per-process id of the handle, never reused after nk_free
 uint64_t counter_uid(const nk_counter *c);
 // the loopback transport (nk_loop.hip)
-int loop_join(nk_loop_group *g, int rank, int device);
+int loop_join(nk_loop_group *g, int rank, int device);  // (a rank joins once)
+void loop_leave(nk_loop_group *g, int rank);            // (nk_comm_free)
 // a rank that failed between collectives releases the others (they fail too)
 void loop_break(nk_loop_group *g);
 int loop_world(const nk_loop_group *g);

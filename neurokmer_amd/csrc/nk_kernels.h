@@ -304,12 +304,14 @@ struct MergePrep {
 // all-gather segment, and the global rows picked from the gathered segments
 // (world * want <= kAdoptMax)
 constexpr int kAdoptMax = 2048;
+// (n: the slice's neurons; a refine or a row >= n exports no rows, the refine flag)
 hipError_t launch_slice_seg(const TopCand *cand, const uint64_t *top_cur, const TopState *st,
-                            const uint64_t *stats, uint32_t m, uint64_t lo, uint64_t *seg,
+                            const uint64_t *stats, uint32_t m, uint64_t lo, uint64_t n, uint64_t *seg,
                             hipStream_t s);
+// (a flagged segment or a row >= pool: want sentinel rows {~0, 0} and st->refine)
 hipError_t launch_slice_adopt(const uint64_t *all, uint32_t world, uint64_t stride, uint32_t want,
-                              TopCand *cand, uint64_t *top_cur, TopState *st, uint64_t *stats,
-                              hipStream_t s);
+                              uint64_t pool, TopCand *cand, uint64_t *top_cur, TopState *st,
+                              uint64_t *stats, hipStream_t s);
 hipError_t launch_export(const unsigned long long *set_keys, const uint64_t *set_mask,
                          uint64_t set_alloc, int w128, bool uniq, bool appended,
                          const uint32_t *special, uint32_t n_top, const TopState *st,
@@ -350,7 +352,13 @@ hipError_t launch_uniq_tiles(const GenPartArgs &ga, int wide, const UniqArgs &u,
                              uint32_t slices, uint32_t *tiles, uint32_t *n_list, uint32_t max_list,
                              uint32_t *flag, uint32_t *mark, uint32_t epoch, uint32_t *lanes,
                              uint32_t hit_queue, hipStream_t s);
-hipError_t launch_split(const GenPartArgs &ga, const PartArgs &fine, hipStream_t s);
+// snap_lo / snap_hi (optional): split only the records [snap_lo[b], snap_hi[b])
+// of each coarse bucket (one k_part_gen launch's, est_records of them about)
+hipError_t launch_split(const GenPartArgs &ga, const PartArgs &fine, hipStream_t s,
+                        const unsigned long long *snap_lo = nullptr,
+                        const unsigned long long *snap_hi = nullptr, uint64_t est_records = 0);
+// snap[b] = min(records reserved in coarse bucket b, cap)
+hipError_t launch_fill_snap(const GenPartArgs &ga, unsigned long long *snap, hipStream_t s);
 // the exact table's kmer_per_neuron: a key array (wpk u64 words per key, *n_keys
 // of them on the device, at most max_n) hashed and partitioned like the count
 hipError_t launch_part_keys(const uint64_t *keys, const unsigned long long *n_keys, uint64_t max_n,

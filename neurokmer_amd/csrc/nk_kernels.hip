@@ -1289,16 +1289,24 @@ __device__ void top_post_block(const TopCand *top, const uint64_t *top_cur, uint
   __shared__ uint32_t s_nb, s_over;
   __shared__ uint32_t s_bk[kMaxTopN];
   if (threadIdx.x == 0) { s_sum = 0; s_nb = 0; s_over = 0; *pa.n_hits = 0; }
+  // a sentinel row (index ~0: a selection deferred to the host's exact redo,
+  // k_slice_adopt) takes no part: no bucket, no set capacity, no hits
+  constexpr uint32_t kNoBucket = 0xFFFFFFFFu;
   for (uint32_t i = threadIdx.x; i < m; i += blockDim.x)
-    s_bk[i] = top[i].idx == ~0ull ? 0u : (uint32_t)(top[i].idx >> pa.bin_bits);  // (an unfilled row)
+    s_bk[i] = top[i].idx == ~0ull ? kNoBucket : (uint32_t)(top[i].idx >> pa.bin_bits);
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
     pa.uniq[i] = 0;
     pa.special[i] = 0;
+    const uint32_t b = s_bk[i];
+    if (b == kNoBucket) continue;
     atomicAdd(&s_sum, (unsigned long long)top_cur[i]);
     if (pa.part) {
-      const uint32_t b = s_bk[i];
       if (pa.n_over && b >= pa.n_over) {  // a row outside the count's buckets: never indexed
+#ifdef NK_DEBUG_ROWS
+        printf("[nk top_post] row %u index %llu outside the count's %u buckets\n", i,
+               (unsigned long long)top[i].idx, pa.n_over);
+#endif
         s_over = 1;                          // (the host takes the rescan path)
         continue;
       }

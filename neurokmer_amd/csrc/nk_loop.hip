@@ -54,6 +54,7 @@ struct nk_loop_group {
   int world = 0;
   int device = -1;
   int joined = 0;
+  std::vector<bool> member;  // rank r holds a live communicator
   std::mutex mu;
   std::condition_variable cv;
   uint64_t gen = 0;
@@ -102,8 +103,20 @@ int loop_join(nk_loop_group *g, int rank, int device) {
   if (rank < 0 || rank >= g->world) return failf(NK_E_INVALID, "rank out of range");
   if (g->device < 0) g->device = device;
   if (g->device != device) return failf(NK_E_INVALID, "all ranks of a loopback group use one device");
+  // two communicators for one rank would overwrite each other's send/recv
+  // slots and corrupt every collective
+  if (g->member[rank]) return failf(NK_E_INVALID, "rank already joined this loopback group");
+  g->member[rank] = true;
   ++g->joined;
   return NK_OK;
+}
+
+void loop_leave(nk_loop_group *g, int rank) {
+  std::lock_guard<std::mutex> lk(g->mu);
+  if (rank >= 0 && rank < g->world && g->member[rank]) {
+    g->member[rank] = false;
+    --g->joined;
+  }
 }
 
 // One collective on rank `rank`: kind 0 all-reduce (sum; n elements), 1
@@ -188,6 +201,7 @@ nk_loop_group *nk_loop_group_new(int world) {
   g->world = world;
   g->send.assign(world, nullptr);
   g->recv.assign(world, nullptr);
+  g->member.assign(world, false);
   return g;
 }
 

@@ -22,16 +22,26 @@ constexpr uint64_t kSegRefine = 1ull << 56;  // header flag: this slice's rows n
 constexpr uint64_t kSegCount = (1ull << 56) - 1;
 
 // seg = [rows | refine << 56, new spikes, largest spike count, (global idx, spikes, current) x rows]
+// A slice whose selection is not resolved on the device (spike counts past
+// 4095: the exact refine; or a row the passes left unfilled, index >= n)
+// exports NO rows, only the refine flag: nothing downstream may rank, adopt or
+// look up rows read from buffers the selection did not finish (the r04 device
+// fault: such rows reached the uniques bookkeeping); the redo
+// selects exactly and rebuilds the segment.
 __global__ void k_slice_seg(const TopCand *__restrict__ cand, const uint64_t *__restrict__ top_cur,
                             const TopState *__restrict__ st, const uint64_t *__restrict__ stats,
-                            uint32_t m, uint64_t lo, uint64_t *__restrict__ seg) {
-  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+                            uint32_t m, uint64_t lo, uint64_t n, uint64_t *__restrict__ seg) {
+  int bad = 0;
+  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) bad |= cand[i].idx >= n ? 1 : 0;
+  const bool refine = __syncthreads_or(bad) || (m && st->refine);
+  const uint32_t rows = refine ? 0u : m;
+  for (uint32_t i = threadIdx.x; i < rows; i += blockDim.x) {
     seg[3 + 3 * (uint64_t)i] = cand[i].idx + lo;
     seg[4 + 3 * (uint64_t)i] = cand[i].sc;
     seg[5 + 3 * (uint64_t)i] = top_cur[i];
   }
   if (threadIdx.x == 0) {
-    seg[0] = (uint64_t)m | ((m && st->refine) ? kSegRefine : 0ull);
+    seg[0] = (uint64_t)rows | (refine ? kSegRefine : 0ull);
     seg[1] = stats[0];
     seg[2] = stats[1];
   }
@@ -43,7 +53,8 @@ __global__ void k_slice_seg(const TopCand *__restrict__ cand, const uint64_t *__
 constexpr int kAdoptBlock = 1024;
 __global__ __launch_bounds__(kAdoptBlock) void k_slice_adopt(const uint64_t *__restrict__ all,
                                                              uint32_t W, uint64_t stride,
-                                                             uint32_t want, TopCand *__restrict__ cand,
+                                                             uint32_t want, uint64_t pool,
+                                                             TopCand *__restrict__ cand,
                                                              uint64_t *__restrict__ top_cur,
                                                              TopState *__restrict__ st,
                                                              uint64_t *__restrict__ stats) {
@@ -94,14 +105,25 @@ __global__ __launch_bounds__(kAdoptBlock) void k_slice_adopt(const uint64_t *__r
   }
   __syncthreads();
   const uint32_t n = s_n;
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-    const uint64_t sc = s_sc[i], idx = s_idx[i];
-    uint32_t rank = 0;
-    for (uint32_t j = 0; j < n; ++j)
-      rank += (s_sc[j] > sc || (s_sc[j] == sc && s_idx[j] < idx)) ? 1u : 0u;
-    if (rank < want) {
-      cand[rank] = TopCand{idx, sc};
-      top_cur[rank] = s_cur[i];
+  // a row outside the pool (a corrupt segment) is a redo too
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+    if (s_idx[i] >= pool) atomicOr(&s_ref, 1u);
+  __syncthreads();
+  if (s_ref) {  // (block-uniform) a redo: sentinel rows, so the uniques pass idles
+    for (uint32_t i = threadIdx.x; i < want; i += blockDim.x) {
+      cand[i] = TopCand{~0ull, 0ull};
+      top_cur[i] = 0;
+    }
+  } else {
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+      const uint64_t sc = s_sc[i], idx = s_idx[i];
+      uint32_t rank = 0;
+      for (uint32_t j = 0; j < n; ++j)
+        rank += (s_sc[j] > sc || (s_sc[j] == sc && s_idx[j] < idx)) ? 1u : 0u;
+      if (rank < want) {
+        cand[rank] = TopCand{idx, sc};
+        top_cur[rank] = s_cur[i];
+      }
     }
   }
   if (threadIdx.x == 0) {
@@ -116,18 +138,18 @@ __global__ __launch_bounds__(kAdoptBlock) void k_slice_adopt(const uint64_t *__r
 }  // namespace
 
 hipError_t launch_slice_seg(const TopCand *cand, const uint64_t *top_cur, const TopState *st,
-                            const uint64_t *stats, uint32_t m, uint64_t lo, uint64_t *seg,
+                            const uint64_t *stats, uint32_t m, uint64_t lo, uint64_t n, uint64_t *seg,
                             hipStream_t s) {
-  hipLaunchKernelGGL(k_slice_seg, dim3(1), dim3(256), 0, s, cand, top_cur, st, stats, m, lo, seg);
+  hipLaunchKernelGGL(k_slice_seg, dim3(1), dim3(256), 0, s, cand, top_cur, st, stats, m, lo, n, seg);
   return hipGetLastError();
 }
 
 hipError_t launch_slice_adopt(const uint64_t *all, uint32_t world, uint64_t stride, uint32_t want,
-                              TopCand *cand, uint64_t *top_cur, TopState *st, uint64_t *stats,
-                              hipStream_t s) {
+                              uint64_t pool, TopCand *cand, uint64_t *top_cur, TopState *st,
+                              uint64_t *stats, hipStream_t s) {
   if ((uint64_t)world * want > (uint64_t)kAdoptMax) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_slice_adopt, dim3(1), dim3(kAdoptBlock), 0, s, all, world, stride, want, cand,
-                     top_cur, st, stats);
+  hipLaunchKernelGGL(k_slice_adopt, dim3(1), dim3(kAdoptBlock), 0, s, all, world, stride, want, pool,
+                     cand, top_cur, st, stats);
   return hipGetLastError();
 }
 

@@ -21,6 +21,7 @@
 // positions are kept: the uniques of these modes come from the rescan pass.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -260,7 +261,14 @@ __global__ __launch_bounds__(kPartBlock) void k_part_gen(KmerInput in, int k, Fa
 // 16-B loads in flight per CU, no gain)
 constexpr int kSplitBlock = kPartBlock;
 constexpr int kSplitPer = kPartTile / kSplitBlock;  // 16
-__global__ __launch_bounds__(kSplitBlock) void k_split(GenPartArgs ga, PartArgs pa) {
+// snap_lo / snap_hi (null: 0 / the whole region): the records [lo, hi) of each
+// coarse bucket, so that the split of one k_part_gen launch's records runs on
+// another stream while the next launch hashes (split_pipelined, nk_counter.cpp).
+// Workgroup L takes tiles L / nb, L / nb + tpb, ... of coarse bucket L % nb.
+__global__ __launch_bounds__(kSplitBlock) void k_split(GenPartArgs ga, PartArgs pa,
+                                                       const unsigned long long *__restrict__ snap_lo,
+                                                       const unsigned long long *__restrict__ snap_hi,
+                                                       uint32_t tpb) {
   using S = GenShape<false>;
   __shared__ uint32_t s_cnt[kMaxSplit + 1];
   __shared__ uint32_t s_start[kMaxSplit + 1];
@@ -275,38 +283,53 @@ __global__ __launch_bounds__(kSplitBlock) void k_split(GenPartArgs ga, PartArgs 
   // Gbase config-5 input, profiles/r04_t3), and bucket b stays on XCD b % 8
   // (nb a multiple of 8), its fine regions' partial lines in one L2
   const uint32_t cb = blockIdx.x % ga.n_buckets;
-  uint64_t n = ga.fill[cb] & ((1ull << 40) - 1);  // (bits 40..: kept segments)
+  // (fill bits 40..: kept segments; the region's records are [0, min(fill, cap)),
+  // multiples of 8, as are the snapshots)
+  uint64_t n = snap_hi ? snap_hi[cb] : ga.fill[cb] & ((1ull << 40) - 1);
   if (n > ga.cap) n = ga.cap;
-  const uint64_t t0 = (uint64_t)(blockIdx.x / ga.n_buckets) * kPartTile;
-  if (t0 >= n) return;  // uniform
+  const uint64_t lo = snap_lo ? snap_lo[cb] : 0;
   const uint32_t F = 1u << (ga.bin_bits - kBinBits);
   const uint32_t cmask = (uint32_t)((1ull << ga.bin_bits) - 1ull);
-  for (uint32_t f = tid; f <= F; f += kSplitBlock) s_cnt[f] = 0;
-  __syncthreads();
   const uint32_t *src = reinterpret_cast<const uint32_t *>(ga.rec) + (uint64_t)cb * ga.cap;
-  // 16 records per lane: four 16-B loads (the region is a multiple of 8
-  // records and 64-record aligned; records past n are ignored)
-  constexpr int kL = kSplitPer / 4;
-  uint4 v[kL];
-  const uint64_t i0 = t0 + (uint64_t)tid * kSplitPer;
+  for (uint64_t t0 = lo + (uint64_t)(blockIdx.x / ga.n_buckets) * kPartTile; t0 < n;
+       t0 += (uint64_t)tpb * kPartTile) {
+    __syncthreads();  // (the previous tile's sort_and_store is done with the LDS)
+    for (uint32_t f = tid; f <= F; f += kSplitBlock) s_cnt[f] = 0;
+    __syncthreads();
+    // 16 records per lane: four 16-B loads (the region is a multiple of 8
+    // records and 64-record aligned; records past n are ignored)
+    constexpr int kL = kSplitPer / 4;
+    uint4 v[kL];
+    const uint64_t i0 = t0 + (uint64_t)tid * kSplitPer;
 #pragma unroll
-  for (int t = 0; t < kL; ++t) {
-    const uint64_t i = i0 + 4 * t;
-    v[t] = i < n ? *reinterpret_cast<const uint4 *>(src + i) : make_uint4(~0u, ~0u, ~0u, ~0u);
-  }
-  uint32_t E[kSplitPer], O[kSplitPer];
+    for (int t = 0; t < kL; ++t) {
+      const uint64_t i = i0 + 4 * t;
+      v[t] = i < n ? *reinterpret_cast<const uint4 *>(src + i) : make_uint4(~0u, ~0u, ~0u, ~0u);
+    }
+    uint32_t E[kSplitPer], O[kSplitPer];
 #pragma unroll
-  for (int j = 0; j < kSplitPer; ++j) {
-    const uint4 &w = v[j >> 2];
-    const uint32_t o = (j & 3) == 0 ? w.x : (j & 3) == 1 ? w.y : (j & 3) == 2 ? w.z : w.w;
-    const bool ok = o != 0xFFFFFFFFu && i0 + j < n;
-    const uint32_t f = ok ? ((o & cmask) >> kBinBits) : F;  // (lane tag bits dropped)
-    E[j] = (f << 16) | atomicAdd(&s_cnt[f], 1u);
-    O[j] = o & (kBinsPerBucket - 1);
+    for (int j = 0; j < kSplitPer; ++j) {
+      const uint4 &w = v[j >> 2];
+      const uint32_t o = (j & 3) == 0 ? w.x : (j & 3) == 1 ? w.y : (j & 3) == 2 ? w.z : w.w;
+      const bool ok = o != 0xFFFFFFFFu && i0 + j < n;
+      const uint32_t f = ok ? ((o & cmask) >> kBinBits) : F;  // (lane tag bits dropped)
+      E[j] = (f << 16) | atomicAdd(&s_cnt[f], 1u);
+      O[j] = o & (kBinsPerBucket - 1);
+    }
+    sort_and_store<false, kSplitPer, kSplitBlock>(E, O, F, s_cnt, s_start, s_base, s_fit, s_rec, s_gmap,
+                                                  pa.fill, pa.overflow, pa.cap, pa.off, (uint64_t)cb * F,
+                                                  kBinBits, pa.currents);
   }
-  sort_and_store<false, kSplitPer, kSplitBlock>(E, O, F, s_cnt, s_start, s_base, s_fit, s_rec, s_gmap,
-                                                pa.fill, pa.overflow, pa.cap, pa.off, (uint64_t)cb * F,
-                                                kBinBits, pa.currents);
+}
+
+// the records each coarse bucket holds now (min(fill, cap)): the upper end of
+// one k_part_gen launch's records for the split that runs beside the next
+__global__ void k_fill_snap(const unsigned long long *__restrict__ fill, uint32_t nb, uint64_t cap,
+                            unsigned long long *__restrict__ snap) {
+  for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += gridDim.x * blockDim.x) {
+    const uint64_t n = fill[b] & ((1ull << 40) - 1);
+    snap[b] = n < cap ? n : cap;
+  }
 }
 
 // U1g: the tiles that hold records of the top rows in the kept Gen/Wide
@@ -588,7 +611,12 @@ hipError_t launch_part_gen(const KmerInput &in, int k, int canonical, int km, ui
     return hipErrorInvalidValue;
   const FastMod fm = make_fastmod(pool);
   const dim3 g((unsigned)in.n_tiles), b(kPartBlock);
-#define NK_GEN(KM_, C_, W_) hipLaunchKernelGGL((k_part_gen<KM_, C_, W_>), g, b, 0, s, in, k, fm, ga)
+  // A/B (occupancy sensitivity): NK_GEN_DYN_LDS bytes of unused dynamic LDS per workgroup
+  static const unsigned dyn = [] {
+    const char *e = getenv("NK_GEN_DYN_LDS");
+    return e ? (unsigned)strtoul(e, nullptr, 10) : 0u;
+  }();
+#define NK_GEN(KM_, C_, W_) hipLaunchKernelGGL((k_part_gen<KM_, C_, W_>), g, b, dyn, s, in, k, fm, ga)
 #define NK_GEN_W(KM_, C_) \
   do {                    \
     if (wide) NK_GEN(KM_, C_, true); else NK_GEN(KM_, C_, false); \
@@ -622,12 +650,29 @@ hipError_t launch_uniq_tiles(const GenPartArgs &ga, int wide, const UniqArgs &u,
   return hipGetLastError();
 }
 
-hipError_t launch_split(const GenPartArgs &ga, const PartArgs &pa, hipStream_t s) {
+hipError_t launch_split(const GenPartArgs &ga, const PartArgs &pa, hipStream_t s,
+                        const unsigned long long *snap_lo, const unsigned long long *snap_hi,
+                        uint64_t est_records) {
   if (!ga.n_buckets) return hipSuccess;
   if (ga.bin_bits < kBinBits || ga.bin_bits - kBinBits > kMaxSplitBits) return hipErrorInvalidValue;
-  const uint64_t tx = (ga.cap + kPartTile - 1) / kPartTile;
+  // tiles per coarse bucket in the grid: the region (whole split), or the
+  // expected share of a range (1.25x + one tile; a bucket past it loops)
+  uint64_t tx = (ga.cap + kPartTile - 1) / kPartTile;
+  if (snap_hi && est_records) {
+    const uint64_t t = (est_records / ga.n_buckets * 5 / 4 + kPartTile - 1) / kPartTile + 1;
+    if (t < tx) tx = t;
+  }
+  if (!tx) tx = 1;
   if (tx * ga.n_buckets > 0x7FFFFFFFull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_split, dim3((unsigned)(tx * ga.n_buckets)), dim3(kSplitBlock), 0, s, ga, pa);
+  hipLaunchKernelGGL(k_split, dim3((unsigned)(tx * ga.n_buckets)), dim3(kSplitBlock), 0, s, ga, pa,
+                     snap_lo, snap_hi, (uint32_t)tx);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_snap(const GenPartArgs &ga, unsigned long long *snap, hipStream_t s) {
+  if (!ga.n_buckets) return hipSuccess;
+  hipLaunchKernelGGL(k_fill_snap, dim3((ga.n_buckets + 255) / 256), dim3(256), 0, s, ga.fill,
+                     ga.n_buckets, ga.cap, snap);
   return hipGetLastError();
 }
 

@@ -342,6 +342,8 @@ POOL2 = 2_000_000
     (33, 30_000_001, True, 64, "queue1"),  # hits resolved in place (LDS hit queue of 1)
     (33, 30_000_001, False, 64, 2),       # Wide, pack_kmer keys, list overflow
     (63, C5_POOL, True, 64, None),        # config-5 pool, compat keys
+    (63, C5_POOL, True, 128, "split7"),   # config 5: the split pipelined over 7 launches
+    (33, 30_000_001, False, 64, "split3"),  # Wide, pack_kmer keys, 3 launches
 ])
 def test_uniques_from_kept_records(k, pool, canon, width, tile_list):
     """Gen/Wide counts keep k_part_gen's records and segment descriptors; the
@@ -354,6 +356,7 @@ def test_uniques_from_kept_records(k, pool, canon, width, tile_list):
     r.process_parallel_arrays(bases, offs, THREADS)
     kv = ({"NK_NO_LANE_TAG": 1} if tile_list == "untagged" else
           {"NK_UNIQ_HIT_QUEUE": 1} if tile_list == "queue1" else
+          {"NK_SPLIT_LAUNCHES": int(tile_list[5:])} if str(tile_list).startswith("split") else
           {"NK_UNIQ_TILE_LIST": tile_list} if tile_list else {})
     with env(**kv):
         g = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, canon, kmer_width=width)

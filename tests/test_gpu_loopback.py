@@ -9,8 +9,9 @@ k-mer union exchange and its redo, the reduce-scatter's slice padding were
 unchecked past one rank).
 
 Each case shards the records over the ranks, runs the N-rank steps, and
-compares every rank's finished state bit-exactly with one handle counting all
-the records (and, for the plain finish, with oracle/nk_oracle.c).
+compares every rank's finished state bit-exactly with oracle/nk_oracle.c
+counting all the records (the 20000-step refine cases: with one handle counting
+all the records, itself checked against the oracle at 20000 steps).
 
 Reference: src/spiking_hash.rs:84-201 (process_parallel: the rayon reduce of
 per-record currents the all-reduce replaces), :661-673 (top rows).
@@ -148,6 +149,7 @@ def test_loopback_finalize_dist(world, wire, cap):
     (4, 64, (1 << 22) + 5, 1000, 4),      # truncated key segments: redo through nk_adopt_slices
     (3, 64, 2_000_000, 1000, 4096),       # the metric's pool
     (2, 64, 2_000_000, 20000, 4096),      # spike counts past 4095 in a slice: the refine redo
+    (3, 64, 2_000_000, 20000, 4096),      # ... at world 3, after every case above in this process
 ])
 def test_loopback_finalize_sliced_dist(world, width, pool, steps, cap):
     """nk_finalize_sliced_dist: reduce-scatter of a zero-padded wire (a pool
@@ -177,13 +179,25 @@ def test_loopback_finalize_sliced_dist(world, width, pool, steps, cap):
         return st
 
     got = _run_ranks(world, body)
-    one = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, True, kmer_width=width)
-    one.set_steps(steps)
-    for _ in range(2):
-        one.process_parallel_arrays(bases, offs)
-    want = _state(one)
-    one.close()
-    if steps > 1000:
+    if steps <= 1000:  # against the restatement (oracle/nk_oracle.c)
+        from oracle import cbind
+        ref = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, True, width=width)
+        ref.set_steps(steps)
+        for _ in range(2):
+            ref.process_parallel_arrays(bases, offs, 4)
+        want = {"currents": ref.currents(), "spike_counts": ref.spike_counts(),
+                "voltages": ref.voltages().view(np.uint32), "refractory": ref.refractory(),
+                "total_spikes": ref.total_spikes, "energy_used": ref.energy_used(),
+                "top": ref.top_abundant_neurons(20)}
+    else:  # 20000 LIF steps over 2 M neurons is minutes for the serial restatement:
+        # one handle counting every record (itself bit-exact vs the oracle at
+        # 20000 steps, tests/test_gpu_parity.py::test_parity_steps)
+        one = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, True, kmer_width=width)
+        one.set_steps(steps)
+        for _ in range(2):
+            one.process_parallel_arrays(bases, offs)
+        want = _state(one)
+        one.close()
         assert int(want["spike_counts"].max()) > 4095  # the case this parameter exists for
     for r in range(world):
         lo, hi, _ = nkdist.slice_bounds(pool, world, r)
@@ -202,4 +216,9 @@ def test_loopback_group_errors():
     g = nkdist.LoopbackGroup(2)
     with pytest.raises(NeuroKmerError):
         nkdist.Comm.loopback(g, 2, 0)
+    c0 = nkdist.Comm.loopback(g, 0, 0)
+    with pytest.raises(NeuroKmerError):  # a rank joins once
+        nkdist.Comm.loopback(g, 0, 0)
+    c0.close()
+    nkdist.Comm.loopback(g, 0, 0).close()  # ... again after it left
     g.close()
