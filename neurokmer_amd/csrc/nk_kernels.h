@@ -357,6 +357,13 @@ hipError_t launch_uniq_tiles(const GenPartArgs &ga, int wide, const UniqArgs &u,
 hipError_t launch_split(const GenPartArgs &ga, const PartArgs &fine, hipStream_t s,
                         const unsigned long long *snap_lo = nullptr,
                         const unsigned long long *snap_hi = nullptr, uint64_t est_records = 0);
+// the wide count's hash of in's tiles fused with the split of the previous
+// launch's records [snap_lo[b], snap_hi[b]) (about split_records of them;
+// snap_hi null: no split)
+hipError_t launch_gen_split(const KmerInput &in, int k, int canonical, int km, uint64_t pool,
+                            const GenPartArgs &ga, const PartArgs &fine,
+                            const unsigned long long *snap_lo, const unsigned long long *snap_hi,
+                            uint64_t split_records, hipStream_t s);
 // snap[b] = min(records reserved in coarse bucket b, cap)
 hipError_t launch_fill_snap(const GenPartArgs &ga, unsigned long long *snap, hipStream_t s);
 // the exact table's kmer_per_neuron: a key array (wpk u64 words per key, *n_keys

@@ -200,45 +200,54 @@ __device__ __forceinline__ void gen_rolled128(const TileLds<kPartTile, false> &L
   }
 }
 
-// K1g: hash + partition for key modes KM 0/1/2 (see the file comment).
-// Lane = 16 consecutive positions of an 8192-position tile.
+// LDS of one k_part_gen tile (and, aliased in one union, of one k_split tile:
+// k_gen_split runs both in one workgroup)
+template <bool WIDE, bool RAW>
+struct GenLds {
+  using S = GenShape<WIDE>;
+  TileLds<kPartTile, RAW> L;
+  uint32_t s_cnt[S::kMaxB + 1];
+  uint32_t s_start[S::kMaxB + 1];
+  uint32_t s_base[S::kMaxB];
+  uint32_t s_fit[S::kMaxB];
+  __align__(16) typename S::Rec s_rec[S::kSlots];
+  typename S::GMap s_gmap[S::kGroups];
+};
+
+// K1g: hash + partition for key modes KM 0/1/2 (see the file comment) of
+// tile in.tile_base + bi.  Lane = 16 consecutive positions of an 8192-position tile.
 template <int KM, bool CANON, bool WIDE>
-__global__ __launch_bounds__(kPartBlock) void k_part_gen(KmerInput in, int k, FastMod fm,
-                                                         GenPartArgs ga) {
+__device__ __forceinline__ void gen_tile(const KmerInput &in, int k, const FastMod &fm,
+                                         const GenPartArgs &ga, uint64_t bi,
+                                         GenLds<WIDE, !CANON> &sm) {
   using S = GenShape<WIDE>;
   constexpr bool kRaw = !CANON;
-  __shared__ TileLds<kPartTile, kRaw> L;
-  __shared__ uint32_t s_cnt[S::kMaxB + 1];
-  __shared__ uint32_t s_start[S::kMaxB + 1];
-  __shared__ uint32_t s_base[S::kMaxB];
-  __shared__ uint32_t s_fit[S::kMaxB];
-  __shared__ __align__(16) typename S::Rec s_rec[S::kSlots];
-  __shared__ typename S::GMap s_gmap[S::kGroups];
-
+  TileLds<kPartTile, kRaw> &L = sm.L;
   const int tid = threadIdx.x;
-  const uint64_t tile = in.tile_base + blockIdx.x;
+  const uint64_t tile = in.tile_base + bi;
   const uint64_t T0 = tile * (uint64_t)kPartTile;
   const uint32_t nb = ga.n_buckets;
   const int bb = ga.bin_bits;
   const bool small_pool = fm.p < (1ull << 30);  // the 32-bit modulo (nk_device.h) holds
   const uint32_t omask = (uint32_t)((1ull << bb) - 1ull);
   const uint32_t ltag = (WIDE && ga.lane_tag) ? ((uint32_t)tid << bb) : 0u;  // (GenPartArgs::lane_tag)
-  for (uint32_t b = tid; b <= nb; b += kPartBlock) s_cnt[b] = 0;
+  for (uint32_t b = tid; b <= nb; b += kPartBlock) sm.s_cnt[b] = 0;
   stage_tile<kPartTile, kPartBlock, kRaw>(L, in, tile, k);  // syncs
 
   const int q0 = tid * kPer;
   uint32_t E[kPer], O[kPer];
   if constexpr (KM == 2 && CANON) {
     if (k > 48) {  // (uniform) the lane's 16 windows rolled from registers
-      gen_rolled128(L, in, T0, q0, k, fm, small_pool, nb, bb, omask, ltag, s_cnt, E, O);
-      sort_and_store<WIDE, kPer>(E, O, nb, s_cnt, s_start, s_base, s_fit, s_rec, s_gmap, ga.fill,
-                                 ga.overflow, ga.cap, reinterpret_cast<typename S::Rec *>(ga.rec),
-                                 0, bb, ga.currents, ga.desc, ga.max_segs, (uint32_t)tile);
+      gen_rolled128(L, in, T0, q0, k, fm, small_pool, nb, bb, omask, ltag, sm.s_cnt, E, O);
+      sort_and_store<WIDE, kPer>(E, O, nb, sm.s_cnt, sm.s_start, sm.s_base, sm.s_fit, sm.s_rec,
+                                 sm.s_gmap, ga.fill, ga.overflow, ga.cap,
+                                 reinterpret_cast<typename S::Rec *>(ga.rec), 0, bb, ga.currents, ga.desc,
+                                 ga.max_segs, (uint32_t)tile);
       return;
     }
   }
   RecCursor rc;
-  rec_cursor_init<KM>(rc, in, T0 + (uint64_t)q0, blockIdx.x);
+  rec_cursor_init<KM>(rc, in, T0 + (uint64_t)q0, bi);
 #pragma unroll 2
   for (int j = 0; j < kPer; ++j) {
     const int q = q0 + j;
@@ -247,12 +256,19 @@ __global__ __launch_bounds__(kPartBlock) void k_part_gen(KmerInput in, int k, Fa
     if (ok) h = gen_hash<KM>(gen_key<KM, CANON>(L, in, q, T0 + (uint64_t)q, k, rc));
     const uint32_t idx = small_pool ? fastmod32(h, fm) : (uint32_t)fastmod(h, fm);
     const uint32_t b = ok ? (idx >> bb) : nb;
-    E[j] = (b << 16) | atomicAdd(&s_cnt[b], 1u);
+    E[j] = (b << 16) | atomicAdd(&sm.s_cnt[b], 1u);
     O[j] = (idx & omask) | ltag;
   }
-  sort_and_store<WIDE, kPer>(E, O, nb, s_cnt, s_start, s_base, s_fit, s_rec, s_gmap, ga.fill,
-                             ga.overflow, ga.cap, reinterpret_cast<typename S::Rec *>(ga.rec), 0,
+  sort_and_store<WIDE, kPer>(E, O, nb, sm.s_cnt, sm.s_start, sm.s_base, sm.s_fit, sm.s_rec, sm.s_gmap,
+                             ga.fill, ga.overflow, ga.cap, reinterpret_cast<typename S::Rec *>(ga.rec), 0,
                              bb, ga.currents, ga.desc, ga.max_segs, (uint32_t)tile);
+}
+
+template <int KM, bool CANON, bool WIDE>
+__global__ __launch_bounds__(kPartBlock) void k_part_gen(KmerInput in, int k, FastMod fm,
+                                                         GenPartArgs ga) {
+  __shared__ GenLds<WIDE, !CANON> sm;
+  gen_tile<KM, CANON, WIDE>(in, k, fm, ga, blockIdx.x, sm);
 }
 
 // K1s: one 8192-record tile of a coarse bucket (u32 offsets of 2^S bins) ->
@@ -261,28 +277,29 @@ __global__ __launch_bounds__(kPartBlock) void k_part_gen(KmerInput in, int k, Fa
 // 16-B loads in flight per CU, no gain)
 constexpr int kSplitBlock = kPartBlock;
 constexpr int kSplitPer = kPartTile / kSplitBlock;  // 16
-// snap_lo / snap_hi (null: 0 / the whole region): the records [lo, hi) of each
-// coarse bucket, so that the split of one k_part_gen launch's records runs on
-// another stream while the next launch hashes (split_pipelined, nk_counter.cpp).
-// Workgroup L takes tiles L / nb, L / nb + tpb, ... of coarse bucket L % nb.
-__global__ __launch_bounds__(kSplitBlock) void k_split(GenPartArgs ga, PartArgs pa,
-                                                       const unsigned long long *__restrict__ snap_lo,
-                                                       const unsigned long long *__restrict__ snap_hi,
-                                                       uint32_t tpb) {
+struct SplitLds {
   using S = GenShape<false>;
-  __shared__ uint32_t s_cnt[kMaxSplit + 1];
-  __shared__ uint32_t s_start[kMaxSplit + 1];
-  __shared__ uint32_t s_base[kMaxSplit];
-  __shared__ uint32_t s_fit[kMaxSplit];
-  __shared__ __align__(16) uint16_t s_rec[S::kSlots];
-  __shared__ S::GMap s_gmap[S::kGroups];
+  uint32_t s_cnt[kMaxSplit + 1];
+  uint32_t s_start[kMaxSplit + 1];
+  uint32_t s_base[kMaxSplit];
+  uint32_t s_fit[kMaxSplit];
+  __align__(16) uint16_t s_rec[S::kSlots];
+  S::GMap s_gmap[S::kGroups];
+};
+
+// K1s work item j of `items` in all: coarse bucket cb = j % nb takes the items
+// j = cb, cb + nb, ... (its count: (items - cb + nb - 1) / nb); item j splits
+// its bucket's records [lo, hi) from tile j / nb on, striding by that count.
+// snap_lo / snap_hi (null: 0 / the whole region): one k_part_gen launch's
+// records of each coarse bucket (the pipelined split, k_gen_split).
+__device__ __forceinline__ void split_item(const GenPartArgs &ga, const PartArgs &pa,
+                                           const unsigned long long *__restrict__ snap_lo,
+                                           const unsigned long long *__restrict__ snap_hi, uint64_t j,
+                                           uint64_t items, SplitLds &sm) {
   const int tid = threadIdx.x;
-  // workgroup L takes tile L / nb of coarse bucket L % nb: the workgroups in
-  // flight spread over every coarse bucket (bucket-major order put ~1000 of
-  // them on one bucket's 32 fine fill counters at a time: 131 ms at a 12.5
-  // Gbase config-5 input, profiles/r04_t3), and bucket b stays on XCD b % 8
-  // (nb a multiple of 8), its fine regions' partial lines in one L2
-  const uint32_t cb = blockIdx.x % ga.n_buckets;
+  const uint32_t nb = ga.n_buckets;
+  const uint32_t cb = (uint32_t)(j % nb);
+  const uint64_t stride = (items - cb + nb - 1) / nb;
   // (fill bits 40..: kept segments; the region's records are [0, min(fill, cap)),
   // multiples of 8, as are the snapshots)
   uint64_t n = snap_hi ? snap_hi[cb] : ga.fill[cb] & ((1ull << 40) - 1);
@@ -291,10 +308,9 @@ __global__ __launch_bounds__(kSplitBlock) void k_split(GenPartArgs ga, PartArgs 
   const uint32_t F = 1u << (ga.bin_bits - kBinBits);
   const uint32_t cmask = (uint32_t)((1ull << ga.bin_bits) - 1ull);
   const uint32_t *src = reinterpret_cast<const uint32_t *>(ga.rec) + (uint64_t)cb * ga.cap;
-  for (uint64_t t0 = lo + (uint64_t)(blockIdx.x / ga.n_buckets) * kPartTile; t0 < n;
-       t0 += (uint64_t)tpb * kPartTile) {
-    __syncthreads();  // (the previous tile's sort_and_store is done with the LDS)
-    for (uint32_t f = tid; f <= F; f += kSplitBlock) s_cnt[f] = 0;
+  for (uint64_t t0 = lo + (j / nb) * kPartTile; t0 < n; t0 += stride * kPartTile) {
+    __syncthreads();  // (the LDS is free: the previous tile's stores read it)
+    for (uint32_t f = tid; f <= F; f += kSplitBlock) sm.s_cnt[f] = 0;
     __syncthreads();
     // 16 records per lane: four 16-B loads (the region is a multiple of 8
     // records and 64-record aligned; records past n are ignored)
@@ -308,17 +324,62 @@ __global__ __launch_bounds__(kSplitBlock) void k_split(GenPartArgs ga, PartArgs 
     }
     uint32_t E[kSplitPer], O[kSplitPer];
 #pragma unroll
-    for (int j = 0; j < kSplitPer; ++j) {
-      const uint4 &w = v[j >> 2];
-      const uint32_t o = (j & 3) == 0 ? w.x : (j & 3) == 1 ? w.y : (j & 3) == 2 ? w.z : w.w;
-      const bool ok = o != 0xFFFFFFFFu && i0 + j < n;
+    for (int q = 0; q < kSplitPer; ++q) {
+      const uint4 &w = v[q >> 2];
+      const uint32_t o = (q & 3) == 0 ? w.x : (q & 3) == 1 ? w.y : (q & 3) == 2 ? w.z : w.w;
+      const bool ok = o != 0xFFFFFFFFu && i0 + q < n;
       const uint32_t f = ok ? ((o & cmask) >> kBinBits) : F;  // (lane tag bits dropped)
-      E[j] = (f << 16) | atomicAdd(&s_cnt[f], 1u);
-      O[j] = o & (kBinsPerBucket - 1);
+      E[q] = (f << 16) | atomicAdd(&sm.s_cnt[f], 1u);
+      O[q] = o & (kBinsPerBucket - 1);
     }
-    sort_and_store<false, kSplitPer, kSplitBlock>(E, O, F, s_cnt, s_start, s_base, s_fit, s_rec, s_gmap,
-                                                  pa.fill, pa.overflow, pa.cap, pa.off, (uint64_t)cb * F,
-                                                  kBinBits, pa.currents);
+    sort_and_store<false, kSplitPer, kSplitBlock>(E, O, F, sm.s_cnt, sm.s_start, sm.s_base, sm.s_fit,
+                                                  sm.s_rec, sm.s_gmap, pa.fill, pa.overflow, pa.cap,
+                                                  pa.off, (uint64_t)cb * F, kBinBits, pa.currents);
+  }
+}
+
+// K1s: one 8192-record tile of a coarse bucket (u32 offsets of 2^S bins) ->
+// its 2^(S-15) fine buckets (u16 offsets), the layout k_bucket_hist reads.
+// 512 threads x 16 records (256 x 32 needs 119 VGPRs: the same 32 waves of
+// 16-B loads in flight per CU, no gain).  Workgroup L takes item L: the
+// workgroups in flight spread over every coarse bucket (bucket-major order put
+// ~1000 of them on one bucket's 32 fine fill counters at a time: 131 ms at a
+// 12.5 Gbase config-5 input, profiles/r04_t3), and bucket b stays on XCD b % 8
+// (nb a multiple of 8), its fine regions' partial lines in one L2.
+__global__ __launch_bounds__(kSplitBlock) void k_split(GenPartArgs ga, PartArgs pa,
+                                                       const unsigned long long *__restrict__ snap_lo,
+                                                       const unsigned long long *__restrict__ snap_hi) {
+  __shared__ SplitLds sm;
+  split_item(ga, pa, snap_lo, snap_hi, blockIdx.x, gridDim.x, sm);
+}
+
+// (6 waves per SIMD: three workgroups per CU, as k_part_gen's LDS allows; the
+// split's registers would otherwise leave two)
+#ifndef NK_GS_WAVES
+#define NK_GS_WAVES 6
+#endif
+// K1g of one launch's tiles fused with K1s of the previous launch's records:
+// k_part_gen is VALU-bound (SipHash) and barely slowed by a third fewer
+// workgroups per CU (config 5, 12.5 Gbases: +3 % at two per CU,
+// profiles/r05_b), k_split is bound by its bytes, so every workgroup hashes
+// its tile and then splits one item of the previous launch's records, while
+// the CU's other workgroups keep the SIMDs busy.  (Two streams, one per
+// kernel, hid only ~4 of the split's 18.5 ms: the hardware kept dispatching
+// the hash kernel's workgroups, r05_a/r05_b.)  One LDS union: the split's
+// arrays alias the hash's.
+template <int KM, bool CANON>
+__global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(NK_GS_WAVES))) void k_gen_split(KmerInput in, int k, FastMod fm, GenPartArgs ga,
+                                                         PartArgs pa,
+                                                         const unsigned long long *__restrict__ snap_lo,
+                                                         const unsigned long long *__restrict__ snap_hi) {
+  __shared__ union U {
+    GenLds<true, !CANON> g;
+    SplitLds s;
+  } sm;
+  if (blockIdx.x < in.n_tiles) gen_tile<KM, CANON, true>(in, k, fm, ga, blockIdx.x, sm.g);
+  if (snap_hi) {
+    __syncthreads();  // (the gen tile's last stores still read its LDS)
+    split_item(ga, pa, snap_lo, snap_hi, blockIdx.x, gridDim.x, sm.s);
   }
 }
 
@@ -665,7 +726,42 @@ hipError_t launch_split(const GenPartArgs &ga, const PartArgs &pa, hipStream_t s
   if (!tx) tx = 1;
   if (tx * ga.n_buckets > 0x7FFFFFFFull) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_split, dim3((unsigned)(tx * ga.n_buckets)), dim3(kSplitBlock), 0, s, ga, pa,
-                     snap_lo, snap_hi, (uint32_t)tx);
+                     snap_lo, snap_hi);
+  return hipGetLastError();
+}
+
+hipError_t launch_gen_split(const KmerInput &in, int k, int canonical, int km, uint64_t pool,
+                            const GenPartArgs &ga, const PartArgs &pa,
+                            const unsigned long long *snap_lo, const unsigned long long *snap_hi,
+                            uint64_t split_records, hipStream_t s) {
+  if (pool == 0 || pool > (1ull << 31) || km < 0 || km > 2) return hipErrorInvalidValue;
+  if (ga.n_buckets > (uint32_t)kWideMaxBuckets || ga.bin_bits < kBinBits ||
+      ga.bin_bits - kBinBits > kMaxSplitBits)
+    return hipErrorInvalidValue;
+  if ((km == 0 && k > 32) || (km == 1 && (k <= 32 || k > 64)) || (km == 2 && k > 64) || k < 1)
+    return hipErrorInvalidValue;
+  // at least the tiles to hash, and enough split items for the previous
+  // launch's records (~1.1 tiles each: a bucket past its share loops)
+  uint64_t grid = in.n_tiles;
+  if (snap_hi) {
+    const uint64_t want = (split_records / ga.n_buckets / kPartTile + 1) * ga.n_buckets;
+    if (want > grid) grid = want;
+  }
+  if (!grid) return hipSuccess;
+  if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  const FastMod fm = make_fastmod(pool);
+  const dim3 g((unsigned)grid), b(kPartBlock);
+#define NK_GS(KM_, C_) hipLaunchKernelGGL((k_gen_split<KM_, C_>), g, b, 0, s, in, k, fm, ga, pa, snap_lo, snap_hi)
+  if (canonical) {
+    if (km == 0) NK_GS(0, true);
+    else if (km == 1) NK_GS(1, true);
+    else NK_GS(2, true);
+  } else {
+    if (km == 0) NK_GS(0, false);
+    else if (km == 1) NK_GS(1, false);
+    else NK_GS(2, false);
+  }
+#undef NK_GS
   return hipGetLastError();
 }
 

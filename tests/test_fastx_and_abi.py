@@ -142,3 +142,77 @@ def test_cli_rejects_bad_usage():
     assert r.returncode == 0 and "--pool-size" in r.stderr
     r = subprocess.run([cli, "-i", "x.fa", "-k", "abc"], capture_output=True, text=True)
     assert r.returncode == 2
+
+
+def mapped(path, window, threads):
+    out = subprocess.run([DUMP, str(path), "--mapped", str(window), str(threads)],
+                         capture_output=True, check=True).stdout
+    d = json.loads(out)
+    return d["rc"], [bytes.fromhex(h) for h in d["records"]], d["truncated"], d["fallback"]
+
+
+def _random_fastq(rng, n):
+    """FASTQ with the cases the ingest must get right: CRLF lines, empty
+    sequences, '+' lines with text, a malformed record (header, '+' line or
+    quality length), blank lines between records, blank lines at the end, a
+    cut-off last record, no final newline."""
+    out = []
+    for i in range(n):
+        eol = b"\r\n" if rng.random() < 0.2 else b"\n"
+        ln = int(rng.integers(0, 40)) if rng.random() < 0.9 else 0
+        seq = bytes(rng.choice(list(b"ACGTNacgt"), ln)) if ln else b""
+        qual = b"I" * ln
+        hdr = b"@r%d" % i
+        plus = b"+" if rng.random() < 0.7 else b"+r%d" % i
+        kind = rng.random()
+        if kind < 0.01:
+            hdr = b"r%d" % i           # header without '@'
+        elif kind < 0.02:
+            plus = b"-"                # no '+' line
+        elif kind < 0.03:
+            qual = qual + b"I"         # quality length != sequence length
+        elif kind < 0.04:
+            out.append(b"\n")          # a blank line where a header is due
+        out.append(hdr + eol + seq + eol + plus + eol + qual + eol)
+    data = b"".join(out)
+    tail = rng.random()
+    if tail < 0.2:
+        data += b"\n\n"                # blank lines end the input
+    elif tail < 0.4:
+        data = data.rstrip(b"\n").rstrip(b"\r")  # no final newline
+    elif tail < 0.5:
+        data += b"@cut\nACGT\n+\n"     # cut-off last record
+    return data
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_mapped_fastq_extraction_matches_reader(tmp_path, seed):
+    """The file ingest's host FASTQ extraction (nk_fqhost.cpp: threads over
+    windows of a mapped file) takes exactly the records the sequential reader
+    takes, stops where it stops, and reports a blank line between records
+    (the ingest then falls back to that reader)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    p = tmp_path / "f.fq"
+    p.write_bytes(_random_fastq(rng, int(rng.integers(1, 400))))
+    rc, recs, trunc = native(p)
+    assert rc == 0
+    for window, threads in ((16, 1), (37, 3), (301, 8), (1 << 20, 5)):
+        mrc, mrecs, mtrunc, fb = mapped(p, window, threads)
+        assert mrc == 0
+        if fb:  # only a blank line between records sends the ingest to the reader
+            assert re.search(rb"\n\r?\n", p.read_bytes())
+            continue
+        assert mrecs == recs, (window, threads)
+        assert mtrunc == trunc, (window, threads)
+
+
+def test_mapped_fastq_large_synthetic(tmp_path):
+    bases, offs = synth.make_reads(20_000, 150, seed=5)
+    p = tmp_path / "r.fq"
+    synth.write_fastq(str(p), bases, offs)
+    want = synth.records_list(bases, offs)
+    for window, threads in ((1 << 16, 8), (100_003, 3), (1 << 26, 16)):
+        rc, recs, trunc, fb = mapped(p, window, threads)
+        assert (rc, fb, trunc) == (0, False, False)
+        assert recs == want

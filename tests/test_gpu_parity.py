@@ -659,17 +659,25 @@ def test_process_sequence_matches_reference(canon):
 from neurokmer_amd.fastx import stream_sequences  # noqa: E402
 
 
-def _ingest_check(path, k, pool, canon, streaming, chunk, exact=False):
-    old = os.environ.get("NK_INGEST_CHUNK")
-    os.environ["NK_INGEST_CHUNK"] = str(chunk)
+def _ingest_check(path, k, pool, canon, streaming, chunk, exact=False, fastq_device=False):
+    """fastq_device: the device FASTQ parse (NK_FASTQ_DEVICE, as gzip FASTQ
+    takes) instead of the host extraction of an uncompressed FASTQ."""
+    keys = {"NK_INGEST_CHUNK": str(chunk), "NK_FASTQ_DEVICE": "1" if fastq_device else None}
+    old = {key: os.environ.get(key) for key in keys}
+    for key, v in keys.items():
+        if v is None:
+            os.environ.pop(key, None)
+        else:
+            os.environ[key] = v
     try:
         g = SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, canon, exact_counts=exact)
         (g.process_file_streaming if streaming else g.process_file_parallel)(path)
     finally:
-        if old is None:
-            os.environ.pop("NK_INGEST_CHUNK", None)
-        else:
-            os.environ["NK_INGEST_CHUNK"] = old
+        for key, v in old.items():
+            if v is None:
+                os.environ.pop(key, None)
+            else:
+                os.environ[key] = v
     recs = list(stream_sequences(path))  # the host reader's records (mirror)
     r = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, canon)
     (r.process_streaming if streaming else r.process_parallel)(recs)
@@ -701,7 +709,8 @@ def test_ingest_fasta_chunks(tmp_path, k, canon, chunk):
 
 @pytest.mark.parametrize("chunk", [1000, 30000, 1 << 26])
 @pytest.mark.parametrize("streaming", [True, False])
-def test_ingest_fastq_chunks(tmp_path, chunk, streaming):
+@pytest.mark.parametrize("fastq_device", [False, True])
+def test_ingest_fastq_chunks(tmp_path, chunk, streaming, fastq_device):
     reads, roffs = synth.make_reads(400, 150, seed=5, n_rate=0.005, repeats_per_mb=40_000,
                                     motif_len=50)
     longr, loffs = synth.make_reads(3, 2500, seed=6)  # records longer than a chunk
@@ -710,7 +719,8 @@ def test_ingest_fastq_chunks(tmp_path, chunk, streaming):
                       np.concatenate([roffs, loffs[1:] + roffs[-1]]).astype(np.uint64))
     data = p.read_bytes()
     p.write_bytes(_crlf(data) if chunk == 30000 else data.rstrip(b"\n"))  # CRLF / no final '\n'
-    recs = _ingest_check(str(p), 21, 5003, True, streaming, chunk, exact=chunk == 1000)
+    recs = _ingest_check(str(p), 21, 5003, True, streaming, chunk, exact=chunk == 1000,
+                         fastq_device=fastq_device)
     assert len(recs) == 403
 
 
@@ -730,14 +740,15 @@ def test_ingest_fastq_record_longer_than_carry_room(tmp_path):
     assert len(recs) == 302
 
 
-def test_ingest_fastq_stops_at_malformed_record(tmp_path):
+@pytest.mark.parametrize("fastq_device", [False, True])
+def test_ingest_fastq_stops_at_malformed_record(tmp_path, fastq_device):
     reads, roffs = synth.make_reads(300, 120, seed=7)
     p = tmp_path / "bad.fq"
     synth.write_fastq(str(p), reads, roffs)
     lines = p.read_bytes().split(b"\n")
     lines[4 * 150 + 3] = lines[4 * 150 + 3][:-1]  # record 150: quality one byte short
     p.write_bytes(b"\n".join(lines))
-    recs = _ingest_check(str(p), 19, 3001, True, True, 2000)
+    recs = _ingest_check(str(p), 19, 3001, True, True, 2000, fastq_device=fastq_device)
     assert len(recs) == 150
 
 
@@ -749,6 +760,8 @@ def test_ingest_fastq_blank_lines_use_host_reader(tmp_path):
     lines.insert(4 * 77, b"")  # a blank line between records: skipped by the reader
     p.write_bytes(b"\n".join(lines))
     recs = _ingest_check(str(p), 17, 2003, True, False, 3000)
+    assert len(recs) == 200
+    recs = _ingest_check(str(p), 17, 2003, True, True, 3000, fastq_device=True)
     assert len(recs) == 200
 
 
