@@ -2,12 +2,14 @@
 // nk_process_file_streaming's parser) so its record semantics are testable
 // without a GPU.  Prints JSON: {"rc":..,"err":..,"truncated":..,"records":[hex..]}.
 // batch (argv[2], bases) exercises record batching across buffer refills.
-// --mapped <window> <threads>: the host FASTQ extraction of the file ingest
-// (nk_fqhost.h), window by window as nk_ingest_host.cpp runs it; prints
+// --mapped <window> <threads> [max_rec]: the host FASTQ extraction of the file ingest
+// (nk_fqhost.h: threads pread and parse), window by window as
+// nk_ingest_host.cpp runs it; prints
 // "fallback" (a blank line where a header is due) instead of records then.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <string>
@@ -29,32 +31,35 @@ static void print_records(const std::vector<uint8_t> &bases, const std::vector<u
   }
 }
 
-static int mapped(const char *path, size_t win, int threads) {
-  nk::MappedFile mf;
+static int mapped(const char *path, size_t win, int threads, uint64_t max_rec) {
+  nk::HostFile hf;
   std::string err;
-  int rc = mf.open(path, err);
+  int rc = hf.open(path, err);
   std::vector<uint8_t> bases;
   std::vector<uint64_t> offs{0};
   bool stop = false, blank = false;
-  if (!rc && !mf.size()) {
+  uint8_t b0 = 0;
+  if (!rc && !hf.size()) {
     rc = NK_E_PARSE;
     err = "empty file";
   }
-  if (!rc && mf.data()[0] != '@') {
+  if (!rc && (pread(hf.fd(), &b0, 1, 0) != 1 || b0 != '@')) {
     rc = NK_E_PARSE;
     err = "not FASTQ";
   }
   if (!rc) {
     nk::HostPool pool(threads);
-    std::vector<uint8_t> hb;
+    std::vector<uint8_t> rb, hb;
     std::vector<uint64_t> he;
     uint64_t pos = 0;
     for (;;) {
-      const size_t len = (size_t)std::min<uint64_t>(win, mf.size() - pos);
-      const bool eof = pos + len >= mf.size();
+      const size_t len = (size_t)std::min<uint64_t>(win, hf.size() - pos);
+      const bool eof = pos + len >= hf.size();
+      rb.resize(len + 64);
       hb.resize(len + 1);
       he.resize(nk::fq_max_records(len));
-      nk::FqResult r = nk::fq_extract(mf.data() + pos, len, eof, hb.data(), he.data(), bases.size(), pool);
+      nk::FqResult r = nk::fq_extract(rb.data(), len, eof, hb.data(), he.data(), bases.size(), pool,
+                                      hf.fd(), pos, nullptr, max_rec);
       if (!r.n_rec && !r.stop && !r.blank && !eof) {  // a record longer than the window
         win *= 2;
         continue;
@@ -64,7 +69,7 @@ static int mapped(const char *path, size_t win, int threads) {
       pos += r.consumed;
       if (r.blank) { blank = true; break; }
       if (r.stop) { stop = true; break; }
-      if (eof) break;
+      if (eof && !r.more) break;
     }
   }
   printf("{\"rc\":%d,\"err\":\"%s\",\"truncated\":%s,\"fallback\":%s,\"records\":[", rc, err.c_str(),
@@ -80,7 +85,8 @@ int main(int argc, char **argv) {
     return 2;
   }
   if (argc > 4 && !strcmp(argv[2], "--mapped"))
-    return mapped(argv[1], strtoull(argv[3], nullptr, 10), atoi(argv[4]));
+    return mapped(argv[1], strtoull(argv[3], nullptr, 10), atoi(argv[4]),
+                  argc > 5 ? strtoull(argv[5], nullptr, 10) : ~0ull);
   size_t batch = argc > 2 ? strtoull(argv[2], nullptr, 10) : (1u << 20);
   nk::FastxReader r;
   std::string err;

@@ -181,7 +181,7 @@ hipError_t gen_hist(nk_counter *c, const CountPlan &cp, bool defer_partials, hip
 // k_part_gen launches of a pipelined wide count: G launches of at least
 // kSplitMinTiles tiles each (NK_SPLIT_LAUNCHES: tests / A/B; 1 = one launch,
 // the split after it)
-constexpr uint64_t kSplitMinTiles = 2048;
+constexpr uint64_t kSplitMinTiles = 8192;  // (115 Mbases, 6 launches: +2 % on the count, r05_g)
 
 uint32_t split_launches(uint64_t n_tiles) {
   const char *e = getenv("NK_SPLIT_LAUNCHES");

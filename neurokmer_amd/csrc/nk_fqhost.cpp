@@ -4,7 +4,6 @@
 #include <emmintrin.h>
 #include <fcntl.h>
 #include <string.h>
-#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -62,13 +61,12 @@ void HostPool::run(const std::function<void(int)> &fn) {
   done_cv_.wait(lk, [&] { return pending_ == 0; });
 }
 
-// ---- MappedFile -------------------------------------------------------------
-MappedFile::~MappedFile() {
-  if (p_) munmap((void *)p_, n_);
+// ---- HostFile ---------------------------------------------------------------
+HostFile::~HostFile() {
   if (fd_ >= 0) ::close(fd_);
 }
 
-int MappedFile::open(const char *path, std::string &err) {
+int HostFile::open(const char *path, std::string &err) {
   fd_ = ::open(path, O_RDONLY);
   if (fd_ < 0) {
     err = std::string("cannot open ") + path;
@@ -79,15 +77,7 @@ int MappedFile::open(const char *path, std::string &err) {
     err = std::string("cannot stat ") + path;
     return NK_E_IO;
   }
-  n_ = (size_t)sb.st_size;
-  if (!n_) return NK_OK;
-  void *m = mmap(nullptr, n_, PROT_READ, MAP_PRIVATE, fd_, 0);
-  if (m == MAP_FAILED) {
-    err = std::string("cannot map ") + path;
-    n_ = 0;
-    return NK_E_IO;
-  }
-  p_ = (const uint8_t *)m;
+  n_ = (uint64_t)sb.st_size;
   return NK_OK;
 }
 
@@ -138,16 +128,28 @@ enum Problem : int { kNone = 0, kBad = 1, kBlank = 2 };
 
 }  // namespace
 
-FqResult fq_extract(const uint8_t *in, size_t len, bool eof, uint8_t *bases, uint64_t *ends,
-                    uint64_t base_off, HostPool &pool) {
+FqResult fq_extract(uint8_t *in, size_t len, bool eof, uint8_t *bases, uint64_t *ends,
+                    uint64_t base_off, HostPool &pool, int fd, uint64_t file_off, FqScratch *scratch,
+                    uint64_t max_rec) {
   FqResult res;
   if (!len) return res;
   const int T = (int)std::min<size_t>((size_t)pool.size(), std::max<size_t>(1, len >> 16));
   // (1) every thread indexes the newlines of its slice
-  std::vector<std::vector<uint32_t>> nl(pool.size());
+  FqScratch local;
+  std::vector<std::vector<uint32_t>> &nl = (scratch ? scratch : &local)->nl;
+  if (nl.size() < (size_t)pool.size()) nl.resize(pool.size());
   pool.run([&](int t) {
     if (t >= T) return;
     const size_t a = len * t / T, b = len * (t + 1) / T;
+    if (fd >= 0) {  // this thread's slice, from the page cache (a short read leaves zeros)
+      size_t g = 0;
+      while (a + g < b) {
+        const ssize_t r = pread(fd, in + a + g, b - a - g, (off_t)(file_off + a + g));
+        if (r <= 0) break;
+        g += (size_t)r;
+      }
+      if (a + g < b) memset(in + a + g, 0, b - a - g);
+    }
     nl[t].clear();
     nl[t].reserve((b - a) / 48 + 64);
     find_newlines(in, a, b, nl[t]);
@@ -211,7 +213,11 @@ FqResult fq_extract(const uint8_t *in, size_t len, bool eof, uint8_t *bases, uin
       problem = kind[t];
       break;
     }
-  if (problem == kNone && eof && n_lines > 4 * R) {
+  if (take > max_rec) {  // room for max_rec record ends: the rest next call
+    take = max_rec;
+    problem = kNone;
+    res.more = true;
+  } else if (problem == kNone && eof && n_lines > 4 * R) {
     // lines after the last whole record at the end of the input: blank lines
     // end it (the host reader skips them); else a cut-off or malformed record
     int h = 0;

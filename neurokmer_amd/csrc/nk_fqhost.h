@@ -54,32 +54,45 @@ struct FqResult {
   uint64_t n_bases = 0;   // sequence bytes written
   bool stop = false;      // a malformed record follows them: the stream ends
   bool blank = false;     // a blank line where a header is due follows them
+  bool more = false;      // max_rec cut the window: records follow (call again from consumed)
 };
 
-// Bytes of output a window of `len` input bytes can need: bases <= len,
-// record ends <= len / 6 + 1 (a record has at least 6 bytes: "@\n\n+\n\n").
+// Records a window of `len` input bytes can hold: len / 6 + 1 (a record has
+// at least 6 bytes: "@\n\n+\n\n").  A caller with less room for record ends
+// passes max_rec to fq_extract.
 inline size_t fq_max_records(size_t len) { return len / 6 + 1; }
+
+// Newline positions per thread, kept between calls (allocating ~1.5 MB per
+// thread per window cost more than the scan at small windows, profiles/r05_g)
+struct FqScratch {
+  std::vector<std::vector<uint32_t>> nl;
+};
 
 // The FASTQ records of in[0, len), which starts at a record boundary; eof: the
 // input ends at len (its last line may lack '\n').  Writes every taken record's
 // sequence to bases (contiguous) and ends[i] = base_off + the end of record i's
 // sequence in bases.  len < 2^32.  Without eof, a record cut by the window end
 // is not taken (n_rec == 0 and !stop: the caller widens the window).
-FqResult fq_extract(const uint8_t *in, size_t len, bool eof, uint8_t *bases, uint64_t *ends,
-                    uint64_t base_off, HostPool &pool);
+// fd >= 0: in[0, len) is first read from the file at file_off, each thread its
+// slice (pread straight into the buffer it then scans: the bytes are read from
+// the page cache once and scanned from the thread's cache; a mapping of the
+// file measured slower -- page faults, and an munmap as long as the parse,
+// profiles/r05_f).
+FqResult fq_extract(uint8_t *in, size_t len, bool eof, uint8_t *bases, uint64_t *ends,
+                    uint64_t base_off, HostPool &pool, int fd = -1, uint64_t file_off = 0,
+                    FqScratch *scratch = nullptr, uint64_t max_rec = ~0ull);
 
-// A read-only mapping of a whole file (MAP_PRIVATE).
-class MappedFile {
+// A file opened for reading, with its size.
+class HostFile {
  public:
-  ~MappedFile();
+  ~HostFile();
   int open(const char *path, std::string &err);  // 0 or an NK_E_* code
-  const uint8_t *data() const { return p_; }
-  size_t size() const { return n_; }
+  int fd() const { return fd_; }
+  uint64_t size() const { return n_; }
 
  private:
-  const uint8_t *p_ = nullptr;
-  size_t n_ = 0;
   int fd_ = -1;
+  uint64_t n_ = 0;
 };
 
 }  // namespace nk

@@ -170,6 +170,7 @@ struct nk_counter {
   PinnedBuf ing_he[3];
   hipEvent_t fq_ev[3] = {};
   HostPool *fq_pool = nullptr;
+  FqScratch fq_scratch;
   // LIF table cache key
   bool lif_valid = false;
   LifParams lif_key{};

@@ -2,6 +2,8 @@
 // (src/utils.rs:9-24 stream_sequences, src/spiking_hash.rs:277-486).
 #include "nk_handle.h"
 
+#include <unistd.h>
+
 // ---------------------------------------------------------------------------
 // Chunked accumulate over a growing resident input (GPU FASTX ingest)
 // ---------------------------------------------------------------------------
@@ -111,27 +113,50 @@ size_t ingest_chunk_bytes() {
   return v;
 }
 
-// An uncompressed FASTQ file: host threads parse the mapped file window by
-// window (nk_fqhost.h) and only each window's sequence bytes and record ends
-// cross PCIe, straight into the resident input (bases, offsets), where the
-// count takes them.  Three stages overlap: the parse of window w + 1, the H2D
-// of window w (copy stream) and the count of window w (count stream); the
-// pinned buffers rotate over three windows.  Headers and quality lines never
-// leave the host (~52 % of a 150-bp FASTQ's bytes: the device FASTQ parse
-// shipped them all, 268 ms for config 3's 10 GB file, profiles/r04_s12).
-static int ingest_fastq_host(nk_counter *c, const MappedFile &mf, bool *fallback, hipStream_t s) {
-  const uint8_t *file = mf.data();
-  const uint64_t fsize = mf.size();
+// An uncompressed FASTQ file: host threads read it window by window (each its
+// slice, pread) and parse it (nk_fqhost.h); only each window's sequence bytes
+// and record ends cross PCIe, straight into the resident input (bases,
+// offsets), where the count takes them.  Three stages overlap: the read +
+// parse of window w + 1, the H2D of window w (copy stream) and its count
+// (count stream); the pinned output buffers rotate over three windows.
+// Headers and quality lines never leave the host (~52 % of a 150-bp FASTQ's
+// bytes: the device FASTQ parse shipped them all, 268 ms for config 3's 10 GB
+// file, profiles/r04_s12).  64 MiB windows: config 3's 10 GB file in 164-169
+// ms (16 MiB: 205-272, 4 MiB: 440 -- per-window costs, profiles/r05_g).
+static size_t fq_window_bytes() {
+  const char *e = getenv("NK_FQ_WINDOW");  // tests / A/B
+  size_t v = e ? (size_t)strtoull(e, nullptr, 10) : 0;
+  if (!v) {
+    const char *ic = getenv("NK_INGEST_CHUNK");  // (tests: small windows like small chunks)
+    v = ic ? (size_t)strtoull(ic, nullptr, 10) : (size_t)64 << 20;
+  }
+  return std::max<size_t>(v, 64);
+}
+
+// record ends a window's pinned buffer holds: one per 32 bytes (a 150-bp
+// FASTQ record is ~330); windows of shorter records are taken in several calls
+// (NK_FQ_MAX_REC, tests: a small cap takes every window in several calls)
+static uint64_t max_rec_for(size_t w) {
+  const char *e = getenv("NK_FQ_MAX_REC");
+  const uint64_t forced = e ? strtoull(e, nullptr, 10) : 0ull;
+  return forced ? forced : w / 32 + 1024;
+}
+
+static int ingest_fastq_host(nk_counter *c, const HostFile &hf, bool *fallback, hipStream_t s) {
+  const int fd = hf.fd();
+  const uint64_t fsize = hf.size();
   int rc;
-  size_t win = ingest_chunk_bytes();
+  size_t win = fq_window_bytes();
   if ((rc = c->in_bases.ensure(fsize + 80)) || (rc = c->in_offs.ensure(std::max<size_t>(c->in_offs.n, 1025))))
     return rc;
-  auto pinned = [&](size_t w) -> int {
+  std::vector<uint8_t> rbuf;  // the window's file bytes (host memory, reused)
+  auto buffers = [&](size_t w) -> int {
+    rbuf.resize(w + 64);
     for (int i = 0; i < 3; ++i)
-      if ((rc = c->ing_hb[i].ensure(w)) || (rc = c->ing_he[i].ensure(fq_max_records(w) * 8))) return rc;
+      if ((rc = c->ing_hb[i].ensure(w)) || (rc = c->ing_he[i].ensure(max_rec_for(w) * 8))) return rc;
     return NK_OK;
   };
-  if ((rc = pinned(win))) return rc;
+  if ((rc = buffers(win))) return rc;
   if (!c->ing_cs) {
     HIPCHK(hipStreamCreateWithFlags(&c->ing_cs, hipStreamNonBlocking));
     for (hipEvent_t &e : c->ing_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -151,10 +176,11 @@ static int ingest_fastq_host(nk_counter *c, const MappedFile &mf, bool *fallback
     FqResult r;
   };
   bool used[3] = {false, false, false};  // the buffer has an H2D in flight (its event)
-  auto parse = [c, file, &used](Job j) -> Job {
+  auto parse = [c, fd, &rbuf, &used](Job j) -> Job {
     if (used[j.b]) (void)hipEventSynchronize(c->fq_ev[j.b]);
-    j.r = fq_extract(file + j.pos, j.len, j.eof, c->ing_hb[j.b].p,
-                     reinterpret_cast<uint64_t *>(c->ing_he[j.b].p), j.base_off, *c->fq_pool);
+    j.r = fq_extract(rbuf.data(), j.len, j.eof, c->ing_hb[j.b].p,
+                     reinterpret_cast<uint64_t *>(c->ing_he[j.b].p), j.base_off, *c->fq_pool, fd, j.pos,
+                     &c->fq_scratch, max_rec_for(j.len));
     return j;
   };
   std::future<Job> fut;
@@ -192,7 +218,7 @@ static int ingest_fastq_host(nk_counter *c, const MappedFile &mf, bool *fallback
       HIPCHK(hipStreamSynchronize(cs));
       HIPCHK(hipStreamSynchronize(s));
       win *= 2;
-      if ((rc = pinned(win))) return rc;
+      if ((rc = buffers(win))) return rc;
       used[0] = used[1] = used[2] = false;
       fut = std::async(std::launch::async, parse, window(j.pos, j.base_off, j.b));
       continue;
@@ -202,7 +228,7 @@ static int ingest_fastq_host(nk_counter *c, const MappedFile &mf, bool *fallback
       return NK_OK;
     }
     const clk::time_point t1 = clk::now();
-    const bool last = j.eof || j.r.stop;
+    const bool last = j.r.stop || (j.eof && !j.r.more);
     if (!last)  // the next window parses while this one goes up and is counted
       fut = std::async(std::launch::async, parse,
                        window(j.pos + j.r.consumed, j.base_off + j.r.n_bases, (j.b + 1) % 3));
@@ -255,11 +281,13 @@ int ingest_file(nk_counter *c, const char *path, bool *fallback) {
   {
     // uncompressed FASTQ: the host extraction (NK_FASTQ_DEVICE=1, tests and
     // A/B: the device parse of every byte, as gzip input still takes)
-    MappedFile mf;
-    std::string merr;
-    if (mf.open(path, merr) == NK_OK && mf.size() && mf.data()[0] == '@' && !getenv("NK_FASTQ_DEVICE")) {
+    HostFile hf;
+    std::string ferr;
+    uint8_t b0 = 0;
+    if (hf.open(path, ferr) == NK_OK && hf.size() && pread(hf.fd(), &b0, 1, 0) == 1 && b0 == '@' &&
+        !getenv("NK_FASTQ_DEVICE")) {
       (void)hipSetDevice(c->device);
-      return ingest_fastq_host(c, mf, fallback, pick_stream(c, nullptr));
+      return ingest_fastq_host(c, hf, fallback, pick_stream(c, nullptr));
     }
   }
   ChunkSource src;

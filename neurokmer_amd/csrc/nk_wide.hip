@@ -271,10 +271,6 @@ __global__ __launch_bounds__(kPartBlock) void k_part_gen(KmerInput in, int k, Fa
   gen_tile<KM, CANON, WIDE>(in, k, fm, ga, blockIdx.x, sm);
 }
 
-// K1s: one 8192-record tile of a coarse bucket (u32 offsets of 2^S bins) ->
-// its 2^(S-15) fine buckets (u16 offsets), the layout k_bucket_hist reads.
-// 512 threads x 16 records (256 x 32 needs 119 VGPRs: the same 32 waves of
-// 16-B loads in flight per CU, no gain)
 constexpr int kSplitBlock = kPartBlock;
 constexpr int kSplitPer = kPartTile / kSplitBlock;  // 16
 struct SplitLds {
@@ -291,11 +287,15 @@ struct SplitLds {
 // j = cb, cb + nb, ... (its count: (items - cb + nb - 1) / nb); item j splits
 // its bucket's records [lo, hi) from tile j / nb on, striding by that count.
 // snap_lo / snap_hi (null: 0 / the whole region): one k_part_gen launch's
-// records of each coarse bucket (the pipelined split, k_gen_split).
+// records of each coarse bucket (the pipelined split, k_gen_split).  PER
+// records per lane: a tile of 8192 records goes in 16 / PER rounds of
+// 512 * PER records (k_gen_split: 8, half the registers of 16).
+template <int PER>
 __device__ __forceinline__ void split_item(const GenPartArgs &ga, const PartArgs &pa,
                                            const unsigned long long *__restrict__ snap_lo,
                                            const unsigned long long *__restrict__ snap_hi, uint64_t j,
                                            uint64_t items, SplitLds &sm) {
+  static_assert(PER % 4 == 0 && kSplitPer % PER == 0, "whole 16-B loads, whole rounds per tile");
   const int tid = threadIdx.x;
   const uint32_t nb = ga.n_buckets;
   const uint32_t cb = (uint32_t)(j % nb);
@@ -308,33 +308,36 @@ __device__ __forceinline__ void split_item(const GenPartArgs &ga, const PartArgs
   const uint32_t F = 1u << (ga.bin_bits - kBinBits);
   const uint32_t cmask = (uint32_t)((1ull << ga.bin_bits) - 1ull);
   const uint32_t *src = reinterpret_cast<const uint32_t *>(ga.rec) + (uint64_t)cb * ga.cap;
+  constexpr uint64_t kRound = (uint64_t)PER * kSplitBlock;
   for (uint64_t t0 = lo + (j / nb) * kPartTile; t0 < n; t0 += stride * kPartTile) {
-    __syncthreads();  // (the LDS is free: the previous tile's stores read it)
-    for (uint32_t f = tid; f <= F; f += kSplitBlock) sm.s_cnt[f] = 0;
-    __syncthreads();
-    // 16 records per lane: four 16-B loads (the region is a multiple of 8
-    // records and 64-record aligned; records past n are ignored)
-    constexpr int kL = kSplitPer / 4;
-    uint4 v[kL];
-    const uint64_t i0 = t0 + (uint64_t)tid * kSplitPer;
+    for (uint64_t r0 = t0; r0 < t0 + kPartTile && r0 < n; r0 += kRound) {  // (uniform)
+      __syncthreads();  // (the LDS is free: the previous round's stores read it)
+      for (uint32_t f = tid; f <= F; f += kSplitBlock) sm.s_cnt[f] = 0;
+      __syncthreads();
+      // PER records per lane: PER / 4 16-B loads (the region is a multiple of 8
+      // records and 64-record aligned; records past n are ignored)
+      constexpr int kL = PER / 4;
+      uint4 v[kL];
+      const uint64_t i0 = r0 + (uint64_t)tid * PER;
 #pragma unroll
-    for (int t = 0; t < kL; ++t) {
-      const uint64_t i = i0 + 4 * t;
-      v[t] = i < n ? *reinterpret_cast<const uint4 *>(src + i) : make_uint4(~0u, ~0u, ~0u, ~0u);
-    }
-    uint32_t E[kSplitPer], O[kSplitPer];
+      for (int t = 0; t < kL; ++t) {
+        const uint64_t i = i0 + 4 * t;
+        v[t] = i < n ? *reinterpret_cast<const uint4 *>(src + i) : make_uint4(~0u, ~0u, ~0u, ~0u);
+      }
+      uint32_t E[PER], O[PER];
 #pragma unroll
-    for (int q = 0; q < kSplitPer; ++q) {
-      const uint4 &w = v[q >> 2];
-      const uint32_t o = (q & 3) == 0 ? w.x : (q & 3) == 1 ? w.y : (q & 3) == 2 ? w.z : w.w;
-      const bool ok = o != 0xFFFFFFFFu && i0 + q < n;
-      const uint32_t f = ok ? ((o & cmask) >> kBinBits) : F;  // (lane tag bits dropped)
-      E[q] = (f << 16) | atomicAdd(&sm.s_cnt[f], 1u);
-      O[q] = o & (kBinsPerBucket - 1);
+      for (int q = 0; q < PER; ++q) {
+        const uint4 &w = v[q >> 2];
+        const uint32_t o = (q & 3) == 0 ? w.x : (q & 3) == 1 ? w.y : (q & 3) == 2 ? w.z : w.w;
+        const bool ok = o != 0xFFFFFFFFu && i0 + q < n;
+        const uint32_t f = ok ? ((o & cmask) >> kBinBits) : F;  // (lane tag bits dropped)
+        E[q] = (f << 16) | atomicAdd(&sm.s_cnt[f], 1u);
+        O[q] = o & (kBinsPerBucket - 1);
+      }
+      sort_and_store<false, PER, kSplitBlock>(E, O, F, sm.s_cnt, sm.s_start, sm.s_base, sm.s_fit,
+                                              sm.s_rec, sm.s_gmap, pa.fill, pa.overflow, pa.cap,
+                                              pa.off, (uint64_t)cb * F, kBinBits, pa.currents);
     }
-    sort_and_store<false, kSplitPer, kSplitBlock>(E, O, F, sm.s_cnt, sm.s_start, sm.s_base, sm.s_fit,
-                                                  sm.s_rec, sm.s_gmap, pa.fill, pa.overflow, pa.cap,
-                                                  pa.off, (uint64_t)cb * F, kBinBits, pa.currents);
   }
 }
 
@@ -350,13 +353,16 @@ __global__ __launch_bounds__(kSplitBlock) void k_split(GenPartArgs ga, PartArgs 
                                                        const unsigned long long *__restrict__ snap_lo,
                                                        const unsigned long long *__restrict__ snap_hi) {
   __shared__ SplitLds sm;
-  split_item(ga, pa, snap_lo, snap_hi, blockIdx.x, gridDim.x, sm);
+  split_item<kSplitPer>(ga, pa, snap_lo, snap_hi, blockIdx.x, gridDim.x, sm);
 }
 
 // (6 waves per SIMD: three workgroups per CU, as k_part_gen's LDS allows; the
 // split's registers would otherwise leave two)
 #ifndef NK_GS_WAVES
 #define NK_GS_WAVES 6
+#endif
+#ifndef NK_GS_SPLIT_PER  // records per lane per round of the fused split (8: no spills at 6 waves)
+#define NK_GS_SPLIT_PER 8
 #endif
 // K1g of one launch's tiles fused with K1s of the previous launch's records:
 // k_part_gen is VALU-bound (SipHash) and barely slowed by a third fewer
@@ -368,7 +374,7 @@ __global__ __launch_bounds__(kSplitBlock) void k_split(GenPartArgs ga, PartArgs 
 // the hash kernel's workgroups, r05_a/r05_b.)  One LDS union: the split's
 // arrays alias the hash's.
 template <int KM, bool CANON>
-__global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(NK_GS_WAVES))) void k_gen_split(KmerInput in, int k, FastMod fm, GenPartArgs ga,
+__global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(CANON ? NK_GS_WAVES : 4))) void k_gen_split(KmerInput in, int k, FastMod fm, GenPartArgs ga,
                                                          PartArgs pa,
                                                          const unsigned long long *__restrict__ snap_lo,
                                                          const unsigned long long *__restrict__ snap_hi) {
@@ -379,7 +385,7 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(NK_G
   if (blockIdx.x < in.n_tiles) gen_tile<KM, CANON, true>(in, k, fm, ga, blockIdx.x, sm.g);
   if (snap_hi) {
     __syncthreads();  // (the gen tile's last stores still read its LDS)
-    split_item(ga, pa, snap_lo, snap_hi, blockIdx.x, gridDim.x, sm.s);
+    split_item<NK_GS_SPLIT_PER>(ga, pa, snap_lo, snap_hi, blockIdx.x, gridDim.x, sm.s);
   }
 }
 

@@ -144,9 +144,11 @@ def test_cli_rejects_bad_usage():
     assert r.returncode == 2
 
 
-def mapped(path, window, threads):
-    out = subprocess.run([DUMP, str(path), "--mapped", str(window), str(threads)],
-                         capture_output=True, check=True).stdout
+def mapped(path, window, threads, max_rec=None):
+    args = [DUMP, str(path), "--mapped", str(window), str(threads)]
+    if max_rec:
+        args.append(str(max_rec))
+    out = subprocess.run(args, capture_output=True, check=True).stdout
     d = json.loads(out)
     return d["rc"], [bytes.fromhex(h) for h in d["records"]], d["truncated"], d["fallback"]
 
@@ -197,8 +199,9 @@ def test_mapped_fastq_extraction_matches_reader(tmp_path, seed):
     p.write_bytes(_random_fastq(rng, int(rng.integers(1, 400))))
     rc, recs, trunc = native(p)
     assert rc == 0
-    for window, threads in ((16, 1), (37, 3), (301, 8), (1 << 20, 5)):
-        mrc, mrecs, mtrunc, fb = mapped(p, window, threads)
+    for window, threads, max_rec in ((16, 1, None), (37, 3, None), (301, 8, None), (1 << 20, 5, None),
+                                     (1 << 20, 4, 7), (5000, 2, 1)):
+        mrc, mrecs, mtrunc, fb = mapped(p, window, threads, max_rec)
         assert mrc == 0
         if fb:  # only a blank line between records sends the ingest to the reader
             assert re.search(rb"\n\r?\n", p.read_bytes())

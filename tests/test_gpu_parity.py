@@ -659,10 +659,13 @@ def test_process_sequence_matches_reference(canon):
 from neurokmer_amd.fastx import stream_sequences  # noqa: E402
 
 
-def _ingest_check(path, k, pool, canon, streaming, chunk, exact=False, fastq_device=False):
+def _ingest_check(path, k, pool, canon, streaming, chunk, exact=False, fastq_device=False,
+                  max_rec=None):
     """fastq_device: the device FASTQ parse (NK_FASTQ_DEVICE, as gzip FASTQ
-    takes) instead of the host extraction of an uncompressed FASTQ."""
-    keys = {"NK_INGEST_CHUNK": str(chunk), "NK_FASTQ_DEVICE": "1" if fastq_device else None}
+    takes) instead of the host extraction of an uncompressed FASTQ; max_rec:
+    record ends per host window call (NK_FQ_MAX_REC)."""
+    keys = {"NK_INGEST_CHUNK": str(chunk), "NK_FASTQ_DEVICE": "1" if fastq_device else None,
+            "NK_FQ_MAX_REC": str(max_rec) if max_rec else None}
     old = {key: os.environ.get(key) for key in keys}
     for key, v in keys.items():
         if v is None:
@@ -740,15 +743,16 @@ def test_ingest_fastq_record_longer_than_carry_room(tmp_path):
     assert len(recs) == 302
 
 
-@pytest.mark.parametrize("fastq_device", [False, True])
-def test_ingest_fastq_stops_at_malformed_record(tmp_path, fastq_device):
+@pytest.mark.parametrize("fastq_device,max_rec", [(False, None), (True, None), (False, 7)])
+def test_ingest_fastq_stops_at_malformed_record(tmp_path, fastq_device, max_rec):
     reads, roffs = synth.make_reads(300, 120, seed=7)
     p = tmp_path / "bad.fq"
     synth.write_fastq(str(p), reads, roffs)
     lines = p.read_bytes().split(b"\n")
     lines[4 * 150 + 3] = lines[4 * 150 + 3][:-1]  # record 150: quality one byte short
     p.write_bytes(b"\n".join(lines))
-    recs = _ingest_check(str(p), 19, 3001, True, True, 2000, fastq_device=fastq_device)
+    recs = _ingest_check(str(p), 19, 3001, True, True, 2000, fastq_device=fastq_device,
+                         max_rec=max_rec)
     assert len(recs) == 150
 
 
