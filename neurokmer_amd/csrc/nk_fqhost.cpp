@@ -217,6 +217,19 @@ FqResult fq_extract(uint8_t *in, size_t len, bool eof, uint8_t *bases, uint64_t 
     take = max_rec;
     problem = kNone;
     res.more = true;
+    // the thread holding record `take` summed past it: its bases up to take
+    for (int t = 0; t < T; ++t) {
+      const uint64_t r0 = R * t / T, r1 = R * (t + 1) / T;
+      if (r0 < take && take < r1) {
+        int h = 0;
+        uint64_t sb = 0;
+        for (uint64_t r = r0; r < take; ++r) {
+          const uint64_t s0 = L.end(4 * r, h) + 1, s1 = L.end(4 * r + 1, h);
+          sb += s1 - s0 - (s1 > s0 && in[s1 - 1] == '\r' ? 1 : 0);
+        }
+        sum[t] = sb;
+      }
+    }
   } else if (problem == kNone && eof && n_lines > 4 * R) {
     // lines after the last whole record at the end of the input: blank lines
     // end it (the host reader skips them); else a cut-off or malformed record

@@ -202,8 +202,11 @@ __device__ __forceinline__ uint64_t window_key(const TileLds<TILE, RAW> &L, int 
 struct Key128 {
   uint64_t lo, hi;
 };
+// (non-short-circuit: three 64-bit compares whose masks combine on the scalar
+// unit; the ?: form cost five more VALU instructions per key, v_cndmask
+// chains over booleans)
 __device__ __forceinline__ bool key128_less(const Key128 &a, const Key128 &b) {
-  return a.hi != b.hi ? a.hi < b.hi : a.lo < b.lo;
+  return (a.hi < b.hi) | ((a.hi == b.hi) & (a.lo < b.lo));
 }
 template <int TILE, bool RAW, bool CANON>
 __device__ __forceinline__ Key128 window_key128(const TileLds<TILE, RAW> &L, int q, int k) {

@@ -155,6 +155,8 @@ __device__ __forceinline__ void sort_and_store(const uint32_t (&E)[PER], const u
 // 128-bit hash-only floor at a 12.5 Gbase input, profiles/r04_t3).  The same
 // keys as window_key128<CANON> (nk_tile.h); every position is hashed, the
 // ones that start no k-mer go to the no-record bucket nb.
+// SH >= 0: 128 - 2k at compile time (k = 63: SH = 2; -1: k at run time).
+template <int SH>
 __device__ __forceinline__ void gen_rolled128(const TileLds<kPartTile, false> &L, const KmerInput &in,
                                               uint64_t T0, int q0, int k, const FastMod &fm,
                                               bool small_pool, uint32_t nb, int bb, uint32_t omask,
@@ -181,14 +183,24 @@ __device__ __forceinline__ void gen_rolled128(const TileLds<kPartTile, false> &L
   for (int j = 0; j < kPer; ++j) {
     uint32_t W[4], Y[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      W[c] = j ? __builtin_amdgcn_alignbit(Fw[c], Fw[c + 1], 32 - 2 * j) : Fw[c];
-      Y[c] = j ? __builtin_amdgcn_alignbit(Rw[c + 1], Rw[c], 2 * j) : Rw[c];
-    }
+    for (int c = 0; c < 4; ++c) Y[c] = j ? __builtin_amdgcn_alignbit(Rw[c + 1], Rw[c], 2 * j) : Rw[c];
     Key128 fwd, rev;
-    fwd.lo = ((uint64_t)__builtin_amdgcn_alignbit(W[1], W[2], sh) << 32) |
-             __builtin_amdgcn_alignbit(W[2], W[3], sh);
-    fwd.hi = ((uint64_t)(W[0] >> sh) << 32) | __builtin_amdgcn_alignbit(W[0], W[1], sh);
+    if (SH >= 0 && 2 * j >= SH) {
+      // (k compile-time) the forward strand is the stream at bit offset
+      // 2j - SH, its top SH bits masked: one funnel shift per word
+      constexpr uint32_t kTop = SH >= 0 ? 0xFFFFFFFFu >> (SH & 31) : 0u;
+      const int o = 2 * j - SH;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) W[c] = o ? __builtin_amdgcn_alignbit(Fw[c], Fw[c + 1], 32 - o) : Fw[c];
+      fwd.lo = ((uint64_t)W[2] << 32) | W[3];
+      fwd.hi = ((uint64_t)(W[0] & kTop) << 32) | W[1];
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) W[c] = j ? __builtin_amdgcn_alignbit(Fw[c], Fw[c + 1], 32 - 2 * j) : Fw[c];
+      fwd.lo = ((uint64_t)__builtin_amdgcn_alignbit(W[1], W[2], sh) << 32) |
+               __builtin_amdgcn_alignbit(W[2], W[3], sh);
+      fwd.hi = ((uint64_t)(W[0] >> sh) << 32) | __builtin_amdgcn_alignbit(W[0], W[1], sh);
+    }
     rev.lo = ((uint64_t)Y[1] << 32) | Y[0];
     rev.hi = (((uint64_t)Y[3] << 32) | Y[2]) & hmask;
     const Key128 key = key128_less(rev, fwd) ? rev : fwd;
@@ -238,7 +250,10 @@ __device__ __forceinline__ void gen_tile(const KmerInput &in, int k, const FastM
   uint32_t E[kPer], O[kPer];
   if constexpr (KM == 2 && CANON) {
     if (k > 48) {  // (uniform) the lane's 16 windows rolled from registers
-      gen_rolled128(L, in, T0, q0, k, fm, small_pool, nb, bb, omask, ltag, sm.s_cnt, E, O);
+      if (k == 63)  // config 5
+        gen_rolled128<2>(L, in, T0, q0, k, fm, small_pool, nb, bb, omask, ltag, sm.s_cnt, E, O);
+      else
+        gen_rolled128<-1>(L, in, T0, q0, k, fm, small_pool, nb, bb, omask, ltag, sm.s_cnt, E, O);
       sort_and_store<WIDE, kPer>(E, O, nb, sm.s_cnt, sm.s_start, sm.s_base, sm.s_fit, sm.s_rec,
                                  sm.s_gmap, ga.fill, ga.overflow, ga.cap,
                                  reinterpret_cast<typename S::Rec *>(ga.rec), 0, bb, ga.currents, ga.desc,

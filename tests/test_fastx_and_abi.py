@@ -154,6 +154,7 @@ def mapped(path, window, threads, max_rec=None):
 
 
 def _random_fastq(rng, n):
+    import numpy as np
     """FASTQ with the cases the ingest must get right: CRLF lines, empty
     sequences, '+' lines with text, a malformed record (header, '+' line or
     quality length), blank lines between records, blank lines at the end, a
@@ -162,18 +163,18 @@ def _random_fastq(rng, n):
     for i in range(n):
         eol = b"\r\n" if rng.random() < 0.2 else b"\n"
         ln = int(rng.integers(0, 40)) if rng.random() < 0.9 else 0
-        seq = bytes(rng.choice(list(b"ACGTNacgt"), ln)) if ln else b""
+        seq = rng.choice(np.frombuffer(b"ACGTNacgt", np.uint8), ln).tobytes() if ln else b""
         qual = b"I" * ln
         hdr = b"@r%d" % i
         plus = b"+" if rng.random() < 0.7 else b"+r%d" % i
         kind = rng.random()
-        if kind < 0.01:
+        if kind < 0.002:
             hdr = b"r%d" % i           # header without '@'
-        elif kind < 0.02:
+        elif kind < 0.004:
             plus = b"-"                # no '+' line
-        elif kind < 0.03:
+        elif kind < 0.006:
             qual = qual + b"I"         # quality length != sequence length
-        elif kind < 0.04:
+        elif kind < 0.008:
             out.append(b"\n")          # a blank line where a header is due
         out.append(hdr + eol + seq + eol + plus + eol + qual + eol)
     data = b"".join(out)
