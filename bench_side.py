@@ -361,8 +361,9 @@ def _config3_run(args, path, fsize, n_reads, nk, k, pool, L, dev, Counter, synth
                  "150-bp reads, @r%09d headers, constant quality 'I')"),
         "config": {"workload": (f"config 3: {fsize / 1e9:.2f} GB FASTQ ({n_reads:,} reads x {L} bp, "
                                 f"{nk:,} k-mers), k=31, pool_size=16,000,000, --canonical, "
-                                f"--streaming (nk_process_file_streaming: GPU FASTQ parse, "
-                                f"chunked count as the chunks arrive, streaming LIF rule)"),
+                                f"--streaming (nk_process_file_streaming: host threads read and "
+                                f"parse 64 MiB windows, only sequence bytes + record ends cross "
+                                f"PCIe, chunked count as they arrive, streaming LIF rule)"),
                    "k": k, "pool_size": pool, "file_bytes": fsize, "reads": n_reads,
                    "kmers": nk, "parallelism": "dp1"},
         "end_to_end": {"file_gb_per_s": round(fsize / t / 1e9, 2),
@@ -371,13 +372,15 @@ def _config3_run(args, path, fsize, n_reads, nk, k, pool, L, dev, Counter, synth
                        "resident_step_ms": round(float(np.median(tot)), 3),
                        "resident_mkmers_per_s": round(nk / (float(np.median(tot)) * 1e-3) / 1e6, 1),
                        "pcie_floor_ms": round(fsize / h2d * 1e3, 1),
-                       "limiter": ("the file path: three stages overlap (the host reads chunk c+2 "
-                                   "from the page cache into pinned memory, the copy stream moves "
-                                   "c+1 up, the device parses and counts c); the host read is the "
-                                   "slowest (NK_INGEST_PROFILE=1, profiles/r04_s8).  The step is "
-                                   "%.1fx the resident count + LIF and %.2fx the PCIe floor; the "
-                                   "file moves %.1fx the bases" % (t * 1e3 / float(np.median(tot)),
-                                                                   t / (fsize / h2d), fsize / n_b))},
+                       "limiter": ("the file path: three stages overlap (16 host threads pread and "
+                                   "parse window w+1 of the file, the copy stream moves window w's "
+                                   "sequence bytes and record ends up, the device counts them); the "
+                                   "host read + parse is the slowest (NK_INGEST_PROFILE=1: the "
+                                   "parse wait).  The step is %.1fx the resident count + LIF and "
+                                   "%.2fx the PCIe floor of the whole file; the file moves %.1fx the "
+                                   "bases, of which only the bases cross PCIe" % (
+                                       t * 1e3 / float(np.median(tot)), t / (fsize / h2d),
+                                       fsize / n_b))},
         "roofline": {"bound": "hbm" if alg / (cm * 1e-3) / HBM_PEAK >= 0.6 else "latency",
                      "kernel": "the resident count of the reads (every batch's K1 + K1b)",
                      "achieved": round(alg / (cm * 1e-3) / 1e9, 2), "peak": HBM_PEAK / 1e9,

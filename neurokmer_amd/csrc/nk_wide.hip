@@ -693,12 +693,7 @@ hipError_t launch_part_gen(const KmerInput &in, int k, int canonical, int km, ui
     return hipErrorInvalidValue;
   const FastMod fm = make_fastmod(pool);
   const dim3 g((unsigned)in.n_tiles), b(kPartBlock);
-  // A/B (occupancy sensitivity): NK_GEN_DYN_LDS bytes of unused dynamic LDS per workgroup
-  static const unsigned dyn = [] {
-    const char *e = getenv("NK_GEN_DYN_LDS");
-    return e ? (unsigned)strtoul(e, nullptr, 10) : 0u;
-  }();
-#define NK_GEN(KM_, C_, W_) hipLaunchKernelGGL((k_part_gen<KM_, C_, W_>), g, b, dyn, s, in, k, fm, ga)
+#define NK_GEN(KM_, C_, W_) hipLaunchKernelGGL((k_part_gen<KM_, C_, W_>), g, b, 0, s, in, k, fm, ga)
 #define NK_GEN_W(KM_, C_) \
   do {                    \
     if (wide) NK_GEN(KM_, C_, true); else NK_GEN(KM_, C_, false); \
