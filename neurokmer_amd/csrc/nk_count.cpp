@@ -107,8 +107,14 @@ int plan_count(nk_counter *c, uint64_t est_bases, uint64_t slack, uint64_t max_s
   int rc;
   uint64_t cap;
   if (cp.path == CountPath::Wide) {
+    // at most 128 coarse buckets (the kernels take 256): ~64 records per
+    // (tile, coarse bucket) segment instead of ~33 -- half the pad records and
+    // descriptors, a 64-way split.  Config 5 (P = 256 M): 123 buckets of 2^21
+    // bins, the count 77.1 ms against 79.7 with 245 of 2^20 and 79.4 with 62 of
+    // 2^22 (the uniques scan of a top bucket grows with it, profiles/r05_i)
+    constexpr uint64_t kCoarse = 128;
     int bits = kBinBits;
-    while (((P + (1ull << bits) - 1) >> bits) > (uint64_t)kWideMaxBuckets) ++bits;
+    while (((P + (1ull << bits) - 1) >> bits) > kCoarse) ++bits;
     if (forced > bits) bits = std::min(forced, kBinBits + kMaxSplitBits);
     const uint64_t C = (P + (1ull << bits) - 1) >> bits;
     uint64_t cap_c = est / C * 5 / 4 + slack;

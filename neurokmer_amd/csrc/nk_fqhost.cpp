@@ -14,6 +14,10 @@
 namespace nk {
 
 // ---- HostPool ---------------------------------------------------------------
+namespace {
+constexpr int kSpin = 1 << 14;  // pause iterations before a thread blocks (~0.2-0.5 ms)
+}
+
 HostPool::HostPool(int threads) : n_(std::max(1, threads)) {
   for (int t = 1; t < n_; ++t) th_.emplace_back(&HostPool::loop, this, t);
 }
@@ -21,7 +25,7 @@ HostPool::HostPool(int threads) : n_(std::max(1, threads)) {
 HostPool::~HostPool() {
   {
     std::lock_guard<std::mutex> lk(mu_);
-    quit_ = true;
+    quit_.store(true);
   }
   cv_.notify_all();
   for (auto &t : th_) t.join();
@@ -30,17 +34,23 @@ HostPool::~HostPool() {
 void HostPool::loop(int t) {
   uint64_t seen = 0;
   for (;;) {
-    const std::function<void(int)> *fn;
-    {
-      std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
-      if (quit_) return;
-      seen = gen_;
-      fn = fn_;
+    uint64_t g = gen_.load(std::memory_order_acquire);
+    for (int i = 0; g == seen && !quit_.load(std::memory_order_relaxed); ++i) {
+      if (i < kSpin) {
+        _mm_pause();
+      } else {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_.load(std::memory_order_acquire) != seen || quit_.load(); });
+      }
+      g = gen_.load(std::memory_order_acquire);
     }
-    (*fn)(t);
-    std::lock_guard<std::mutex> lk(mu_);
-    if (--pending_ == 0) done_cv_.notify_one();
+    if (quit_.load()) return;
+    seen = g;
+    (*fn_)(t);
+    if (pending_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+      std::lock_guard<std::mutex> lk(mu_);
+      done_cv_.notify_one();
+    }
   }
 }
 
@@ -49,16 +59,22 @@ void HostPool::run(const std::function<void(int)> &fn) {
     fn(0);
     return;
   }
+  fn_ = &fn;
+  pending_.store(n_ - 1, std::memory_order_relaxed);
+  gen_.fetch_add(1, std::memory_order_release);
   {
-    std::lock_guard<std::mutex> lk(mu_);
-    fn_ = &fn;
-    pending_ = n_ - 1;
-    ++gen_;
+    std::lock_guard<std::mutex> lk(mu_);  // (a thread between its check and its wait sees gen_)
   }
   cv_.notify_all();
   fn(0);
-  std::unique_lock<std::mutex> lk(mu_);
-  done_cv_.wait(lk, [&] { return pending_ == 0; });
+  for (int i = 0; pending_.load(std::memory_order_acquire) != 0; ++i) {
+    if (i < kSpin) {
+      _mm_pause();
+    } else {
+      std::unique_lock<std::mutex> lk(mu_);
+      done_cv_.wait(lk, [&] { return pending_.load(std::memory_order_acquire) == 0; });
+    }
+  }
 }
 
 // ---- HostFile ---------------------------------------------------------------

@@ -168,51 +168,36 @@ static int ingest_fastq_host(nk_counter *c, const HostFile &hf, bool *fallback, 
     c->fq_pool = new HostPool((int)std::max<unsigned>(1, std::min<unsigned>(16, hc ? hc : 8)));
   }
   hipStream_t cs = c->ing_cs;
-  struct Job {
-    uint64_t pos, base_off;
-    size_t len;
-    bool eof;
-    int b;
-    FqResult r;
-  };
-  bool used[3] = {false, false, false};  // the buffer has an H2D in flight (its event)
-  auto parse = [c, fd, &rbuf, &used](Job j) -> Job {
-    if (used[j.b]) (void)hipEventSynchronize(c->fq_ev[j.b]);
-    j.r = fq_extract(rbuf.data(), j.len, j.eof, c->ing_hb[j.b].p,
-                     reinterpret_cast<uint64_t *>(c->ing_he[j.b].p), j.base_off, *c->fq_pool, fd, j.pos,
-                     &c->fq_scratch, max_rec_for(j.len));
-    return j;
-  };
-  std::future<Job> fut;
-  // every exit leaves no parse running and no copy in flight from the pinned buffers
+  // every exit leaves no copy in flight from the pinned buffers
   struct Drain {
     hipStream_t cs;
-    std::future<Job> *f;
-    ~Drain() {
-      if (f->valid()) f->wait();
-      (void)hipStreamSynchronize(cs);
-    }
-  } drain{cs, &fut};
+    ~Drain() { (void)hipStreamSynchronize(cs); }
+  } drain{cs};
+  bool used[3] = {false, false, false};  // the buffer has an H2D in flight (its event)
   StreamAcc sa;
   if ((rc = acc_begin(c, fsize / 2, win + 64, sa, s))) return rc;
   HIPCHK(hipMemsetAsync(c->in_offs.p, 0, 8, s));  // offsets[0]
   static const bool prof = getenv("NK_INGEST_PROFILE") != nullptr;
   using clk = std::chrono::steady_clock;
-  double t_wait = 0, t_enq = 0;
+  double t_parse = 0, t_enq = 0;
   uint64_t n_win = 0;
   auto since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
-  auto window = [&](uint64_t pos, uint64_t base_off, int b) {
-    const size_t len = (size_t)std::min<uint64_t>(win, fsize - pos);
-    return Job{pos, base_off, len, pos + len >= fsize, b, FqResult{}};
-  };
-  fut = std::async(std::launch::async, parse, window(0, 0, 0));
-  uint64_t data_end = 0, n_rec = 0, counted = 0;
+  // The host parses window w while the copy engine moves window w - 1 up and
+  // the device counts it (the parse waits only for the H2D that last read the
+  // pinned buffers it writes, window w - 3's).
+  uint64_t pos = 0, data_end = 0, n_rec = 0, counted = 0;
+  int b = 0;
   for (;;) {
+    const size_t len = (size_t)std::min<uint64_t>(win, fsize - pos);
+    const bool eof = pos + len >= fsize;
     const clk::time_point t0 = clk::now();
-    Job j = fut.get();
-    if (prof) t_wait += since(t0);
+    if (used[b]) HIPCHK(hipEventSynchronize(c->fq_ev[b]));
+    const FqResult r = fq_extract(rbuf.data(), len, eof, c->ing_hb[b].p,
+                                  reinterpret_cast<uint64_t *>(c->ing_he[b].p), data_end, *c->fq_pool, fd,
+                                  pos, &c->fq_scratch, max_rec_for(len));
+    if (prof) t_parse += since(t0);
     ++n_win;
-    if (!j.r.n_rec && !j.r.stop && !j.r.blank && !j.eof) {
+    if (!r.n_rec && !r.stop && !r.blank && !eof) {
       // a record longer than the window: widen it (no copy may read the buffers)
       if (win >= ((size_t)1 << 31)) return fail(NK_E_PARSE, "a FASTQ record longer than 2 GiB");
       HIPCHK(hipStreamSynchronize(cs));
@@ -220,37 +205,33 @@ static int ingest_fastq_host(nk_counter *c, const HostFile &hf, bool *fallback, 
       win *= 2;
       if ((rc = buffers(win))) return rc;
       used[0] = used[1] = used[2] = false;
-      fut = std::async(std::launch::async, parse, window(j.pos, j.base_off, j.b));
       continue;
     }
-    if (j.r.blank) {  // a blank line between records: the host reader takes the file
+    if (r.blank) {  // a blank line between records: the host reader takes the file
       *fallback = true;
       return NK_OK;
     }
     const clk::time_point t1 = clk::now();
-    const bool last = j.r.stop || (j.eof && !j.r.more);
-    if (!last)  // the next window parses while this one goes up and is counted
-      fut = std::async(std::launch::async, parse,
-                       window(j.pos + j.r.consumed, j.base_off + j.r.n_bases, (j.b + 1) % 3));
-    if (n_rec + j.r.n_rec + 1 > c->in_offs.n) {  // grow the offsets: wait, copy, free
+    const bool last = r.stop || (eof && !r.more);
+    if (n_rec + r.n_rec + 1 > c->in_offs.n) {  // grow the offsets: wait, copy, free
       HIPCHK(hipStreamSynchronize(cs));
       HIPCHK(hipStreamSynchronize(s));
       DevBuf<uint64_t> no;
-      if ((rc = no.ensure(std::max<uint64_t>(n_rec + j.r.n_rec + 1, 2 * c->in_offs.n)))) return rc;
+      if ((rc = no.ensure(std::max<uint64_t>(n_rec + r.n_rec + 1, 2 * c->in_offs.n)))) return rc;
       HIPCHK(hipMemcpy(no.p, c->in_offs.p, (n_rec + 1) * 8, hipMemcpyDeviceToDevice));
       std::swap(no.p, c->in_offs.p);
       std::swap(no.n, c->in_offs.n);
       no.release();
     }
-    if (j.r.n_bases)
-      HIPCHK(hipMemcpyAsync(c->in_bases.p + data_end, c->ing_hb[j.b].p, j.r.n_bases, hipMemcpyHostToDevice, cs));
-    if (j.r.n_rec)
-      HIPCHK(hipMemcpyAsync(c->in_offs.p + 1 + n_rec, c->ing_he[j.b].p, j.r.n_rec * 8, hipMemcpyHostToDevice, cs));
-    HIPCHK(hipEventRecord(c->fq_ev[j.b], cs));
-    used[j.b] = true;
-    HIPCHK(hipStreamWaitEvent(s, c->fq_ev[j.b], 0));
-    data_end += j.r.n_bases;
-    n_rec += j.r.n_rec;
+    if (r.n_bases)
+      HIPCHK(hipMemcpyAsync(c->in_bases.p + data_end, c->ing_hb[b].p, r.n_bases, hipMemcpyHostToDevice, cs));
+    if (r.n_rec)
+      HIPCHK(hipMemcpyAsync(c->in_offs.p + 1 + n_rec, c->ing_he[b].p, r.n_rec * 8, hipMemcpyHostToDevice, cs));
+    HIPCHK(hipEventRecord(c->fq_ev[b], cs));
+    used[b] = true;
+    HIPCHK(hipStreamWaitEvent(s, c->fq_ev[b], 0));
+    data_end += r.n_bases;
+    n_rec += r.n_rec;
     KmerInput whole{};
     whole.bases = c->in_bases.p;
     whole.offsets = c->in_offs.p;
@@ -265,10 +246,12 @@ static int ingest_fastq_host(nk_counter *c, const HostFile &hf, bool *fallback, 
       if ((rc = acc_end(c, sa, whole, s))) return rc;
       break;
     }
+    pos += r.consumed;
+    b = (b + 1) % 3;
   }
   if (prof)
-    fprintf(stderr, "[nk ingest fastq host] windows %llu  parse wait %.1f ms  enqueue %.1f ms\n",
-            (unsigned long long)n_win, t_wait, t_enq);
+    fprintf(stderr, "[nk ingest fastq host] windows %llu  parse %.1f ms  enqueue %.1f ms\n",
+            (unsigned long long)n_win, t_parse, t_enq);
   return NK_OK;
 }
 
