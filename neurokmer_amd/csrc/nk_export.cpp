@@ -483,6 +483,10 @@ int nk_slice_export(nk_counter *c, int streaming, const uint32_t *d_slice, size_
     // (its uniques bookkeeping is redone for the global rows by nk_adopt_export)
     tf.post = PostArgs{c->set_alloc, nullptr, 0, c->set_mask_d.p, c->tbuckets.p, c->post_flags.p,
                        c->uniq.p, c->special.p, c->n_hits.p, c->last_pa.bin_bits};
+    // the final step writes the slice's segment too (no k_slice_seg launch)
+    tf.seg = d_seg;
+    tf.seg_lo = lo;
+    tf.seg_stats = c->stats.p;
   }
   if (n)
     HIPCHK(launch_lif_apply(c->cur.p + lo, d_slice, 1u, 1, nullptr, (int)c->last_pa.bin_bits,
@@ -500,7 +504,8 @@ int nk_slice_export(nk_counter *c, int streaming, const uint32_t *d_slice, size_
     HIPCHK(launch_topn_threshold(c->hist.p, m, n, c->topst.p, s));
     if ((rc = enqueue_select(c, m, s, lo, n))) return rc;
   }
-  HIPCHK(launch_slice_seg(c->cand.p, c->top_cur.p, c->topst.p, c->stats.p, (uint32_t)m, lo, n, d_seg, s));
+  if (!fuse)
+    HIPCHK(launch_slice_seg(c->cand.p, c->top_cur.p, c->topst.p, c->stats.p, (uint32_t)m, lo, n, d_seg, s));
   c->slice_ready = true;
   return NK_OK;
 }
@@ -519,10 +524,13 @@ int nk_adopt_export(nk_counter *c, const uint64_t *d_all, size_t world, size_t s
   hipStream_t s = pick_stream(c, stream);
   c->slice_ready = false;
   int rc;
-  // every rank's slice yields min(top_n, its size) rows: together >= min(top_n, pool) = want
-  HIPCHK(launch_slice_adopt(d_all, (uint32_t)world, stride, (uint32_t)want, c->pool, c->cand.p,
-                            c->top_cur.p, c->topst.p, c->stats.p, s));
+  // every rank's slice yields min(top_n, its size) rows: together >= min(top_n, pool) = want;
+  // the adopt kernel also runs the top-N post step of the uniques pass (no k_top_post)
   const bool uniq = want && c->have_input && c->last_in.n_tiles;
+  if ((rc = c->tbuckets.ensure(std::max<uint64_t>(want, 1)))) return rc;
+  const PostArgs post = post_args(c, false);
+  HIPCHK(launch_slice_adopt(d_all, (uint32_t)world, stride, (uint32_t)want, c->pool, c->cand.p,
+                            c->top_cur.p, c->topst.p, c->stats.p, s, uniq ? &post : nullptr));
   if ((rc = c->export_n.ensure(1))) return rc;
   if (!c->export_n_zeroed) {
     HIPCHK(hipMemsetAsync(c->export_n.p, 0, 8, s));
@@ -530,7 +538,7 @@ int nk_adopt_export(nk_counter *c, const uint64_t *d_all, size_t world, size_t s
   }
   c->xport_dst = d_keyseg;  // the uniques pass appends each new key to the segment
   c->xport_cap = cap;
-  rc = uniq ? enqueue_uniques(c, (uint32_t)want, false, false, s) : NK_OK;
+  rc = uniq ? enqueue_uniques(c, (uint32_t)want, false, /*post_done=*/true, s) : NK_OK;
   c->xport_dst = nullptr;
   if (rc) return rc;
   MergePrep mp{};

@@ -182,19 +182,39 @@ int enqueue_select(nk_counter *c, uint64_t want, hipStream_t s, uint64_t lo,
 #ifndef NK_U1_SLICE_BUDGET
 #define NK_U1_SLICE_BUDGET 1024  // scan workgroups per launch (A/B: 1024 with 4 loads in flight best)
 #endif
+// the top-N post step's arguments for the uniques pass that follows (the count
+// path's buckets: Part, or kept Gen/Wide records; none for a rescan).  The
+// caller has sized c->tbuckets for the rows.
+PostArgs post_args(nk_counter *c, bool rescan) {
+  const bool part = c->part_used && !rescan;
+  const bool genk = c->gen_keep && !rescan;
+  PostArgs pa{};
+  pa.set_alloc = c->set_alloc;
+  pa.overflow = part ? c->p_over.p : genk ? c->last_ga.overflow : nullptr;
+  pa.part = (part || genk) ? 1 : 0;
+  pa.set_mask = c->set_mask_d.p;
+  pa.tbuckets = c->tbuckets.p;
+  pa.flags = c->post_flags.p;
+  pa.uniq = c->uniq.p;
+  pa.special = c->special.p;
+  pa.n_hits = c->n_hits.p;
+  pa.bin_bits = genk ? (uint32_t)c->last_ga.bin_bits : c->last_pa.bin_bits;
+  pa.n_over = part ? c->last_pa.n_buckets : genk ? c->last_ga.n_buckets : 0u;
+  return pa;
+}
+
 int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, bool post_done,
                            hipStream_t s) {
   const bool part = c->part_used && !rescan;
   const bool genk = c->gen_keep && !rescan;  // kept Gen/Wide records: rescan the hit tiles only
   int rc;
   if ((rc = c->tbuckets.ensure(m))) return rc;
-  if (!post_done)
-    HIPCHK(launch_top_post(c->cand.p, c->top_cur.p, m, c->set_alloc,
-                           part ? c->p_over.p : genk ? c->last_ga.overflow : nullptr,
-                           (part || genk) ? 1 : 0, c->set_mask_d.p, c->tbuckets.p, c->post_flags.p,
-                           c->uniq.p, c->special.p, c->n_hits.p,
-                           genk ? (uint32_t)c->last_ga.bin_bits : c->last_pa.bin_bits, s,
-                           part ? c->last_pa.n_buckets : genk ? c->last_ga.n_buckets : 0u));
+  if (!post_done) {
+    const PostArgs pa = post_args(c, rescan);
+    HIPCHK(launch_top_post(c->cand.p, c->top_cur.p, m, pa.set_alloc, pa.overflow, pa.part, pa.set_mask,
+                           pa.tbuckets, pa.flags, pa.uniq, pa.special, pa.n_hits, pa.bin_bits, s,
+                           pa.n_over));
+  }
   // the set must be empty up to the pass's mask: after the count's prep it is
   c->dirty_before = c->set_clean ? 0 : c->set_alloc;
   if (!part || !c->set_clean)

@@ -392,6 +392,7 @@ int enqueue_lif(nk_counter *c, int streaming, uint32_t fuse_want, bool part,
                        hipStream_t s, const uint32_t *wire = nullptr);
 int enqueue_select(nk_counter *c, uint64_t want, hipStream_t s, uint64_t lo = 0,
                           uint64_t n = ~0ull);
+PostArgs post_args(nk_counter *c, bool rescan);
 int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, bool post_done,
                            hipStream_t s);
 int enqueue_readback(nk_counter *c, uint32_t m, bool uniq, hipStream_t s,

@@ -88,7 +88,15 @@ struct TopFuse {
   TopCand *cand;      // final rows, sorted
   uint64_t *top_cur;  // currents of the final rows
   PostArgs post;
+  // the pool-sliced finish (nk_slice_export): the final step also writes this
+  // slice's all-gather segment (k_slice_seg's layout; neurons [seg_lo, ...),
+  // new spikes and largest count from seg_stats); a deferred selection exports
+  // no rows, only the refine flag
+  uint64_t *seg = nullptr;
+  uint64_t seg_lo = 0;
+  const uint64_t *seg_stats = nullptr;
 };
+constexpr uint64_t kSegRefine = 1ull << 56;  // slice segment header: this slice needs the exact refine
 
 constexpr int kZeroMax = 8;
 struct ZeroList {  // (filled with fill[b] bytes: 0, or 0xFF for the uniques set's kEmpty)
@@ -309,9 +317,10 @@ hipError_t launch_slice_seg(const TopCand *cand, const uint64_t *top_cur, const 
                             const uint64_t *stats, uint32_t m, uint64_t lo, uint64_t n, uint64_t *seg,
                             hipStream_t s);
 // (a flagged segment or a row >= pool: want sentinel rows {~0, 0} and st->refine)
+// post (non-null): the top-N post step (k_top_post) for the adopted rows too
 hipError_t launch_slice_adopt(const uint64_t *all, uint32_t world, uint64_t stride, uint32_t want,
                               uint64_t pool, TopCand *cand, uint64_t *top_cur, TopState *st,
-                              uint64_t *stats, hipStream_t s);
+                              uint64_t *stats, hipStream_t s, const PostArgs *post = nullptr);
 hipError_t launch_export(const unsigned long long *set_keys, const uint64_t *set_mask,
                          uint64_t set_alloc, int w128, bool uniq, bool appended,
                          const uint32_t *special, uint32_t n_top, const TopState *st,

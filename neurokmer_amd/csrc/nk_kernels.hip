@@ -26,6 +26,7 @@
 #include "nk_gen.h"
 #include "nk_kernels.h"
 #include "nk_tile.h"
+#include "nk_post.h"
 
 namespace nk {
 
@@ -1281,54 +1282,7 @@ __device__ __forceinline__ T block_excl_scan(T x, T *s_w, T *total) {
   return pre + incl - x;
 }
 
-// Set sizing and bookkeeping for the uniques pass from the final top rows
-// (one block of 1024 threads).
-__device__ void top_post_block(const TopCand *top, const uint64_t *top_cur, uint32_t m,
-                               const PostArgs &pa) {
-  __shared__ unsigned long long s_sum;
-  __shared__ uint32_t s_nb, s_over;
-  __shared__ uint32_t s_bk[kMaxTopN];
-  if (threadIdx.x == 0) { s_sum = 0; s_nb = 0; s_over = 0; *pa.n_hits = 0; }
-  // a sentinel row (index ~0: a selection deferred to the host's exact redo,
-  // k_slice_adopt) takes no part: no bucket, no set capacity, no hits
-  constexpr uint32_t kNoBucket = 0xFFFFFFFFu;
-  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x)
-    s_bk[i] = top[i].idx == ~0ull ? kNoBucket : (uint32_t)(top[i].idx >> pa.bin_bits);
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
-    pa.uniq[i] = 0;
-    pa.special[i] = 0;
-    const uint32_t b = s_bk[i];
-    if (b == kNoBucket) continue;
-    atomicAdd(&s_sum, (unsigned long long)top_cur[i]);
-    if (pa.part) {
-      if (pa.n_over && b >= pa.n_over) {  // a row outside the count's buckets: never indexed
-#ifdef NK_DEBUG_ROWS
-        printf("[nk top_post] row %u index %llu outside the count's %u buckets\n", i,
-               (unsigned long long)top[i].idx, pa.n_over);
-#endif
-        s_over = 1;                          // (the host takes the rescan path)
-        continue;
-      }
-      if (pa.overflow[b]) s_over = 1;
-      bool first = true;  // first row of its bucket in the list
-      for (uint32_t j = 0; j < i; ++j)
-        if (s_bk[j] == b) { first = false; break; }
-      if (first) pa.tbuckets[atomicAdd(&s_nb, 1u)] = b;
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint64_t cap = 64;
-    while (cap < 2 * (uint64_t)s_sum + 2 && cap < (1ull << 48)) cap <<= 1;  // (bounded: a row's
-    // current read before its selection was resolved must not spin the loop)
-    pa.flags[0] = cap > pa.set_alloc ? 1u : 0u;  // set too small
-    pa.flags[1] = s_over;                        // a top bucket overflowed
-    pa.flags[2] = s_nb;                          // distinct top buckets
-    pa.flags[3] = 0;
-    *pa.set_mask = (cap > pa.set_alloc ? pa.set_alloc : cap) - 1;
-  }
-}
+// (top_post_block: nk_post.h)
 
 #ifndef NK_LIF_PER_THREAD
 #define NK_LIF_PER_THREAD 8
@@ -1456,6 +1410,11 @@ __device__ void defer_to_host(const TopFuse &tf) {
   for (int i = 0; i < 4; ++i) tf.post.flags[i] = 0;
   *tf.post.n_hits = 0;
   if (tf.post.set_mask) *tf.post.set_mask = 0;  // the (idle) uniques pass clears one slot
+  if (tf.seg) {  // the slice exports no rows, only the refine flag (k_slice_seg's rule)
+    tf.seg[0] = kSegRefine;
+    tf.seg[1] = tf.seg_stats[0];
+    tf.seg[2] = tf.seg_stats[1];
+  }
 }
 
 // The final selection over the blocks' candidate lists C (one block of
@@ -1600,6 +1559,19 @@ __device__ void final_top(uint64_t pool, const uint64_t *currents, uint32_t nb,
     tf.top_cur[lane] = cur;
     pa.uniq[lane] = 0;
     pa.special[lane] = 0;
+  }
+  if (tf.seg) {  // the slice's all-gather segment (nk_slice_export; k_slice_seg's layout)
+    const bool bad = __ballot(row && !in_pool) != 0;  // a row the passes left unfilled
+    if (row && !bad) {
+      tf.seg[3 + 3 * (uint64_t)lane] = idx + tf.seg_lo;
+      tf.seg[4 + 3 * (uint64_t)lane] = sc;
+      tf.seg[5 + 3 * (uint64_t)lane] = cur;
+    }
+    if (lane == 0) {
+      tf.seg[0] = bad ? kSegRefine : (uint64_t)m;
+      tf.seg[1] = tf.seg_stats[0];
+      tf.seg[2] = tf.seg_stats[1];
+    }
   }
   unsigned long long sum = cur;
   for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);

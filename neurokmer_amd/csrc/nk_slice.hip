@@ -13,13 +13,13 @@
 #include <stdint.h>
 
 #include "nk_kernels.h"
+#include "nk_post.h"
 
 namespace nk {
 
 namespace {
 
-constexpr uint64_t kSegRefine = 1ull << 56;  // header flag: this slice's rows need the exact refine
-constexpr uint64_t kSegCount = (1ull << 56) - 1;
+constexpr uint64_t kSegCount = kSegRefine - 1;  // (kSegRefine: nk_kernels.h)
 
 // seg = [rows | refine << 56, new spikes, largest spike count, (global idx, spikes, current) x rows]
 // A slice whose selection is not resolved on the device (spike counts past
@@ -57,7 +57,8 @@ __global__ __launch_bounds__(kAdoptBlock) void k_slice_adopt(const uint64_t *__r
                                                              TopCand *__restrict__ cand,
                                                              uint64_t *__restrict__ top_cur,
                                                              TopState *__restrict__ st,
-                                                             uint64_t *__restrict__ stats) {
+                                                             uint64_t *__restrict__ stats,
+                                                             PostArgs post, int do_post) {
   __shared__ uint64_t s_idx[kAdoptMax], s_sc[kAdoptMax], s_cur[kAdoptMax];
   __shared__ uint32_t s_n;
   __shared__ unsigned long long s_new, s_max;
@@ -133,6 +134,11 @@ __global__ __launch_bounds__(kAdoptBlock) void k_slice_adopt(const uint64_t *__r
     stats[0] = s_new;
     stats[1] = s_max;
   }
+  if (do_post) {  // the top-N post step of the adopted rows (k_top_post's work)
+    __syncthreads();  // (global cand / top_cur of this block: written above)
+    __threadfence_block();
+    top_post_block(cand, top_cur, want, post);
+  }
 }
 
 }  // namespace
@@ -146,10 +152,10 @@ hipError_t launch_slice_seg(const TopCand *cand, const uint64_t *top_cur, const 
 
 hipError_t launch_slice_adopt(const uint64_t *all, uint32_t world, uint64_t stride, uint32_t want,
                               uint64_t pool, TopCand *cand, uint64_t *top_cur, TopState *st,
-                              uint64_t *stats, hipStream_t s) {
+                              uint64_t *stats, hipStream_t s, const PostArgs *post) {
   if ((uint64_t)world * want > (uint64_t)kAdoptMax) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_slice_adopt, dim3(1), dim3(kAdoptBlock), 0, s, all, world, stride, want, pool,
-                     cand, top_cur, st, stats);
+                     cand, top_cur, st, stats, post ? *post : PostArgs{}, post ? 1 : 0);
   return hipGetLastError();
 }
 
