@@ -133,10 +133,26 @@ int plan_count(nk_counter *c, uint64_t est_bases, uint64_t slack, uint64_t max_s
     // records per tile (at 245 buckets about 10 % of the records)
     if (part_bits) cap += 4 * n_tiles_for(est, kPartTile);
   }
+  // Part with many buckets (P > 128 x 32768; not the keyed count, whose
+  // records the table reads per bucket): a sub-region per XCD in each bucket
+  // region (PartArgs::sub_shift).  At 489 buckets (P = 16 M) a tile writes a
+  // descriptor and a ~17-record segment per bucket; the descriptors of one
+  // bucket, written from all eight XCDs, cost 155 MB of K1a's 926 MB written,
+  // 62 MB with a table per XCD (the step 1.4-3 % faster, profiles/r05_o-q;
+  // NK_NO_XCD_REGIONS=1: one region per bucket)
+  uint32_t sub_shift = 0;
+  if (cp.path == CountPath::Part && !part_bits && B > kSubMinBuckets && !getenv("NK_NO_XCD_REGIONS")) {
+    sub_shift = kSubShift;
+    // records per sub-region (1/8 of the tiles each), with room for the
+    // segments' padding to whole 8-record groups (~3.5 per (tile, bucket))
+    cap = ((cap + 4 * n_tiles_for(est, kPartTile)) >> sub_shift) + 64;
+    max_segs = (max_segs >> sub_shift) + 64;
+  }
   cap = (cap + 63) & ~63ull;
   // one round of 1-per-CU workgroups (128 KiB LDS each) on 256 CUs
   cp.slices = (uint32_t)std::max<uint64_t>(1, NK_K1B_WGS / B);
-  if ((rc = c->p_off.ensure(B * cap)) || (rc = c->p_fill.ensure(B)) || (rc = c->p_over.ensure(B)) ||
+  const uint64_t V = B << sub_shift;  // (virtual) buckets: fill counters, regions
+  if ((rc = c->p_off.ensure(V * cap)) || (rc = c->p_fill.ensure(V)) || (rc = c->p_over.ensure(B)) ||
       ((cp.path == CountPath::Part || cp.slices > 1) && (rc = c->partials.ensure(cp.slices * P))))
     return rc;
   PartArgs &pa = cp.pa;
@@ -147,8 +163,9 @@ int plan_count(nk_counter *c, uint64_t est_bases, uint64_t slack, uint64_t max_s
   pa.overflow = c->p_over.p;
   pa.currents = (unsigned long long *)c->cur.p;
   pa.bin_bits = (uint32_t)pbits;
+  pa.sub_shift = sub_shift;
   if (cp.path == CountPath::Part) {
-    if ((rc = c->p_pos.ensure(B * cap)) || (rc = c->p_desc.ensure(B * max_segs))) return rc;
+    if ((rc = c->p_pos.ensure(V * cap)) || (rc = c->p_desc.ensure(V * max_segs))) return rc;
     pa.pos = c->p_pos.p;
     pa.desc = c->p_desc.p;
     pa.max_segs = max_segs;
@@ -164,7 +181,7 @@ int plan_count(nk_counter *c, uint64_t est_bases, uint64_t slack, uint64_t max_s
     cp.ga.lane_tag = (cp.path == CountPath::Wide && cp.ga.bin_bits <= kLaneTagMaxBits &&
                       !getenv("NK_NO_LANE_TAG")) ? 1u : 0u;
   }
-  z.ptr[z.n] = c->p_fill.p; z.bytes[z.n++] = B * 8;
+  z.ptr[z.n] = c->p_fill.p; z.bytes[z.n++] = V * 8;
   z.ptr[z.n] = c->p_over.p; z.bytes[z.n++] = B * 4;
   return NK_OK;
 }
@@ -208,6 +225,7 @@ hipError_t split_pipelined(nk_counter *c, const CountPlan &cp, const KmerInput &
   const uint64_t nb = cp.ga.n_buckets;
   if (c->w_snap.ensure((uint64_t)G * nb)) return hipErrorOutOfMemory;
   const uint64_t per = (in.n_tiles + G - 1) / G;
+  const bool defer = getenv("NK_GS_DEFER") != nullptr;  // A/B: every split after the last launch
   uint32_t g = 0;
   uint64_t prev_tiles = 0;
   for (uint64_t t0 = 0; t0 < in.n_tiles; t0 += per, ++g) {
@@ -218,6 +236,7 @@ hipError_t split_pipelined(nk_counter *c, const CountPlan &cp, const KmerInput &
     unsigned long long *snap = c->w_snap.p + (uint64_t)g * nb;  // after this launch
     const unsigned long long *hi = g ? snap - nb : nullptr;      // the previous launch's records
     const unsigned long long *lo = g > 1 ? snap - 2 * nb : nullptr;
+    if (defer) lo = hi = nullptr;
     if ((e = launch_gen_split(bi, (int)c->k, c->canonical, cp.km, c->pool, cp.ga, cp.pa, lo, hi,
                               prev_tiles * kPartTile * 9 / 8, s)) ||
         (e = launch_fill_snap(cp.ga, snap, s)))
@@ -225,6 +244,7 @@ hipError_t split_pipelined(nk_counter *c, const CountPlan &cp, const KmerInput &
     prev_tiles = bi.n_tiles;
   }
   const unsigned long long *last = c->w_snap.p + (uint64_t)(g - 1) * nb;
+  if (defer) return launch_split(cp.ga, cp.pa, s);
   return launch_split(cp.ga, cp.pa, s, g > 1 ? last - nb : nullptr, last, prev_tiles * kPartTile);
 }
 
@@ -251,7 +271,7 @@ hipError_t batch_count(nk_counter *c, const CountPlan &cp, const KmerInput &in, 
   if (e == hipSuccess) e = gen_hist(c, cp, false, s);
   if (e != hipSuccess) return e;
   ZeroList z{};
-  z.ptr[z.n] = cp.pa.fill; z.bytes[z.n++] = (uint64_t)cp.pa.n_buckets * 8;
+  z.ptr[z.n] = cp.pa.fill; z.bytes[z.n++] = ((uint64_t)cp.pa.n_buckets << cp.pa.sub_shift) * 8;
   if (cp.path == CountPath::Wide) {
     z.ptr[z.n] = cp.ga.fill; z.bytes[z.n++] = (uint64_t)cp.ga.n_buckets * 8;
   }

@@ -236,7 +236,9 @@ int enqueue_uniques(nk_counter *c, uint32_t m, bool rescan, bool post_done,
     u.xcap = c->xport_cap;
   }
   if (part) {
-    const uint32_t slices = std::max<uint32_t>(1, NK_U1_SLICE_BUDGET / m);
+    // (whole rounds of the bucket's sub-regions: k_uniq_scan)
+    const uint32_t sh = c->last_pa.sub_shift;
+    const uint32_t slices = ((std::max<uint32_t>(1, NK_U1_SLICE_BUDGET / m) + (1u << sh) - 1) >> sh) << sh;
     HIPCHK(launch_part_uniques(c->last_in, (int)c->k, c->canonical, c->last_pa, u, c->tbuckets.p,
                                c->post_flags.p + 2, m, slices, s));
   } else {

@@ -16,6 +16,8 @@ constexpr int kPartBlock = 512;       // threads per K1a workgroup
 constexpr int kBinBits = 15;
 constexpr int kBinsPerBucket = 1 << kBinBits;  // 32768 u32 bins = 128 KiB LDS
 constexpr int kMaxBuckets = 512;      // pool <= 16,777,216 takes the partitioned path
+constexpr uint32_t kSubShift = 3;       // K1a sub-regions per bucket: one per XCD (PartArgs::sub_shift)
+constexpr uint64_t kSubMinBuckets = 128;  // ... when the Part count has more buckets than this
 constexpr int kHistBlock = 1024;
 
 struct LifParams {
@@ -170,6 +172,12 @@ struct PartArgs {
   unsigned long long *out = nullptr;
   const uint32_t *over_coarse = nullptr;  // wide: coarse overflow flags
   uint32_t coarse_shift = 0;              // fine bucket -> coarse bucket
+  // K1a (Part path, many buckets): 2^sub_shift sub-regions per bucket, one per
+  // XCD (tile & 7: workgroup i runs on XCD i mod 8, tools/xccmap.hip), so a
+  // bucket's consecutive descriptors are written through one L2.  fill / desc
+  // / the region then index the virtual bucket v = b << sub_shift | x, each
+  // of `cap` records and `max_segs` descriptors; overflow stays per bucket.
+  uint32_t sub_shift = 0;
   K1bLif lif;                             // write-through only
 };
 

@@ -694,20 +694,24 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
     }
     if (tid == 0) s_start[B] = carry;
   }
+  const uint32_t xs = blockIdx.x & ((1u << pa.sub_shift) - 1u);  // this tile's sub-region (its XCD)
   for (uint32_t b = tid; b < B; b += kPartBlock) {
     const uint32_t c = (s_cnt[b] + 7u) & ~7u;
     uint32_t fit = 0, base = 0;
     if (c) {
-      unsigned long long ret = atomicAdd(&pa.fill[b], (unsigned long long)c | (1ull << 40));
+      const uint64_t v = ((uint64_t)b << pa.sub_shift) | xs;
+      unsigned long long ret = atomicAdd(&pa.fill[v], (unsigned long long)c | (1ull << 40));
       uint64_t eb = ret & ((1ull << 40) - 1);
       uint64_t seg = ret >> 40;
+#if !defined(NK_ABL_NODESC)  // ablation: no descriptor writes (the uniques break; traffic only)
       if (seg < pa.max_segs)
-        pa.desc[(uint64_t)b * pa.max_segs + seg] = make_uint2((uint32_t)tile, (uint32_t)eb);
+        pa.desc[v * pa.max_segs + seg] = make_uint2((uint32_t)tile, (uint32_t)eb);
+#endif
       fit = eb >= pa.cap ? 0u : (uint32_t)(pa.cap - eb < c ? pa.cap - eb : c);
       // past the region, or past the descriptor table (chunked input: a tile can
       // add a segment per launch): the uniques of this bucket fall back to a rescan
       if (fit < c || (seg >= pa.max_segs && (!KEYS || pa.desc))) pa.overflow[b] = 1u;
-      base = (uint32_t)eb;
+      base = (uint32_t)(xs * pa.cap + eb);  // from the bucket's first sub-region
     }
     s_base[b] = base;
     s_fit[b] = fit;
@@ -748,7 +752,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
     continue;
 #endif
     if (j8 < s_fit[b]) {
-      const uint64_t dst = (uint64_t)b * pa.cap + s_base[b] + j8;
+      const uint64_t dst = ((uint64_t)b << pa.sub_shift) * pa.cap + s_base[b] + j8;
       // v_perm: bytes {lo16(a), lo16(b)} and {hi16(a), hi16(b)}
       const uint4 off = make_uint4(__builtin_amdgcn_perm(w0.y, w0.x, 0x05040100u),
                                    __builtin_amdgcn_perm(w0.w, w0.z, 0x05040100u),
@@ -761,7 +765,11 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
       // nontemporal: the records are read once, by K1b, from HBM (A/B: K1a
       // 0.4177-0.4179 vs 0.4205-0.4217 ms with plain stores)
       typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      // (plain stores instead wrote as much at pool 16 M, also with the
+      // sub-regions per XCD: profiles/r05_l, r05_p)
       __builtin_nontemporal_store(u32x4{off.x, off.y, off.z, off.w}, reinterpret_cast<u32x4 *>(pa.off + dst));
+      if (!KEYS)
+        __builtin_nontemporal_store(u32x4{pos.x, pos.y, pos.z, pos.w}, reinterpret_cast<u32x4 *>(pa.pos + dst));
       if constexpr (KEYS) {
         if (pa.pos)  // the count's arena: positions kept for a multi-GPU uniques pass
           __builtin_nontemporal_store(u32x4{pos.x, pos.y, pos.z, pos.w}, reinterpret_cast<u32x4 *>(pa.pos + dst));
@@ -777,8 +785,6 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           reinterpret_cast<ulonglong2 *>(pa.key + dst)[i] = make_ulonglong2(kk[2 * i], kk[2 * i + 1]);
-      } else {
-        __builtin_nontemporal_store(u32x4{pos.x, pos.y, pos.z, pos.w}, reinterpret_cast<u32x4 *>(pa.pos + dst));
       }
     } else {  // bucket region full: count directly (correct, slow, rare)
       const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
@@ -864,55 +870,71 @@ __global__ __launch_bounds__(kHistBlock) void k_bucket_hist(PartArgs pa, uint64_
   }
   auto bin = [](uint32_t off) { return off < kBins ? off : kBins; };
   __syncthreads();
-  uint64_t n = pa.fill[b] & ((1ull << 40) - 1);
-  if (n > pa.cap) n = pa.cap;
-  const uint64_t lo = n * r / slices, hi = n * (r + 1) / slices;
-  const uint16_t *src = pa.off + (uint64_t)b * pa.cap;
-  // 8 records (16 B) per lane per step where aligned
-  uint64_t i = lo;
-  for (; i < hi && (i & 7); ++i)
-    if (threadIdx.x == 0) atomicAdd(&h[bin(src[i])], 1u);
-  const uint64_t hi8 = i + ((hi - i) & ~7ull);
-  const uint64_t step = 8ull * kHistBlock;
-  // NK_HIST_KU 16-B loads per lane per round, software-pipelined: the next
-  // round's loads are in flight while this round's 8*KU LDS atomics issue.
-  // Loads past hi8 are clamped to a valid address (static wait counts) and
-  // their records skipped, so there is no serial tail of single loads.
-  auto hist8 = [&](const uint4 &v) {
-    atomicAdd(&h[bin(v.x & 0xFFFFu)], 1u); atomicAdd(&h[bin(v.x >> 16)], 1u);
-    atomicAdd(&h[bin(v.y & 0xFFFFu)], 1u); atomicAdd(&h[bin(v.y >> 16)], 1u);
-    atomicAdd(&h[bin(v.z & 0xFFFFu)], 1u); atomicAdd(&h[bin(v.z >> 16)], 1u);
-    atomicAdd(&h[bin(v.w & 0xFFFFu)], 1u); atomicAdd(&h[bin(v.w >> 16)], 1u);
-  };
-  uint64_t j = i + 8ull * threadIdx.x;
-  if (j < hi8) {
-    auto load_round = [&](uint64_t jb, uint4 *v) {
-#pragma unroll
-      for (int t = 0; t < KU; ++t) {
-        const uint64_t jt = jb + (uint64_t)t * step;
-        // nontemporal: each record is read once (A/B: step 0.561 vs 0.575-0.578 ms)
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src + (jt < hi8 ? jt : i)));
-        v[t] = make_uint4(q.x, q.y, q.z, q.w);
-      }
-    };
-    uint4 cur[KU];
-    load_round(j, cur);
-    for (;;) {
-      const uint64_t jn = j + (uint64_t)KU * step;
-      const bool more = jn < hi8;
-      uint4 nxt[KU];
-      load_round(more ? jn : j, nxt);
-#pragma unroll
-      for (int t = 0; t < KU; ++t)
-        if (j + (uint64_t)t * step < hi8) hist8(cur[t]);
-      if (!more) break;
-      j = jn;
-#pragma unroll
-      for (int t = 0; t < KU; ++t) cur[t] = nxt[t];
-    }
+  // the bucket's records: its sub-regions' (pa.sub_shift) in order, this
+  // slice's share [lo, hi) of them
+  const uint32_t nsub = 1u << pa.sub_shift;
+  uint64_t n = 0;
+  for (uint32_t x = 0; x < nsub; ++x) {
+    const uint64_t f = pa.fill[((uint64_t)b << pa.sub_shift) | x] & ((1ull << 40) - 1);
+    n += f < pa.cap ? f : pa.cap;
   }
-  for (uint64_t j = hi8 + threadIdx.x; j < hi; j += kHistBlock) atomicAdd(&h[bin(src[j])], 1u);
+  const uint64_t lo_all = n * r / slices, hi_all = n * (r + 1) / slices;
+  uint64_t c0 = 0;
+  for (uint32_t x = 0; x < nsub; ++x) {
+    const uint64_t vb = ((uint64_t)b << pa.sub_shift) | x;
+    uint64_t nv = pa.fill[vb] & ((1ull << 40) - 1);
+    if (nv > pa.cap) nv = pa.cap;
+    const uint64_t a = lo_all > c0 ? lo_all : c0, z = hi_all < c0 + nv ? hi_all : c0 + nv;
+    const uint64_t lo = a - c0, hi = z > a ? z - c0 : lo;  // (uniform) this sub-region's part
+    c0 += nv;
+    if (lo >= hi) continue;
+    const uint16_t *src = pa.off + vb * pa.cap;
+    // 8 records (16 B) per lane per step where aligned
+    uint64_t i = lo;
+    for (; i < hi && (i & 7); ++i)
+      if (threadIdx.x == 0) atomicAdd(&h[bin(src[i])], 1u);
+    const uint64_t hi8 = i + ((hi - i) & ~7ull);
+    const uint64_t step = 8ull * kHistBlock;
+    // NK_HIST_KU 16-B loads per lane per round, software-pipelined: the next
+    // round's loads are in flight while this round's 8*KU LDS atomics issue.
+    // Loads past hi8 are clamped to a valid address (static wait counts) and
+    // their records skipped, so there is no serial tail of single loads.
+    auto hist8 = [&](const uint4 &v) {
+      atomicAdd(&h[bin(v.x & 0xFFFFu)], 1u); atomicAdd(&h[bin(v.x >> 16)], 1u);
+      atomicAdd(&h[bin(v.y & 0xFFFFu)], 1u); atomicAdd(&h[bin(v.y >> 16)], 1u);
+      atomicAdd(&h[bin(v.z & 0xFFFFu)], 1u); atomicAdd(&h[bin(v.z >> 16)], 1u);
+      atomicAdd(&h[bin(v.w & 0xFFFFu)], 1u); atomicAdd(&h[bin(v.w >> 16)], 1u);
+    };
+    uint64_t j = i + 8ull * threadIdx.x;
+    if (j < hi8) {
+      auto load_round = [&](uint64_t jb, uint4 *v) {
+#pragma unroll
+        for (int t = 0; t < KU; ++t) {
+          const uint64_t jt = jb + (uint64_t)t * step;
+          // nontemporal: each record is read once (A/B: step 0.561 vs 0.575-0.578 ms)
+          typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+          const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src + (jt < hi8 ? jt : i)));
+          v[t] = make_uint4(q.x, q.y, q.z, q.w);
+        }
+      };
+      uint4 cur[KU];
+      load_round(j, cur);
+      for (;;) {
+        const uint64_t jn = j + (uint64_t)KU * step;
+        const bool more = jn < hi8;
+        uint4 nxt[KU];
+        load_round(more ? jn : j, nxt);
+#pragma unroll
+        for (int t = 0; t < KU; ++t)
+          if (j + (uint64_t)t * step < hi8) hist8(cur[t]);
+        if (!more) break;
+        j = jn;
+#pragma unroll
+        for (int t = 0; t < KU; ++t) cur[t] = nxt[t];
+      }
+    }
+    for (uint64_t j = hi8 + threadIdx.x; j < hi; j += kHistBlock) atomicAdd(&h[bin(src[j])], 1u);
+  }  // sub-regions
   __syncthreads();
   const uint64_t nb0 = (uint64_t)b << BB;
   const uint64_t nbins = pool - nb0 < (uint64_t)kBins ? pool - nb0 : kBins;
@@ -1085,7 +1107,7 @@ constexpr int kScanBuf = 4096;
 
 // A scan hit {bucket | top row | record index} as k_uniq_hits takes it:
 // top row << 48 | base position of the k-mer (segment a holds the record).
-__device__ __forceinline__ unsigned long long hit_at(const PartArgs &pa, uint32_t b, uint64_t a,
+__device__ __forceinline__ unsigned long long hit_at(const PartArgs &pa, uint64_t b, uint64_t a,
                                                      unsigned long long e) {
   const uint64_t i = e & ((1ull << 38) - 1);
   const uint64_t slot = (e >> 38) & 0x3FFu;
@@ -1096,7 +1118,7 @@ __device__ __forceinline__ unsigned long long hit_at(const PartArgs &pa, uint32_
 
 // Same, the segment found by a binary search of descriptors [a, z) in global
 // memory (d[a].y <= the record index).
-__device__ unsigned long long resolve_hit(const PartArgs &pa, uint32_t b, uint64_t a, uint64_t z,
+__device__ unsigned long long resolve_hit(const PartArgs &pa, uint64_t b, uint64_t a, uint64_t z,
                                           unsigned long long e) {
   const uint64_t i = e & ((1ull << 38) - 1);
   const uint2 *d = pa.desc + (uint64_t)b * pa.max_segs;
@@ -1138,13 +1160,18 @@ __global__ __launch_bounds__(kHistBlock) void k_uniq_scan(KmerInput in, int k, P
     }
   }
   __syncthreads();
-  uint64_t n = pa.fill[b] & ((1ull << 40) - 1);
+  // sub-regions (pa.sub_shift): slice r scans sub-region r mod 2^sub_shift,
+  // its share r >> sub_shift of (slices >> sub_shift); vb indexes the region,
+  // the fill and the descriptors (the host passes a multiple of 2^sub_shift)
+  const uint64_t vb = ((uint64_t)b << pa.sub_shift) | (r & ((1u << pa.sub_shift) - 1u));
+  const uint32_t rs = r >> pa.sub_shift, ns_sl = slices >> pa.sub_shift;
+  uint64_t n = pa.fill[vb] & ((1ull << 40) - 1);
   if (n > pa.cap) n = pa.cap;
-  const uint64_t lo = n * r / slices, hi = n * (r + 1) / slices;
-  uint64_t n_seg = pa.fill[b] >> 40;
+  const uint64_t lo = n * rs / ns_sl, hi = n * (rs + 1) / ns_sl;
+  uint64_t n_seg = pa.fill[vb] >> 40;
   if (n_seg > pa.max_segs) n_seg = pa.max_segs;
   const uint32_t tn = t_n;
-  const uint16_t *src = pa.off + (uint64_t)b * pa.cap;
+  const uint16_t *src = pa.off + vb * pa.cap;
   // a hit's key into the set: recomputed from the bases at its position
   auto insert_hit = [&](unsigned long long h) {
     const uint32_t slot = (uint32_t)(h >> 48);
@@ -1161,7 +1188,7 @@ __global__ __launch_bounds__(kHistBlock) void k_uniq_scan(KmerInput in, int k, P
                                  ((unsigned long long)slot << 38) | i;
     const uint32_t at = atomicAdd(&s_nh, 1u);
     if (at < kScanBuf) buf[at] = e;
-    else insert_hit(resolve_hit(pa, b, 0, n_seg, e));  // LDS list full (very hit-dense slice)
+    else insert_hit(resolve_hit(pa, vb, 0, n_seg, e));  // LDS list full (very hit-dense slice)
   };
   // 8 records per 16-B load, eight loads in flight per lane (the slice is a
   // few dozen loads per lane: latency, not bandwidth, bounds a shallow loop);
@@ -1208,7 +1235,7 @@ __global__ __launch_bounds__(kHistBlock) void k_uniq_scan(KmerInput in, int k, P
   // searches, have their first-record indices staged in LDS (the bitmap is
   // done with), so each hit costs an LDS search plus two parallel loads
   // instead of a chain of ~log2(segments) dependent global loads
-  const uint2 *d = pa.desc + (uint64_t)b * pa.max_segs;
+  const uint2 *d = pa.desc + vb * pa.max_segs;
   if (threadIdx.x < 128) {
     const uint64_t x = threadIdx.x < 64 ? lo : hi - 1;
     const uint64_t a = wave_search_le(d, n_seg, x);
@@ -1232,9 +1259,9 @@ __global__ __launch_bounds__(kHistBlock) void k_uniq_scan(KmerInput in, int k, P
         if (tab[m] <= i) a = m;
         else z = m;
       }
-      out = hit_at(pa, b, s0 + a, e);
+      out = hit_at(pa, vb, s0 + a, e);
     } else {
-      out = resolve_hit(pa, b, s0, s0 + ns, e);
+      out = resolve_hit(pa, vb, s0, s0 + ns, e);
     }
     insert_hit(out);
   }

@@ -156,10 +156,10 @@ __device__ __forceinline__ void sort_and_store(const uint32_t (&E)[PER], const u
 // keys as window_key128<CANON> (nk_tile.h); every position is hashed, the
 // ones that start no k-mer go to the no-record bucket nb.
 // SH >= 0: 128 - 2k at compile time (k = 63: SH = 2; -1: k at run time).
-template <int SH>
+template <int SH, bool SMALL>
 __device__ __forceinline__ void gen_rolled128(const TileLds<kPartTile, false> &L, const KmerInput &in,
                                               uint64_t T0, int q0, int k, const FastMod &fm,
-                                              bool small_pool, uint32_t nb, int bb, uint32_t omask,
+                                              uint32_t nb, int bb, uint32_t omask,
                                               uint32_t ltag, uint32_t *s_cnt, uint32_t (&E)[kPer],
                                               uint32_t (&O)[kPer]) {
   const int w = q0 >> 4;  // q0 is 16-aligned
@@ -205,9 +205,13 @@ __device__ __forceinline__ void gen_rolled128(const TileLds<kPartTile, false> &L
     rev.hi = (((uint64_t)Y[3] << 32) | Y[2]) & hmask;
     const Key128 key = key128_less(rev, fwd) ? rev : fwd;
     const uint64_t h = sip13_u128(key.lo, key.hi);
-    const uint32_t idx = small_pool ? fastmod32(h, fm) : (uint32_t)fastmod(h, fm);
+    const uint32_t idx = SMALL ? fastmod32(h, fm) : (uint32_t)fastmod(h, fm);
     const uint32_t b = ((ok >> j) & 1u) ? (idx >> bb) : nb;
+#if defined(NK_ABL_G_NORANK)  // ablation: no LDS rank atomic
+    E[j] = (b << 16) | j;
+#else
     E[j] = (b << 16) | atomicAdd(&s_cnt[b], 1u);
+#endif
     O[j] = (idx & omask) | ltag;
   }
 }
@@ -244,16 +248,35 @@ __device__ __forceinline__ void gen_tile(const KmerInput &in, int k, const FastM
   const uint32_t omask = (uint32_t)((1ull << bb) - 1ull);
   const uint32_t ltag = (WIDE && ga.lane_tag) ? ((uint32_t)tid << bb) : 0u;  // (GenPartArgs::lane_tag)
   for (uint32_t b = tid; b <= nb; b += kPartBlock) sm.s_cnt[b] = 0;
+#if defined(NK_ABL_G_NOSTAGE)  // ablation: the tile's LDS not loaded
+  __syncthreads();
+#else
   stage_tile<kPartTile, kPartBlock, kRaw>(L, in, tile, k);  // syncs
+#endif
 
   const int q0 = tid * kPer;
   uint32_t E[kPer], O[kPer];
   if constexpr (KM == 2 && CANON) {
     if (k > 48) {  // (uniform) the lane's 16 windows rolled from registers
-      if (k == 63)  // config 5
-        gen_rolled128<2>(L, in, T0, q0, k, fm, small_pool, nb, bb, omask, ltag, sm.s_cnt, E, O);
+      // (the pool's modulo a template argument too: a uniform branch per
+      // window between the two forms cost K1g 1.3 %, profiles/r05_m)
+      if (k == 63 && small_pool)  // config 5
+        gen_rolled128<2, true>(L, in, T0, q0, k, fm, nb, bb, omask, ltag, sm.s_cnt, E, O);
+      else if (k == 63)
+        gen_rolled128<2, false>(L, in, T0, q0, k, fm, nb, bb, omask, ltag, sm.s_cnt, E, O);
+      else if (small_pool)
+        gen_rolled128<-1, true>(L, in, T0, q0, k, fm, nb, bb, omask, ltag, sm.s_cnt, E, O);
       else
-        gen_rolled128<-1>(L, in, T0, q0, k, fm, small_pool, nb, bb, omask, ltag, sm.s_cnt, E, O);
+        gen_rolled128<-1, false>(L, in, T0, q0, k, fm, nb, bb, omask, ltag, sm.s_cnt, E, O);
+#if defined(NK_ABL_G_NOSORT)  // ablation: the records folded into one store per lane
+      {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) acc ^= E[j] + O[j];
+        reinterpret_cast<uint32_t *>(ga.rec)[bi * kPartBlock + tid] = acc;
+        return;
+      }
+#endif
       sort_and_store<WIDE, kPer>(E, O, nb, sm.s_cnt, sm.s_start, sm.s_base, sm.s_fit, sm.s_rec,
                                  sm.s_gmap, ga.fill, ga.overflow, ga.cap,
                                  reinterpret_cast<typename S::Rec *>(ga.rec), 0, bb, ga.currents, ga.desc,
@@ -397,6 +420,8 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(CANO
     GenLds<true, !CANON> g;
     SplitLds s;
   } sm;
+  // (Measured and not kept: workgroups that either hash a tile or split an
+  // item, interleaved in one grid -- the count 79.3 vs 67.8 ms, profiles/r05_n.)
   if (blockIdx.x < in.n_tiles) gen_tile<KM, CANON, true>(in, k, fm, ga, blockIdx.x, sm.g);
   if (snap_hi) {
     __syncthreads();  // (the gen tile's last stores still read its LDS)
