@@ -421,7 +421,9 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(CANO
     SplitLds s;
   } sm;
   // (Measured and not kept: workgroups that either hash a tile or split an
-  // item, interleaved in one grid -- the count 79.3 vs 67.8 ms, profiles/r05_n.)
+  // item, interleaved in one grid -- the count 79.3 vs 67.8 ms, profiles/r05_n;
+  // the first 256 / 512 / 768 workgroups splitting every item of the launch
+  // and the rest hashing -- the step equal / +3 % / +8 %, profiles/r05_s.)
   if (blockIdx.x < in.n_tiles) gen_tile<KM, CANON, true>(in, k, fm, ga, blockIdx.x, sm.g);
   if (snap_hi) {
     __syncthreads();  // (the gen tile's last stores still read its LDS)
