@@ -796,6 +796,13 @@ def extras(args, ctr, bases, offsets, nk, d_bases, d_offs, s_handle, dev_idx, Co
                                     "distinct_kmers": x.distinct_kmers(),
                                     "same_results": x.top_abundant_neurons(20) == ctr.top_abundant_neurons(20)}
         x.close()
+        # what the exact table's keys would cost recomputed from the kept
+        # records' positions instead of written by K1a<KEYS>
+        log("key gather diagnostic")
+        g_ms, _ = ctr.diag_key_gather(reps=5)
+        out["key_gather"] = {"ms_best": round(g_ms, 4), "keys": nk,
+                             "note": "every kept record's key recomputed from (tile, position) and "
+                                     "the resident bases (nk_diag_key_gather_ms), no table built"}
     if not args.no_cpu_baseline:
         log("cpu_baseline: oracle process_parallel on the whole input")
         ref, dt, threads = cpu_baseline(bases, offsets, k, pool)

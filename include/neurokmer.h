@@ -425,6 +425,14 @@ int nk_diag_hash_ms(int device, uint64_t n_keys, uint64_t pool, int reps, float 
 /* The same for width 128: SipHash-1-3 over 16-byte keys (NK_KMER_128, the
  * config-5 count kernel's hash), or 64.  (No reference counterpart.) */
 int nk_diag_hash_ms_w(int device, uint64_t n_keys, uint64_t pool, int width, int reps, float *ms);
+/* Diagnostic: the best of `reps` device times (ms) of a kernel that recomputes
+ * the key of every record the handle's last count kept (the partitioned count,
+ * k <= 32, one batch, no exact table) from its position in the input -- the
+ * tile from the segment descriptors, the k bases from the resident input --
+ * and XOR-folds the keys into *checksum (may be NULL): what an exact-table pass
+ * that reads positions instead of K1a-written keys would pay for its keys.
+ * Synchronises the device.  (No reference counterpart: measurement only.) */
+int nk_diag_key_gather_ms(nk_counter *c, int reps, float *ms, uint64_t *checksum);
 
 /* ---- associative memory (src/associative.rs) -------------
  * WillshawNetwork — :12-62.  Binary weights of pattern_size^2 bits on the

@@ -314,6 +314,14 @@ class SpikingKmerCounter:
         m = self._L.nk_count_history(self._h, buf, n)
         return [float(buf[i]) for i in range(m)]
 
+    def diag_key_gather(self, reps: int = 5) -> tuple:
+        """(best ms, XOR of the keys) of recomputing the key of every record
+        the last count kept from its input position (nk_diag_key_gather_ms):
+        the key cost of an exact table built from positions, measured."""
+        ms, cs = C.c_float(0.0), C.c_uint64(0)
+        _lib.check(self._L.nk_diag_key_gather_ms(self._h, reps, C.byref(ms), C.byref(cs)))
+        return float(ms.value), int(cs.value)
+
     def count_spans(self, n: int) -> list:
         """K1a (partitioned count kernel) duration in ms of each of the last
         min(n, 256) calls that ran it, oldest first, from in-kernel

@@ -523,6 +523,45 @@ int nk_diag_hash_ms_w(int device, uint64_t n_keys, uint64_t pool, int width, int
   return rc;
 }
 
+int nk_diag_key_gather_ms(nk_counter *c, int reps, float *ms, uint64_t *checksum) {
+  if (!c || !ms || reps < 1) return fail(NK_E_INVALID, "nk_diag_key_gather_ms: counter, reps >= 1, ms");
+  if (!c->part_used || !c->have_input || !c->last_pa.desc || !c->last_pa.pos || c->last_pa.key ||
+      c->k > 32 || c->w128)
+    return fail(NK_E_INVALID, "nk_diag_key_gather_ms: the last count kept no Part records (k <= 32, one batch)");
+  (void)hipSetDevice(c->device);
+  if (hipDeviceSynchronize() != hipSuccess) return fail(NK_E_DEVICE, "device synchronisation failed");
+  unsigned long long *sink = nullptr;
+  hipStream_t s = nullptr;
+  hipEvent_t a = nullptr, b = nullptr;
+  int rc = NK_OK;
+  float best = 1e30f;
+  unsigned long long sum = 0;
+  if (hipMalloc(&sink, 8) != hipSuccess) return fail(NK_E_OOM, "hipMalloc");
+  if (hipStreamCreate(&s) != hipSuccess || hipEventCreate(&a) != hipSuccess ||
+      hipEventCreate(&b) != hipSuccess)
+    rc = fail(NK_E_DEVICE, "stream/event creation failed");
+  for (int i = 0; rc == NK_OK && i < reps + 1; ++i) {  // + 1 untimed warm-up
+    float t = 0.0f;
+    if (hipMemsetAsync(sink, 0, 8, s) != hipSuccess || hipEventRecord(a, s) != hipSuccess ||
+        launch_diag_key_gather(c->last_in, (int)c->k, c->canonical, c->last_pa, sink, s) != hipSuccess ||
+        hipEventRecord(b, s) != hipSuccess || hipEventSynchronize(b) != hipSuccess ||
+        hipEventElapsedTime(&t, a, b) != hipSuccess ||
+        hipMemcpy(&sum, sink, 8, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = fail(NK_E_DEVICE, "diag key gather kernel failed");
+    else if (i > 0 && t < best)
+      best = t;
+  }
+  if (a) (void)hipEventDestroy(a);
+  if (b) (void)hipEventDestroy(b);
+  if (s) (void)hipStreamDestroy(s);
+  (void)hipFree(sink);
+  if (rc == NK_OK) {
+    *ms = best;
+    if (checksum) *checksum = sum;
+  }
+  return rc;
+}
+
 int nk_set_stage_timing(nk_counter *c, uint32_t level) {
   if (!c) return fail(NK_E_INVALID, "null counter");
   if (level > 3) return fail(NK_E_INVALID, "stage timing level must be 0, 1, 2 or 3");

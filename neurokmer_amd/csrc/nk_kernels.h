@@ -394,6 +394,10 @@ hipError_t launch_bucket_hist(const PartArgs &pa, uint64_t pool, uint32_t slices
                               uint32_t *partials, hipStream_t s);
 hipError_t launch_partials_add(const uint32_t *partials, uint32_t slices, uint64_t pool,
                                uint64_t *currents, hipStream_t s);
+// diagnostic: every kept Part record's key recomputed from its position,
+// XOR-folded into *sink (nk_diag_key_gather_ms)
+hipError_t launch_diag_key_gather(const KmerInput &in, int k, int canonical, const PartArgs &pa,
+                                  unsigned long long *sink, hipStream_t s);
 // (also empties the uniques hash set u.set_keys[0 .. *u.set_mask])
 hipError_t launch_part_uniques(const KmerInput &in, int k, int canonical, const PartArgs &pa,
                                const UniqArgs &u, const uint32_t *tbuckets, const uint32_t *n_tb,

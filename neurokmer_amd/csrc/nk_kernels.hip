@@ -2580,6 +2580,77 @@ hipError_t launch_partials_add(const uint32_t *partials, uint32_t slices, uint64
   return hipGetLastError();
 }
 
+// Diagnostic (measure, do not estimate): the cost of
+// recomputing every kept record's key from its position, as an exact-table
+// pass without K1a<KEYS>'s 8-B key per record would have to.  One workgroup
+// per (slice, virtual bucket): each thread takes 8-record groups, finds the
+// group's segment (tile) in an LDS copy of the slice's descriptors, loads the
+// 8 positions and recomputes the keys from the bases (vec_window_key, as the
+// uniques scan does for its hits); the keys are XOR-folded into *sink.
+constexpr int kGatherTab = 4096;
+template <bool CANON>
+__global__ __launch_bounds__(256) void k_diag_key_gather(KmerInput in, int k, PartArgs pa,
+                                                         uint32_t slices,
+                                                         unsigned long long *__restrict__ sink) {
+  __shared__ uint32_t tab[kGatherTab];
+  __shared__ uint64_t s_seg[2];
+  const uint64_t v = blockIdx.y, r = blockIdx.x;
+  uint64_t n = pa.fill[v] & ((1ull << 40) - 1);
+  if (n > pa.cap) n = pa.cap;
+  uint64_t n_seg = pa.fill[v] >> 40;
+  if (n_seg > pa.max_segs) n_seg = pa.max_segs;
+  const uint64_t lo = (n * r / slices) & ~7ull;
+  const uint64_t hi = r + 1 == slices ? n : (n * (r + 1) / slices) & ~7ull;
+  if (lo >= hi || !n_seg) return;
+  const uint2 *d = pa.desc + v * pa.max_segs;
+  if (threadIdx.x < 128) {
+    const uint64_t a = wave_search_le(d, n_seg, threadIdx.x < 64 ? lo : hi - 1);
+    if ((threadIdx.x & 63) == 0) s_seg[threadIdx.x >> 6] = a;
+  }
+  __syncthreads();
+  const uint64_t s0 = s_seg[0], ns = s_seg[1] - s0 + 1;
+  const bool staged = ns <= (uint64_t)kGatherTab;
+  if (staged)
+    for (uint32_t j = threadIdx.x; j < ns; j += blockDim.x) tab[j] = d[s0 + j].y;
+  __syncthreads();
+  const uint16_t *off = pa.off + v * pa.cap, *pos = pa.pos + v * pa.cap;
+  unsigned long long acc = 0;
+  for (uint64_t g = lo / 8 + threadIdx.x; g < hi / 8; g += blockDim.x) {
+    const uint64_t i = g * 8;
+    uint64_t a = 0, z = ns;  // last segment whose first record <= i
+    while (z - a > 1) {
+      const uint64_t m = (a + z) >> 1;
+      if ((staged ? (uint64_t)tab[m] : (uint64_t)d[s0 + m].y) <= i) a = m;
+      else z = m;
+    }
+    const uint64_t t0 = (uint64_t)d[s0 + a].x * kPartTile;
+    const uint4 o = *reinterpret_cast<const uint4 *>(off + i);
+    const uint4 q = *reinterpret_cast<const uint4 *>(pos + i);
+    const uint32_t ow[4] = {o.x, o.y, o.z, o.w}, qw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (((ow[j >> 1] >> (16 * (j & 1))) & 0xFFFFu) == kPadOff) continue;
+      const uint64_t p = t0 + ((qw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
+      acc ^= vec_window_key<CANON>(in.bases, in.n_bases, p, k);
+    }
+  }
+  for (int o = 32; o; o >>= 1) acc ^= __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0 && acc) atomicXor(sink, acc);
+}
+
+hipError_t launch_diag_key_gather(const KmerInput &in, int k, int canonical, const PartArgs &pa,
+                                  unsigned long long *sink, hipStream_t s) {
+  if (!pa.desc || !pa.pos || k > 32) return hipErrorInvalidValue;
+  const uint64_t V = (uint64_t)pa.n_buckets << pa.sub_shift;
+  const uint32_t slices = (uint32_t)std::max<uint64_t>(1, 4096 / V);
+  const dim3 g(slices, (unsigned)V);
+  if (canonical)
+    hipLaunchKernelGGL(k_diag_key_gather<true>, g, dim3(256), 0, s, in, k, pa, slices, sink);
+  else
+    hipLaunchKernelGGL(k_diag_key_gather<false>, g, dim3(256), 0, s, in, k, pa, slices, sink);
+  return hipGetLastError();
+}
+
 // the set must be empty (kEmpty) up to *u.set_mask: the caller clears it
 hipError_t launch_part_uniques(const KmerInput &in, int k, int canonical, const PartArgs &pa,
                                const UniqArgs &u, const uint32_t *tbuckets, const uint32_t *n_tb,
