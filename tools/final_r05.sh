@@ -8,7 +8,7 @@ R=$(pwd)
 OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 if [ "${NK_FINAL_SKIP_PYTEST:-0}" != 1 ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread \
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread \
     > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
   tail -2 "$OUT/pytest_gpu.log"
 fi
