@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5, session l: K1a record stores nontemporal vs plain at pool 16M
 # (489 buckets: short segments per tile), kernel trace + WRITE_SIZE each;
-# then the end-of-round measurements (tools/final_r05.sh, no pytest)
+# then the end-of-round measurements (tools/sessions/final_r05.sh, no pytest)
 set -u
 R=$(pwd)
 OUT=$R/gpurun_out/${1:-r05_l}; mkdir -p $OUT
@@ -16,4 +16,4 @@ for mode in nt plain; do
     > "$OUT/pmc_$mode.log" 2>&1) || { tail "$OUT/pmc_$mode.log"; exit 1; }
   python3 tools/pmc_summary.py "$OUT/pmc_$mode" "$OUT/pmc_$mode" > /dev/null 2>&1 || true
 done
-NK_FINAL_SKIP_PYTEST=1 bash tools/final_r05.sh r05_final
+NK_FINAL_SKIP_PYTEST=1 bash tools/sessions/final_r05.sh r05_final

@@ -2,7 +2,7 @@
 # Side lines of bench.py at their real per-GPU sizes (configs 3-5), each
 # preceded by its PMC passes (one counter set per rocprofv3 run) so that the
 # line picks up the measured HBM traffic of its count phase.
-#   bash tools/session_side.sh <tag> config5 config4 config3
+#   bash tools/sessions/session_side.sh <tag> config5 config4 config3
 set -u
 TAG=${1:-side}
 shift

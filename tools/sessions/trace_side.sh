@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 kernel trace + stats of a short side-line run (no parity legs):
-#   bash tools/trace_side.sh <tag> config4|config5 [extra bench args]
+#   bash tools/sessions/trace_side.sh <tag> config4|config5 [extra bench args]
 set -u
 TAG=$1; W=$2; shift 2
 R=$(pwd)
