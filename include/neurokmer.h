@@ -431,7 +431,9 @@ int nk_diag_hash_ms_w(int device, uint64_t n_keys, uint64_t pool, int width, int
  * tile from the segment descriptors, the k bases from the resident input --
  * and XOR-folds the keys into *checksum (may be NULL): what an exact-table pass
  * that reads positions instead of K1a-written keys would pay for its keys.
- * Synchronises the device.  (No reference counterpart: measurement only.) */
+ * (The checksum covers the kept records: the excess of an overflowed region,
+ * counted directly, is not among them.)  Synchronises the device.  (No
+ * reference counterpart: measurement only.) */
 int nk_diag_key_gather_ms(nk_counter *c, int reps, float *ms, uint64_t *checksum);
 
 /* ---- associative memory (src/associative.rs) -------------
