@@ -798,11 +798,12 @@ def extras(args, ctr, bases, offsets, nk, d_bases, d_offs, s_handle, dev_idx, Co
         x.close()
         # what the exact table's keys would cost recomputed from the kept
         # records' positions instead of written by K1a<KEYS>
-        log("key gather diagnostic")
-        g_ms, _ = ctr.diag_key_gather(reps=5)
-        out["key_gather"] = {"ms_best": round(g_ms, 4), "keys": nk,
-                             "note": "every kept record's key recomputed from (tile, position) and "
-                                     "the resident bases (nk_diag_key_gather_ms), no table built"}
+        if k <= 32 and args.kmer_width == 64:  # (the partitioned count's kept records)
+            log("key gather diagnostic")
+            g_ms, _ = ctr.diag_key_gather(reps=5)
+            out["key_gather"] = {"ms_best": round(g_ms, 4), "keys": nk,
+                                 "note": "every kept record's key recomputed from (tile, position) "
+                                         "and the resident bases (nk_diag_key_gather_ms), no table built"}
     if not args.no_cpu_baseline:
         log("cpu_baseline: oracle process_parallel on the whole input")
         ref, dt, threads = cpu_baseline(bases, offsets, k, pool)

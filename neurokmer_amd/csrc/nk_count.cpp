@@ -322,7 +322,7 @@ int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_offs,
   uint64_t est = std::min<uint64_t>(n_bases, chunk);
   // the exact table grouped by neuron from this count's own records (K1a also
   // writes each record's key, nk_table.hip), in 4096-neuron buckets
-  const bool want_keyed = c->opts.exact_counts && grouped_ok(c, n_bases);
+  const bool want_keyed = c->opts.exact_counts && c->k <= 32 && grouped_ok(c, n_bases);
   int rc = plan_count(c, est, kPartTile, n_tiles_for(est, kPartTile), cp, z,
                      /*keep_gen=*/n_bases <= chunk, want_keyed ? xbin_bits() : 0);
   if (rc == NK_E_OOM && chunk > count_chunk()) {

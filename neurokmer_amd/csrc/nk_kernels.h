@@ -206,6 +206,13 @@ struct GenPartArgs {
   uint32_t lane_tag = 0;
 };
 constexpr int kLaneTagMaxBits = 22;  // + 9 lane bits < 32: never the pad (all ones)
+// K1g<KEYS> (k_part_gen_keys): where each kept record's u64 key goes
+struct GenKeyArgs {
+  uint64_t *key;                  // [bucket][cap], beside the u16 records
+  uint64_t *spill;                // keys of records past a full region
+  unsigned long long *n_spill;
+  uint64_t spill_cap;
+};
 constexpr int kLaneWords = 16;       // 512 lanes of a k_part_gen tile, one bit each
 
 // keys handed to the uniques merge: a flat list (world == 0) or the
@@ -351,6 +358,10 @@ hipError_t launch_part(const KmerInput &in, int k, int canonical, uint64_t pool,
 // key mode km: 0 k <= 32 u64, 1 k > 32 compat, 2 --kmer-width=128
 hipError_t launch_part_gen(const KmerInput &in, int k, int canonical, int km, uint64_t pool,
                            const GenPartArgs &ga, int wide, hipStream_t s);
+// the same narrow partition (km 0/1, buckets of 2^12..2^15 neurons) also
+// writing each kept record's key (the grouped exact table for k > 32)
+hipError_t launch_part_gen_keys(const KmerInput &in, int k, int canonical, int km, uint64_t pool,
+                                const GenPartArgs &ga, const GenKeyArgs &ka, hipStream_t s);
 // uniques rescan over kPartTile tiles for the Gen/Wide count paths; with a
 // tile list (tiles, *n_list <= max_list) only those tiles
 // the windows of the listed (tile << 9 | lane) entries of lane-tagged records

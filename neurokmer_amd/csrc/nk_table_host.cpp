@@ -159,7 +159,8 @@ uint32_t xbin_bits() {
 // for a group's distinct keys to fit the LDS table.  NK_EXACT_SORT=1 (tests,
 // A/B) takes the sorted build.
 bool grouped_ok(const nk_counter *c, uint64_t n_bases) {
-  if (c->w128 || c->k > 32 || !c->pool || !n_bases) return false;
+  // (k > 32: NK_KMER_COMPAT u64 keys, the table's own K1g<KEYS> pass)
+  if (c->w128 || c->k > 64 || !c->pool || !n_bases) return false;
   const char *e = getenv("NK_EXACT_SORT");
   if (e && atoi(e)) return false;
   if (((c->pool + kBinsPerBucket - 1) >> kBinBits) > (uint64_t)kMaxBuckets) return false;
@@ -223,7 +224,20 @@ int build_grouped(nk_counter *c, const KmerInput &in0, const PartArgs *keyed, hi
     HIPCHK(hipMemsetAsync(c->xg_fill.p, 0, B * 8, s));
     HIPCHK(hipMemsetAsync(c->xg_over.p, 0, B * 4, s));
     HIPCHK(launch_tile_rec(in, kPartTile, c->xg_trec.p, s));
-    HIPCHK(launch_part(in, (int)c->k, c->canonical, P, pa, s));
+    if (c->k > 32) {  // NK_KMER_COMPAT u64 keys: K1g<KEYS> (k_part counts k <= 32 only)
+      GenPartArgs ga{};
+      ga.n_buckets = pa.n_buckets;
+      ga.bin_bits = (int)pa.bin_bits;
+      ga.cap = pa.cap;
+      ga.rec = pa.off;
+      ga.fill = pa.fill;
+      ga.overflow = pa.overflow;
+      ga.currents = nullptr;
+      const GenKeyArgs ka{pa.key, pa.spill, pa.n_spill, pa.spill_cap};
+      HIPCHK(launch_part_gen_keys(in, (int)c->k, c->canonical, 1, P, ga, ka, s));
+    } else {
+      HIPCHK(launch_part(in, (int)c->k, c->canonical, P, pa, s));
+    }
   }
   XGroupArgs t{};
   t.n_buckets = pa.n_buckets;
@@ -268,7 +282,7 @@ int build_grouped(nk_counter *c, const KmerInput &in0, const PartArgs *keyed, hi
   HIPCHK(hipStreamSynchronize(s));
   if (cnt[1] > t.side_cap) return build_sorted(c, in0, s);
   if (cnt[1]) {  // the side part: sorted, run-length encoded after the grouped span
-    const int end_bit = (int)(2 * c->k);
+    const int end_bit = (int)std::min<uint64_t>(64, 2 * c->k);  // (k > 32: u64 compat keys)
     if ((rc = c->x_sorted.ensure(cnt[1])) || (rc = c->x_tmp.ensure(exact_temp_bytes(cnt[1], end_bit))))
       return rc;
     HIPCHK(exact_sort_rle(t.side, c->x_sorted.p, cnt[1], end_bit, c->x_uniq.p + cnt[0],

@@ -136,7 +136,7 @@ __device__ __forceinline__ void sort_and_store(const uint32_t (&E)[PER], const u
       } else {
         reinterpret_cast<uint4 *>(d)[0] = src[0];
       }
-    } else {  // region full: count directly (exact, slow, rare)
+    } else if (currents) {  // region full: count directly (exact, slow, rare; none in a table-only pass)
       for (int i = 0; i < 8; ++i) {
         const uint32_t o = (uint32_t)s_rec[g * 8 + i];
         if (o != S::kPad) atomicAdd(&currents[(bg << bin_bits) | (o & ((1u << bin_bits) - 1u))], 1ULL);
@@ -232,10 +232,15 @@ struct GenLds {
 
 // K1g: hash + partition for key modes KM 0/1/2 (see the file comment) of
 // tile in.tile_base + bi.  Lane = 16 consecutive positions of an 8192-position tile.
-template <int KM, bool CANON, bool WIDE>
+// KEYS (narrow, u64 keys: KM 0/1): each kept record's key is also written to
+// ka->key at the record's slot (the grouped exact table's input, as
+// K1a<KEYS> writes it for k <= 32), a record past its full region's key to
+// the side list, pad slots' keys as 0.
+template <int KM, bool CANON, bool WIDE, bool KEYS = false>
 __device__ __forceinline__ void gen_tile(const KmerInput &in, int k, const FastMod &fm,
                                          const GenPartArgs &ga, uint64_t bi,
-                                         GenLds<WIDE, !CANON> &sm) {
+                                         GenLds<WIDE, !CANON> &sm, const GenKeyArgs *ka = nullptr) {
+  static_assert(!KEYS || (KM < 2 && !WIDE), "keys: narrow u64-key modes");
   using S = GenShape<WIDE>;
   constexpr bool kRaw = !CANON;
   TileLds<kPartTile, kRaw> &L = sm.L;
@@ -286,6 +291,40 @@ __device__ __forceinline__ void gen_tile(const KmerInput &in, int k, const FastM
   }
   RecCursor rc;
   rec_cursor_init<KM>(rc, in, T0 + (uint64_t)q0, bi);
+  if constexpr (KEYS) {
+    uint64_t K[kPer];  // (fully unrolled: the keys stay in registers until their slots are known)
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int q = q0 + j;
+      const bool ok = window_valid(L, T0, q, k, in.n_bases, in.pos_lo, in.pos_hi);
+      K[j] = ok ? gen_key<KM, CANON>(L, in, q, T0 + (uint64_t)q, k, rc).lo : 0ull;
+      const uint64_t h = ok ? gen_hash<KM>(Key128{K[j], 0}) : 0ull;
+      const uint32_t idx = small_pool ? fastmod32(h, fm) : (uint32_t)fastmod(h, fm);
+      const uint32_t b = ok ? (idx >> bb) : nb;
+      E[j] = (b << 16) | atomicAdd(&sm.s_cnt[b], 1u);
+      O[j] = idx & omask;
+    }
+    sort_and_store<false, kPer>(E, O, nb, sm.s_cnt, sm.s_start, sm.s_base, sm.s_fit, sm.s_rec,
+                                sm.s_gmap, ga.fill, ga.overflow, ga.cap,
+                                reinterpret_cast<typename S::Rec *>(ga.rec), 0, bb, ga.currents);
+    // s_base / s_fit / s_cnt stay as the reservation left them (the stores only read them)
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const uint32_t b = E[j] >> 16, r = E[j] & 0xFFFFu;
+      if (b >= nb) continue;
+      if (r < sm.s_fit[b]) {
+        ka->key[(uint64_t)b * ga.cap + sm.s_base[b] + r] = K[j];
+      } else {
+        const unsigned long long at = atomicAdd(ka->n_spill, 1ull);
+        if (at < ka->spill_cap) ka->spill[at] = K[j];
+      }
+    }
+    for (uint32_t b = tid; b < nb; b += kPartBlock) {
+      const uint32_t c = sm.s_cnt[b], cp = (c + 7u) & ~7u, fit = sm.s_fit[b];
+      for (uint32_t i = c; i < cp && i < fit; ++i) ka->key[(uint64_t)b * ga.cap + sm.s_base[b] + i] = 0ull;
+    }
+    return;
+  }
 #pragma unroll 2
   for (int j = 0; j < kPer; ++j) {
     const int q = q0 + j;
@@ -307,6 +346,15 @@ __global__ __launch_bounds__(kPartBlock) void k_part_gen(KmerInput in, int k, Fa
                                                          GenPartArgs ga) {
   __shared__ GenLds<WIDE, !CANON> sm;
   gen_tile<KM, CANON, WIDE>(in, k, fm, ga, blockIdx.x, sm);
+}
+
+// K1g<KEYS>: the grouped exact table's own partition pass for k > 32
+// (NK_KMER_COMPAT u64 keys; nk_table_host.cpp::build_grouped)
+template <int KM, bool CANON>
+__global__ __launch_bounds__(kPartBlock) void k_part_gen_keys(KmerInput in, int k, FastMod fm,
+                                                              GenPartArgs ga, GenKeyArgs ka) {
+  __shared__ GenLds<false, !CANON> sm;
+  gen_tile<KM, CANON, false, true>(in, k, fm, ga, blockIdx.x, sm, &ka);
 }
 
 constexpr int kSplitBlock = kPartBlock;
@@ -736,6 +784,27 @@ hipError_t launch_part_gen(const KmerInput &in, int k, int canonical, int km, ui
   }
 #undef NK_GEN_W
 #undef NK_GEN
+  return hipGetLastError();
+}
+
+hipError_t launch_part_gen_keys(const KmerInput &in, int k, int canonical, int km, uint64_t pool,
+                                const GenPartArgs &ga, const GenKeyArgs &ka, hipStream_t s) {
+  if (!in.n_tiles) return hipSuccess;
+  if (pool == 0 || pool > (1ull << 31) || km < 0 || km > 1 || !ka.key || !ka.n_spill) return hipErrorInvalidValue;
+  if (ga.n_buckets > (uint32_t)kMaxBuckets || ga.bin_bits < 12 || ga.bin_bits > kBinBits)
+    return hipErrorInvalidValue;
+  if ((km == 0 && k > 32) || (km == 1 && (k <= 32 || k > 64)) || k < 1) return hipErrorInvalidValue;
+  const FastMod fm = make_fastmod(pool);
+  const dim3 g((unsigned)in.n_tiles), b(kPartBlock);
+#define NK_GK(KM_, C_) hipLaunchKernelGGL((k_part_gen_keys<KM_, C_>), g, b, 0, s, in, k, fm, ga, ka)
+  if (canonical) {
+    if (km == 0) NK_GK(0, true);
+    else NK_GK(1, true);
+  } else {
+    if (km == 0) NK_GK(0, false);
+    else NK_GK(1, false);
+  }
+#undef NK_GK
   return hipGetLastError();
 }
 

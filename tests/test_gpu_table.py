@@ -95,7 +95,11 @@ MODES = [
 
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("k,pool,canon", [(31, 2_000_000, True), (21, 100_003, False),
-                                          (32, 40_000, False), (11, 5_000, True)])
+                                          (32, 40_000, False), (11, 5_000, True),
+                                          # k > 32 (NK_KMER_COMPAT u64 keys): the table's
+                                          # own K1g<KEYS> pass (k_part_gen_keys)
+                                          (40, 50_021, True), (63, 1_000_003, False),
+                                          (33, 7_001, True)])
 def test_grouped_table(mode, k, pool, canon):
     bases, offs = synth.make_records(600_000, 5, repeats_per_mb=2000, motif_len=120,
                                      n_rate=0.005, mixed_case=True, seed=41 + k)
@@ -106,17 +110,18 @@ def test_grouped_table(mode, k, pool, canon):
     np.testing.assert_array_equal(g.currents(), r.currents())
 
 
-@pytest.mark.parametrize("exact", [True, False])
-def test_overflowed_regions_spill_to_the_side(exact):
-    """One k-mer dominates (a long poly-A record): its bucket's K1a region
-    overflows, the excess keys spill, the bucket goes through the side part."""
+@pytest.mark.parametrize("exact,k", [(True, 31), (False, 31), (True, 45), (False, 45)])
+def test_overflowed_regions_spill_to_the_side(exact, k):
+    """One k-mer dominates (a long poly-A record): its bucket's K1a (k > 32:
+    K1g<KEYS>) region overflows, the excess keys spill, the bucket goes
+    through the side part."""
     rnd, _ = synth.make_records(300_000, 1, seed=5)
     bases = np.concatenate([np.full(400_000, ord("A"), np.uint8), rnd,
                             np.frombuffer(b"AAAAT" * 20_000, np.uint8)])
     offs = np.array([0, 400_000, 700_000, bases.size], np.uint64)
-    g = run(bases, offs, 31, 2_000_000, True, exact=exact)
-    r = oracle(bases, offs, 31, 2_000_000, True)
-    check_table(g, r, keys_of(bases, offs, 31, True), n_probe_keys=20_000)
+    g = run(bases, offs, k, 2_000_000, True, exact=exact)
+    r = oracle(bases, offs, k, 2_000_000, True)
+    check_table(g, r, keys_of(bases, offs, k, True), n_probe_keys=20_000)
     np.testing.assert_array_equal(g.currents(), r.currents())
     assert g.top_abundant_neurons(20) == r.top_abundant_neurons(20)
 
