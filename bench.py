@@ -816,6 +816,24 @@ def extras(args, ctr, bases, offsets, nk, d_bases, d_offs, s_handle, dev_idx, Co
                        f"process_parallel restatement, one thread per record like rayon over "
                        f"records (src/spiking_hash.rs:94-95), exact k-mer map, serial merge and "
                        f"1000-step LIF")}
+        # SURVEY.md §8d's optional stronger baseline, labelled as such: the same
+        # currents and spike counts by chunked threads with no exact k-mer map
+        # and a memoised LIF (oracle/nk_oracle.c nko_lean_currents_lif)
+        from oracle import cbind
+        lt = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1))
+        log(f"cpu_baseline: lean variant on {lt} threads")
+        t_l = time.perf_counter()
+        l_cur, l_sp, l_tot = cbind.lean_currents_lif(bases, offsets, k, pool, True, 1000, lt)
+        dt_l = time.perf_counter() - t_l
+        out["cpu_baseline"]["lean"] = {
+            "value": round(nk / dt_l / 1e6, 4), "unit": "Mk-mers/s", "cores": lt,
+            "seconds": round(dt_l, 3),
+            "kind": "lean (NOT the reference's structure): currents + spike counts only",
+            "sample": "the same whole rank-0 input: windows split across threads, per-thread u64 "
+                      "currents summed, no exact k-mer map, 1000-step LIF memoised by count",
+            "same_results": bool(np.array_equal(l_cur, ref.currents())
+                                 and np.array_equal(l_sp, ref.spike_counts())
+                                 and l_tot == ref.total_spikes)}
         # the timed GPU run's final state (the last step) vs the restatement
         out["parity_full"] = parity(ctr, ref)
         if "exact_counts_step" in out:  # counts.len() of the exact table vs the map

@@ -725,3 +725,114 @@ int nko_get_count128(const nko_counter *c, uint64_t lo, uint64_t hi, uint32_t *o
 int nko_get_count(const nko_counter *c, uint64_t kmer, uint32_t *out) {
   return kmap_get(&c->counts, kmer, out);
 }
+
+/* ------------------------------------------------------------------------ */
+/* Lean CPU baseline (not the reference's structure; see nk_oracle.h)        */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  const uint8_t *bases;
+  const uint64_t *offsets;
+  size_t n_recs, k;
+  int canonical;
+  uint64_t pool, steps, w_lo, w_hi; /* this thread's windows [w_lo, w_hi) of all windows */
+  uint64_t *cur;                    /* this thread's currents (pool) */
+  uint64_t *cur_all, *spikes, n_lo, n_hi, total; /* the LIF phase: neurons [n_lo, n_hi) */
+  int nthreads, idx;
+  void *all;
+} lean_ctx;
+
+static void *lean_count(void *p) {
+  lean_ctx *t = (lean_ctx *)p;
+  uint64_t w0 = 0; /* windows before record r */
+  for (size_t r = 0; r < t->n_recs; ++r) {
+    const uint64_t s0 = t->offsets[r], len = t->offsets[r + 1] - s0;
+    const uint64_t nw = len >= t->k ? len - t->k + 1 : 0;
+    const uint64_t a = t->w_lo > w0 ? t->w_lo - w0 : 0, b = t->w_hi < w0 + nw ? t->w_hi - w0 : nw;
+    if (a < b) {
+      const uint8_t *seq = t->bases + s0;
+      if (t->canonical) {
+        roll_t h;
+        roll_new(&h, t->k);
+        roll_init(&h, seq + a);
+        t->cur[nko_sip13_u64(h.fwd < h.rev ? h.fwd : h.rev) % t->pool] += 1;
+        for (uint64_t i = a + 1; i < b; ++i) {
+          roll_slide(&h, seq[i + t->k - 1], seq[i - 1]);
+          t->cur[nko_sip13_u64(h.fwd < h.rev ? h.fwd : h.rev) % t->pool] += 1;
+        }
+      } else {
+        for (uint64_t i = a; i < b; ++i) t->cur[nko_sip13_u64(nko_pack_kmer(seq + i, t->k)) % t->pool] += 1;
+      }
+    }
+    w0 += nw;
+    if (w0 >= t->w_hi) break;
+  }
+  return NULL;
+}
+
+static void *lean_lif(void *p) {
+  lean_ctx *t = (lean_ctx *)p;
+  lean_ctx *all = (lean_ctx *)t->all;
+  uint64_t tot = 0;
+  enum { kMemo = 4096 };  /* spikes depend on the count alone (fresh state): memoised */
+  uint64_t memo[kMemo];
+  for (int i = 0; i < kMemo; ++i) memo[i] = UINT64_MAX;
+  for (uint64_t i = t->n_lo; i < t->n_hi; ++i) {
+    uint64_t c = 0;
+    for (int j = 0; j < t->nthreads; ++j) c += all[j].cur[i];
+    t->cur_all[i] = c;
+    uint64_t sp;
+    if (c < kMemo && memo[c] != UINT64_MAX) {
+      sp = memo[c];
+    } else {
+      float v = 0.0f;
+      uint32_t r = 0;
+      sp = 0;
+      nko_lif(c, t->steps, 1.0f, 0.95f, 2, 0, &v, &r, &sp);
+      if (c < kMemo) memo[c] = sp;
+    }
+    t->spikes[i] = sp;
+    tot += sp;
+  }
+  t->total = tot;
+  return NULL;
+}
+
+int nko_lean_currents_lif(const uint8_t *bases, const uint64_t *offsets, size_t n_recs, size_t k,
+                          int canonical, uint64_t pool, uint64_t steps, int n_threads,
+                          uint64_t *currents, uint64_t *spikes, uint64_t *total_spikes) {
+  if (!pool || k < 1 || k > 32 || n_threads < 1) return -1;
+  uint64_t nw = 0;
+  for (size_t r = 0; r < n_recs; ++r) {
+    const uint64_t len = offsets[r + 1] - offsets[r];
+    nw += len >= k ? len - k + 1 : 0;
+  }
+  lean_ctx *t = (lean_ctx *)calloc((size_t)n_threads, sizeof(lean_ctx));
+  pthread_t *th = (pthread_t *)calloc((size_t)n_threads, sizeof(pthread_t));
+  if (!t || !th) { free(t); free(th); return -1; }
+  int rc = 0;
+  for (int j = 0; j < n_threads; ++j) {
+    t[j].bases = bases; t[j].offsets = offsets; t[j].n_recs = n_recs; t[j].k = k;
+    t[j].canonical = canonical; t[j].pool = pool; t[j].steps = steps;
+    t[j].w_lo = nw * (uint64_t)j / (uint64_t)n_threads;
+    t[j].w_hi = nw * (uint64_t)(j + 1) / (uint64_t)n_threads;
+    t[j].cur = (uint64_t *)calloc(pool, sizeof(uint64_t));
+    t[j].cur_all = currents; t[j].spikes = spikes;
+    t[j].n_lo = pool * (uint64_t)j / (uint64_t)n_threads;
+    t[j].n_hi = pool * (uint64_t)(j + 1) / (uint64_t)n_threads;
+    t[j].nthreads = n_threads; t[j].idx = j; t[j].all = t;
+    if (!t[j].cur) rc = -1;
+  }
+  if (!rc) {
+    for (int j = 0; j < n_threads; ++j) pthread_create(&th[j], NULL, lean_count, &t[j]);
+    for (int j = 0; j < n_threads; ++j) pthread_join(th[j], NULL);
+    for (int j = 0; j < n_threads; ++j) pthread_create(&th[j], NULL, lean_lif, &t[j]);
+    for (int j = 0; j < n_threads; ++j) pthread_join(th[j], NULL);
+    uint64_t tot = 0;
+    for (int j = 0; j < n_threads; ++j) tot += t[j].total;
+    *total_spikes = tot;
+  }
+  for (int j = 0; j < n_threads; ++j) free(t[j].cur);
+  free(t);
+  free(th);
+  return rc;
+}

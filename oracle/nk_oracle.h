@@ -78,6 +78,18 @@ int nko_process_streaming(nko_counter *c, const uint8_t *bases,
 /* simulate_spikes_auto (src/spiking_hash.rs:697-714 -> simulate_spikes_simd,
  * :544-659): the streaming LIF rule over the held currents */
 void nko_simulate_spikes_auto(nko_counter *c);
+
+/* A lean CPU baseline, NOT the reference's structure ("an
+ * honest stronger baseline, clearly labelled not-the-reference"): the
+ * currents of one in-memory call without the exact k-mer map, over n_threads
+ * chunks of the windows (each record's k-mers split by position; k <= 32, where
+ * the canonical key is a function of its window alone, models.rs:254-286),
+ * per-thread u64 currents summed, then the 1000-step LIF of every neuron from
+ * the fresh state in parallel over neurons (nko_lif: the reference's update
+ * loop, bit-identical).  Writes currents[pool], spikes[pool], *total_spikes. */
+int nko_lean_currents_lif(const uint8_t *bases, const uint64_t *offsets, size_t n_recs, size_t k,
+                          int canonical, uint64_t pool, uint64_t steps, int n_threads,
+                          uint64_t *currents, uint64_t *spikes, uint64_t *total_spikes);
 /* process_sequence (src/spiking_hash.rs:203-273): per-record single-step form */
 int nko_process_sequence(nko_counter *c, const uint8_t *seq, size_t len);
 

@@ -407,3 +407,20 @@ def test_oracle_fast_paths_equal_the_plain_loops():
             vv, r1, s1 = cbind.lif(int(cur[i]), 1000, 1.0, 0.95, 2, not streaming)
             assert (s1, r1) == (int(sc[i]), int(rr[i]))
             assert np.float32(vv).view(np.uint32) == v[i].view(np.uint32)
+
+
+@pytest.mark.parametrize("canon,threads", [(True, 1), (True, 4), (False, 3)])
+def test_lean_cpu_baseline_matches_the_restatement(canon, threads):
+    """bench.py's lean CPU baseline (nko_lean_currents_lif: no exact map, chunked
+    windows, memoised LIF; not the reference's structure) gives the
+    restatement's currents, spike counts and total spikes."""
+    from neurokmer_amd import synth
+    bases, offs = synth.make_records(60_000, 5, seed=17, repeats_per_mb=20_000, motif_len=80,
+                                     n_rate=0.003, mixed_case=True)
+    k, pool = 21, 5_003
+    cur, sp, tot = cbind.lean_currents_lif(bases, offs, k, pool, canonical=canon, n_threads=threads)
+    r = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, canon)
+    r.process_parallel_arrays(bases, offs)
+    np.testing.assert_array_equal(cur, r.currents())
+    np.testing.assert_array_equal(sp, r.spike_counts())
+    assert tot == r.total_spikes
