@@ -224,6 +224,14 @@ def main() -> int:
                     help="batches in flight (default: 3 on one GPU, 1 across ranks and for "
                          "config5): > 1 "
                          "overlaps a batch's finish with the next batch's count")
+    ap.add_argument("--count-streams", type=int, default=1, choices=(1, 2),
+                    help="2: batches alternate between two count streams (A/B, with "
+                         "NK_COUNT_CHAIN=1: a count kernel waits for the previous batch's count "
+                         "kernel, not its histogram)")
+    ap.add_argument("--defer-hist", choices=("auto", "on", "off"), default="auto",
+                    help="each handle's bucket histogram (K1b) inside the next handle's count "
+                         "kernel (nk_opts.defer_hist, k_part_fused); auto: on with >= 3 batches "
+                         "in flight on one GPU")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -357,8 +365,14 @@ def main() -> int:
     # next batch's count.  The library orders a handle's calls across streams
     # itself (pick_stream: the finish waits for the end of ITS handle's count
     # only).  --inflight 1: one handle, one stream, one batch at a time.
+    # K1b of batch i inside K1a of batch i+1 (k_part_fused): a batch's finish
+    # then waits for the next count, so it needs three batches in flight (with
+    # two the count stream would idle through every finish)
+    defer_hist = (args.defer_hist == "on" or
+                  (args.defer_hist == "auto" and args.inflight >= 3 and not dist_on))
     ctrs = [SpikingKmerCounter(k, 1.0, 0.95, 2, 1.0, pool, True, device=dev_idx,
-                               kmer_width=args.kmer_width) for _ in range(args.inflight)]
+                               kmer_width=args.kmer_width, defer_hist=defer_hist)
+            for _ in range(args.inflight)]
     ctr = ctrs[0]
     # non-default streams: a NULL stream handle would mean the library's own.
     # (Count streams CU-masked to leave 8-32 CUs to the finishes slowed K1a by
@@ -371,6 +385,9 @@ def main() -> int:
     # 0.529-0.537 vs 0.507-0.514 ms, profiles/r02_s31); handles alternating
     # between two count streams (0.5166 vs 0.5026 ms, profiles/r03_cs2).
     count_streams = [torch.cuda.Stream(device=dev)] * args.inflight
+    batch_streams = [count_streams[0]] + ([torch.cuda.Stream(device=dev)]
+                                          if args.count_streams == 2 else [])
+    n_started = [0]
     run_stream = count_streams[0]
     fin_stream = (torch.cuda.Stream(device=dev, priority=torch.cuda.Stream.priority_range()[1])
                   if args.inflight > 1 else run_stream)
@@ -387,7 +404,8 @@ def main() -> int:
     def start(j):
         """Enqueue one batch's count on handle j (returns at once)."""
         t_s = time.perf_counter()
-        c, cs = ctrs[j], count_streams[j]
+        c, cs = ctrs[j], batch_streams[n_started[0] % len(batch_streams)]
+        n_started[0] += 1
         sh = cs.cuda_stream
         c.reset(sh, blocking=False)
         if side:
@@ -516,6 +534,11 @@ def main() -> int:
     # handle 1's steps in the overlapped run (the other batch's finish beside it)
     spans = ctr.count_spans(args.steps)
     spans2 = ctrs[1].count_spans(args.steps // args.inflight) if args.inflight > 1 else []
+    # the overlapped run's count kernels (handles 1.., whose last counts are that
+    # run's; handle 0's are the one-in-flight run's): with defer_hist each is
+    # k_part_fused (K1a of its batch + K1b of the batch before)
+    spans_ov = [x for c in ctrs[1:] for x in c.count_spans(args.steps // args.inflight)] \
+        if args.inflight > 1 else []
     # the same steps writing the per-neuron state out in each (the reference
     # writes v, refractory and spike counts in every call, src/spiking_hash.rs:
     # 186-200; the step above leaves them derived from the currents until a
@@ -548,6 +571,14 @@ def main() -> int:
             world * nk_rank / (dt / args.steps) / 1e6
         sp = [x for x in spans if x > 0]
         k1_ms = float(np.mean(sp)) if sp else (float(np.mean(ev_ms)) if ev_ms else float("nan"))
+        k1a_alone_ms = k1_ms  # K1a without K1b (the one-in-flight run)
+        fused = defer_hist and args.workload == "config2" and k <= 32 and pool <= (1 << 23)
+        if fused:
+            # the metric's dominant kernel is then k_part_fused, as it runs in
+            # the timed overlapped steps (the next batch's finish beside it):
+            # the count's whole work, K1a's hash + K1b's histogram, per launch
+            sp = [x for x in spans_ov if x > 0]
+            k1_ms = float(np.mean(sp)) if sp else k1_ms
         # roofline of the dominant kernel (K1a), algorithmic bytes per launch =
         # input bases read once + one 8-B counter update per k-mer
         alg_bytes = n_bases + 8 * nk_rank
@@ -586,6 +617,7 @@ def main() -> int:
             "steps": args.steps, "warmup": args.warmup, "settle_steps": settle,
             "ms_per_step": round(ms_step, 4),
             "inflight": args.inflight,
+            "defer_hist": defer_hist,
             "ms_per_step_one_in_flight": round(dt1 / args.steps * 1e3, 4),
             "ms_per_step_state_written": (round(dt_settle / args.steps * 1e3, 4)
                                           if dt_settle is not None else None),
@@ -615,8 +647,11 @@ def main() -> int:
             "roofline": {"bound": bound,
                          "kernel": ("the count of a step: every batch's K1 (k_part / k_part_gen "
                                     "+ k_split) + K1b (k_bucket_hist)" if cm else
+                                    "k_part_fused (K1a of batch i+1 + K1b of batch i: the "
+                                    "count's hash and histogram, one launch per step)" if fused else
                                     "k_part<canonical> (K1a)" if k <= 32 and pool <= (1 << 24)
                                     else "the count: k_part_gen (K1g) + k_split (K1s)"),
+                         "k1a_alone_ms": round(k1a_alone_ms, 4) if fused else None,
                          "achieved": round(achieved / 1e9, 2), "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": round(hbm_frac, 4),
                          "traffic": traffic,
@@ -626,6 +661,8 @@ def main() -> int:
                          "avg_launch_source": (
                              "hipEvents on the count stream around each timed step's count "
                              "(every batch's K1 + K1b), median" if cm else
+                             "in-kernel s_memrealtime span over the timed (overlapped) steps' "
+                             "count kernels" if fused and sp else
                              ("in-kernel s_memrealtime span over the one-in-flight timed steps"
                               if sp else "hipEvents")),
                          "launches_timed": len(sp),

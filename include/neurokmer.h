@@ -75,7 +75,19 @@ typedef struct nk_opts {
                             unless exact_counts = 1).  The multi-GPU exact
                             table (nk_exact_*) needs exact_counts = 1 and
                             NK_KMER_COMPAT keys. */
-  uint32_t reserved[11];
+  uint32_t defer_hist;   /* 1: batches in flight on one stream (several handles
+                            counting one after the other, each finish on another
+                            stream): a partitioned count (k <= 32, pool <= 8.4 M)
+                            leaves its bucket histogram (K1b) pending and the
+                            next such count on the same stream and host thread
+                            -- of another handle -- runs it inside its own hash
+                            kernel (k_part_fused), where it takes HBM and LDS
+                            time the hash leaves idle.  The results are the
+                            same; whatever reads this handle's counts first
+                            waits for that kernel (or runs the histogram itself
+                            when no count took it).  Default 0: each count
+                            histograms its own records. */
+  uint32_t reserved[10];
 } nk_opts;
 
 /* Fills *o with the defaults above. */
@@ -432,8 +444,12 @@ int nk_diag_hash_ms_w(int device, uint64_t n_keys, uint64_t pool, int width, int
  * and XOR-folds the keys into *checksum (may be NULL): what an exact-table pass
  * that reads positions instead of K1a-written keys would pay for its keys.
  * (The checksum covers the kept records: the excess of an overflowed region,
- * counted directly, is not among them.)  Synchronises the device.  (No
- * reference counterpart: measurement only.) */
+ * counted directly, is not among them.)  Synchronises the device.  The last
+ * count's input must still be resident: when it was the caller's device
+ * memory (nk_accumulate_device*), the caller keeps it allocated until this
+ * returns -- the kernel reads those bases (the handle's own copies, from the
+ * host-array and file entry points, are always resident).  (No reference
+ * counterpart: measurement only.) */
 int nk_diag_key_gather_ms(nk_counter *c, int reps, float *ms, uint64_t *checksum);
 
 /* ---- associative memory (src/associative.rs) -------------

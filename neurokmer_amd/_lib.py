@@ -56,7 +56,7 @@ EXPORTS = (
 class NkOpts(C.Structure):
     _fields_ = [("device", C.c_int32), ("kmer_width", C.c_int32), ("top_n", C.c_uint32),
                 ("stage_timing", C.c_uint32), ("exact_counts", C.c_uint32),
-                ("reserved", C.c_uint32 * 11)]
+                ("defer_hist", C.c_uint32), ("reserved", C.c_uint32 * 10)]
 
 
 class NkTopRow(C.Structure):

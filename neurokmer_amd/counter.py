@@ -51,7 +51,11 @@ class SpikingKmerCounter:
     def __init__(self, k: int, threshold: float, leak: float, refractory: int,
                  spike_cost: float, pool_size: int, use_canonical: bool, *,
                  device: int = 0, top_n: int = 20, stage_timing: bool = False,
-                 kmer_width: int = 64, exact_counts: bool = False):
+                 kmer_width: int = 64, exact_counts: bool = False,
+                 defer_hist: bool = False):
+        """defer_hist: batches in flight on one count stream across handles --
+        this handle's bucket histogram runs inside the next handle's count
+        kernel (nk_opts.defer_hist); same results."""
         self._L = _lib.load()
         o = NkOpts()
         self._L.nk_opts_default(C.byref(o))
@@ -62,6 +66,7 @@ class SpikingKmerCounter:
             raise ValueError("kmer_width must be 64 (the reference's u64 keys) or 128")
         o.kmer_width = _lib.NK_KMER_128 if kmer_width == 128 else _lib.NK_KMER_COMPAT
         o.exact_counts = 1 if exact_counts else 0
+        o.defer_hist = 1 if defer_hist else 0
         self.kmer_width = kmer_width
         self.exact_counts = bool(exact_counts)
         self._h = None

@@ -6,6 +6,8 @@
 // (nk_fqhost.h: threads pread and parse), window by window as
 // nk_ingest_host.cpp runs it; prints
 // "fallback" (a blank line where a header is due) instead of records then.
+// --shrink <bytes> after --mapped's arguments: the file is cut to that size
+// after it was opened and sized (a read that ends early: NK_E_IO, not a stop).
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -31,10 +33,14 @@ static void print_records(const std::vector<uint8_t> &bases, const std::vector<u
   }
 }
 
-static int mapped(const char *path, size_t win, int threads, uint64_t max_rec) {
+static int mapped(const char *path, size_t win, int threads, uint64_t max_rec, long long shrink) {
   nk::HostFile hf;
   std::string err;
   int rc = hf.open(path, err);
+  if (!rc && shrink >= 0 && truncate(path, (off_t)shrink) != 0) {
+    rc = NK_E_IO;
+    err = "truncate failed";
+  }
   std::vector<uint8_t> bases;
   std::vector<uint64_t> offs{0};
   bool stop = false, blank = false;
@@ -60,6 +66,11 @@ static int mapped(const char *path, size_t win, int threads, uint64_t max_rec) {
       he.resize(nk::fq_max_records(len));
       nk::FqResult r = nk::fq_extract(rb.data(), len, eof, hb.data(), he.data(), bases.size(), pool,
                                       hf.fd(), pos, nullptr, max_rec);
+      if (!r.io_error.empty()) {  // (nk_ingest_host.cpp: NK_E_IO)
+        rc = NK_E_IO;
+        err = r.io_error;
+        break;
+      }
       if (!r.n_rec && !r.stop && !r.blank && !eof) {  // a record longer than the window
         win *= 2;
         continue;
@@ -68,7 +79,11 @@ static int mapped(const char *path, size_t win, int threads, uint64_t max_rec) {
       offs.insert(offs.end(), he.begin(), he.begin() + r.n_rec);
       pos += r.consumed;
       if (r.blank) { blank = true; break; }
-      if (r.stop) { stop = true; break; }
+      if (r.stop) {
+        nk::warn_malformed(path, offs.size() - 1, "a FASTQ record is malformed or cut off");
+        stop = true;
+        break;
+      }
       if (eof && !r.more) break;
     }
   }
@@ -84,9 +99,15 @@ int main(int argc, char **argv) {
     fprintf(stderr, "usage: fastx_dump <file> [batch_bases | --mapped <window> <threads>]\n");
     return 2;
   }
-  if (argc > 4 && !strcmp(argv[2], "--mapped"))
-    return mapped(argv[1], strtoull(argv[3], nullptr, 10), atoi(argv[4]),
-                  argc > 5 ? strtoull(argv[5], nullptr, 10) : ~0ull);
+  if (argc > 4 && !strcmp(argv[2], "--mapped")) {
+    long long shrink = -1;
+    uint64_t max_rec = ~0ull;
+    for (int i = 5; i < argc; ++i) {
+      if (!strcmp(argv[i], "--shrink") && i + 1 < argc) shrink = atoll(argv[++i]);
+      else max_rec = strtoull(argv[i], nullptr, 10);
+    }
+    return mapped(argv[1], strtoull(argv[3], nullptr, 10), atoi(argv[4]), max_rec, shrink);
+  }
   size_t batch = argc > 2 ? strtoull(argv[2], nullptr, 10) : (1u << 20);
   nk::FastxReader r;
   std::string err;
@@ -96,6 +117,10 @@ int main(int argc, char **argv) {
   if (!rc)
     while (r.next_batch(batch, bases, offs)) {
     }
+  if (!rc && r.io_error()) {
+    rc = NK_E_IO;
+    err = r.io_why();
+  }
   printf("{\"rc\":%d,\"err\":\"%s\",\"truncated\":%s,\"records\":[", rc, err.c_str(),
          r.truncated() ? "true" : "false");
   print_records(bases, offs);

@@ -3,6 +3,9 @@
 // launches (k_part / k_part_gen [+ k_split] + k_bucket_hist), batches.
 #include "nk_handle.h"
 
+#include <mutex>
+#include <thread>
+
 // How one count batch runs:
 //   Part   k <= 32 keys, pool <= 16.7 M: k_part (rolled keys) + k_bucket_hist;
 //          the records are kept for the uniques scan
@@ -278,6 +281,174 @@ hipError_t batch_count(nk_counter *c, const CountPlan &cp, const KmerInput &in, 
   return launch_zero(z, s);
 }
 
+// ---------------------------------------------------------------------------
+// K1b deferred across handles (opts.defer_hist).  With batches in flight on
+// one count stream, K1b of batch i (HBM- and LDS-bound, ~50 us at config 2)
+// runs inside K1a of batch i+1 (VALU-bound, HBM ~80 % idle): k_part_fused.
+// One slot per device holds the Part count whose K1b has not run; the next
+// fusable count on the same stream, from the same host thread and of another
+// handle, takes it (its own K1b then waits in the slot in turn).  The owner's
+// readers (hist_ready) wait for the fused kernel's end (hist_ev), or run the
+// K1b themselves when nothing took it.
+// ---------------------------------------------------------------------------
+namespace {
+struct HistSlot {
+  nk_counter *owner = nullptr;
+  hipStream_t s = nullptr;
+  std::thread::id tid;
+};
+std::mutex g_hist_mu;
+constexpr int kHistSlots = 64;
+HistSlot g_hist_slot[kHistSlots];
+HistSlot &slot_of(int dev) { return g_hist_slot[(unsigned)dev % kHistSlots]; }
+constexpr uint64_t kFuseMinTiles = 512;  // a count this small runs its own K1b
+
+// K1b of the Part count c as the standalone kernel
+hipError_t hist_run(nk_counter *c, hipStream_t s) {
+  return launch_bucket_hist(c->last_pa, c->pool, c->hist_slices, c->partials.p, s);
+}
+
+// slices of a deferred K1b (partials the LIF folds; NK_FUSE_SLICES: A/B)
+uint32_t fuse_slices(uint32_t dflt) {
+  const char *e = getenv("NK_FUSE_SLICES");
+  const long v = e ? strtol(e, nullptr, 10) : 0;
+  return v > 0 && v <= 64 ? (uint32_t)v : dflt;
+}
+
+// the workgroups of the taking count that host the items: the first
+// NK_FUSE_HOST_PCT percent of its grid (default 75: no item in the tail)
+uint32_t fuse_hosts(uint64_t n_tiles) {
+  const char *e = getenv("NK_FUSE_HOST_PCT");
+  const long v = e ? strtol(e, nullptr, 10) : 0;
+  const uint64_t pct = v > 0 && v <= 100 ? (uint64_t)v : 75;
+  return (uint32_t)std::max<uint64_t>(1, n_tiles * pct / 100);
+}
+
+// another handle's pending K1b that the count of c on stream s can take
+nk_counter *hist_take(nk_counter *c, hipStream_t s, uint64_t n_tiles, HistJob &hj) {
+  std::lock_guard<std::mutex> g(g_hist_mu);
+  HistSlot &h = slot_of(c->device);
+  nk_counter *a = h.owner;
+  if (!a || a == c || h.s != s || h.tid != std::this_thread::get_id()) return nullptr;
+  h.owner = nullptr;
+  const PartArgs &pa = a->last_pa;
+  hj.off = pa.off;
+  hj.fill = pa.fill;
+  hj.cap = pa.cap;
+  hj.n_buckets = pa.n_buckets;
+  hj.sub_shift = pa.sub_shift;
+  hj.slices = a->hist_slices;
+  hj.partials = a->partials.p;
+  hj.pool = a->pool;
+  hj.n_items = pa.n_buckets * a->hist_slices * kFusePasses;
+  hj.n_host = fuse_hosts(n_tiles);
+  a->hist_state = 2;
+  return a;
+}
+
+// c's own K1b into the slot (false: the slot holds another thread's count)
+bool hist_leave(nk_counter *c, hipStream_t s) {
+  std::lock_guard<std::mutex> g(g_hist_mu);
+  HistSlot &h = slot_of(c->device);
+  if (h.owner && h.owner != c) {
+    if (h.tid != std::this_thread::get_id()) return false;
+    // an older pending K1b of this thread that no count took (another
+    // stream): it runs now, on its own stream
+    nk_counter *a = h.owner;
+    if (hist_run(a, h.s) != hipSuccess) return false;
+    a->hist_state = 0;
+  }
+  h.owner = c;
+  h.s = s;
+  h.tid = std::this_thread::get_id();
+  c->hist_state = 1;
+  return true;
+}
+
+void hist_unslot(nk_counter *c) {
+  std::lock_guard<std::mutex> g(g_hist_mu);
+  HistSlot &h = slot_of(c->device);
+  if (h.owner == c) h.owner = nullptr;
+}
+}  // namespace
+
+int hist_ready(nk_counter *c, hipStream_t s) {
+  if (c->hist_state == 1) {
+    hist_unslot(c);
+    c->hist_state = 0;
+    HIPCHK(hist_run(c, s));
+  } else if (c->hist_state == 2) {
+    c->hist_state = 0;
+    HIPCHK(hipStreamWaitEvent(s, c->hist_ev, 0));
+  }
+  return NK_OK;
+}
+
+int hist_arena(nk_counter *c, hipStream_t s) {
+  if (c->hist_state == 1) hist_unslot(c);
+  else if (c->hist_state == 2) HIPCHK(hipStreamWaitEvent(s, c->hist_ev, 0));
+  c->hist_state = 0;
+  return NK_OK;
+}
+
+void hist_void(nk_counter *c) {
+  if (c->hist_state == 1) {
+    hist_unslot(c);
+    c->hist_state = 0;
+  }
+}
+
+void hist_forget(nk_counter *c) {
+  hist_unslot(c);
+  if (c->hist_state == 2) (void)hipEventSynchronize(c->hist_ev);
+  c->hist_state = 0;
+}
+
+// ---------------------------------------------------------------------------
+// Count chain (NK_COUNT_CHAIN=1, A/B): the partitioned count kernel of one
+// batch waits for the previous batch's count KERNEL on the device (an event
+// recorded right after it), not for its K1b -- with batches alternating
+// between two count streams, K1a of batch i+1 then starts as K1b of batch i
+// drains instead of after it, its prep and the kernel gaps off the path.
+// ---------------------------------------------------------------------------
+namespace {
+struct ChainSlot {
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  int next = 0;
+  bool valid = false;
+  hipStream_t s = nullptr;
+};
+std::mutex g_chain_mu;
+ChainSlot g_chain[kHistSlots];
+bool chain_on() {
+  static const bool on = getenv("NK_COUNT_CHAIN") && atoi(getenv("NK_COUNT_CHAIN")) != 0;
+  return on;
+}
+}  // namespace
+
+// before the count kernel on s: wait for the previous chained count kernel
+int chain_wait(nk_counter *c, hipStream_t s) {
+  if (!chain_on()) return NK_OK;
+  std::lock_guard<std::mutex> g(g_chain_mu);
+  ChainSlot &h = g_chain[(unsigned)c->device % kHistSlots];
+  if (h.valid && h.s != s) HIPCHK(hipStreamWaitEvent(s, h.ev[h.next ^ 1], 0));
+  return NK_OK;
+}
+
+// right after the count kernel on s
+int chain_mark(nk_counter *c, hipStream_t s) {
+  if (!chain_on()) return NK_OK;
+  std::lock_guard<std::mutex> g(g_chain_mu);
+  ChainSlot &h = g_chain[(unsigned)c->device % kHistSlots];
+  for (hipEvent_t &e : h.ev)
+    if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence));
+  HIPCHK(hipEventRecord(h.ev[h.next], s));
+  h.next ^= 1;
+  h.valid = true;
+  h.s = s;
+  return NK_OK;
+}
+
 // a positive integer from the environment (tests: force the rare branches)
 uint32_t env_u32(const char *name, uint32_t dflt) {
   const char *e = getenv(name);
@@ -299,6 +470,8 @@ int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_offs,
     return fail(NK_E_INVALID, "pool_size 0 with k-mers present (the reference panics on % 0)");
   (void)hipSetDevice(c->device);
   hipStream_t s = pick_stream(c, stream);
+  // a fused count of another handle may still read this handle's records
+  if (int rc0 = hist_arena(c, s)) return rc0;
   // a derived state is a function of the counts this call replaces
   if (int rc0 = settle_state(c, s)) return rc0;
   c->pend_slices = 0;  // this call zeroes the currents: earlier partials are void
@@ -447,14 +620,37 @@ int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_offs,
   c->cur_fresh = false;
   HIPCHK(mark(c, 1, s));
   if (c->part_used) {
-    HIPCHK(launch_part(in, (int)c->k, c->canonical, c->pool, cp.pa, s));
+    // K1a; with another handle's K1b pending on this stream, fused with it
+    const bool fusable = !keyed && part_fused_ok(cp.pa) && in.n_tiles >= kFuseMinTiles;
+    HistJob hj{};
+    nk_counter *taken = fusable ? hist_take(c, s, in.n_tiles, hj) : nullptr;
+    if ((rc = chain_wait(c, s))) return rc;
+    if (taken) {
+      HIPCHK(launch_part_fused(in, (int)c->k, c->canonical, c->pool, cp.pa, hj, s));
+      HIPCHK(hipEventRecord(taken->hist_ev, s));
+    } else {
+      HIPCHK(launch_part(in, (int)c->k, c->canonical, c->pool, cp.pa, s));
+    }
+    if ((rc = chain_mark(c, s))) return rc;
     HIPCHK(mark(c, 2, s));
-    HIPCHK(launch_bucket_hist(cp.pa, c->pool, cp.slices, c->partials.p, s));
-    if (defer_partials)
-      c->pend_slices = cp.slices;
-    else
-      HIPCHK(launch_partials_add(c->partials.p, cp.slices, c->pool, c->cur.p, s));
     c->last_pa = cp.pa;
+    // this count's K1b: left to the next count on this stream, or now
+    const uint32_t fs = fuse_slices(cp.slices);
+    bool left = false;
+    if (defer_partials && fusable && c->opts.defer_hist) {
+      if ((rc = c->partials.ensure((uint64_t)fs * c->pool))) return rc;
+      c->hist_slices = fs;
+      left = hist_leave(c, s);
+    }
+    if (left) {
+      c->pend_slices = fs;
+    } else {
+      HIPCHK(launch_bucket_hist(cp.pa, c->pool, cp.slices, c->partials.p, s));
+      if (defer_partials)
+        c->pend_slices = cp.slices;
+      else
+        HIPCHK(launch_partials_add(c->partials.p, cp.slices, c->pool, c->cur.p, s));
+    }
   } else if (counted) {
     HIPCHK(gen_count(c, cp, in, s, /*pipeline=*/true));
     HIPCHK(mark(c, 2, s));

@@ -72,6 +72,7 @@ void record_order(nk_counter *c, hipStream_t s) {
 // kernel; the copy-out / pointer entry points materialise zeros on demand.
 int zero_state_on(nk_counter *c, hipStream_t) {
   c->total_spikes = c->total_energy = 0;
+  hist_void(c);
   c->pend_slices = 0;
   c->cur_in_wire = false;
   c->export_pending = c->redo_ready = false;
@@ -151,6 +152,7 @@ int materialize(nk_counter *c, bool currents, hipStream_t s) {
 // (the LIF of nk_finalize folds them itself): for every other reader
 int fold_pending(nk_counter *c, hipStream_t s) {
   if (!c->pend_slices) return NK_OK;
+  if (int rc = hist_ready(c, s)) return rc;
   HIPCHK(launch_partials_add(c->partials.p, c->pend_slices, c->pool, c->cur.p, s));
   c->pend_slices = 0;
   return NK_OK;
@@ -281,7 +283,8 @@ nk_counter *nk_new(size_t k, float threshold, float leak, uint32_t refractory, d
   c->w128 = o.kmer_width == NK_KMER_128;
   c->device = o.device;
   bool ok = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) == hipSuccess &&
-            hipEventCreateWithFlags(&c->order_ev, hipEventDisableTiming) == hipSuccess;
+            hipEventCreateWithFlags(&c->order_ev, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&c->hist_ev, hipEventDisableTiming) == hipSuccess;
   // timing-only markers: no system-scope fence (a fenced marker between two
   // kernels writes back L2 and idles the GPU ~2.5 us; tools/syncbench.hip)
   for (int i = 0; ok && i <= kStages; ++i)
@@ -317,6 +320,7 @@ nk_counter *nk_new(size_t k, float threshold, float leak, uint32_t refractory, d
 void nk_free(nk_counter *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
+  hist_forget(c);
   if (c->last_s) (void)hipStreamSynchronize(c->last_s);
   if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
   c->cur.release(); c->sc.release(); c->v.release(); c->r.release();
@@ -345,7 +349,6 @@ void nk_free(nk_counter *c) {
   for (PinnedBuf &b : c->ing_he) b.release();
   for (hipEvent_t &e : c->fq_ev)
     if (e) (void)hipEventDestroy(e);
-  delete c->fq_pool;
   c->ing_draw.release();
   c->ing_draw2.release(); c->ing_scratch.release(); c->ing_dst.release();
   if (c->ing_cs) (void)hipStreamSynchronize(c->ing_cs);
@@ -366,6 +369,7 @@ void nk_free(nk_counter *c) {
     for (auto &e : pr)
       if (e) (void)hipEventDestroy(e);
   if (c->order_ev) (void)hipEventDestroy(c->order_ev);
+  if (c->hist_ev) (void)hipEventDestroy(c->hist_ev);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
 }

@@ -151,6 +151,7 @@ int nk_wire32(nk_counter *c, uint32_t *d_wire, void *stream) {
   int rc = settle_state(c, s);
   if (rc || (rc = materialize(c, true, s))) return rc;
   // partitioned count with its partials pending: only overflowed buckets added into cur
+  if (c->pend_slices && (rc = hist_ready(c, s))) return rc;
   const uint32_t *over = (c->pend_slices && c->part_used) ? c->p_over.p : nullptr;
   HIPCHK(launch_wire32(c->cur.p, c->partials.p, c->pend_slices, over, (int)c->last_pa.bin_bits,
                        c->pool, d_wire, s));

@@ -32,6 +32,10 @@ class FastxReader {
   int next_batch(size_t max_bases, std::vector<uint8_t> &bases, std::vector<uint64_t> &offsets);
   bool truncated() const { return truncated_; }  // stopped at a malformed record
   uint64_t records() const { return n_records_; }
+  // the input could not be read to its end (gzip/read error): not a malformed record
+  bool io_error() const { return !io_why_.empty(); }
+  const std::string &io_why() const { return io_why_; }
+  void set_path(const std::string &p) { path_ = p; }
 
  private:
   bool fill();
@@ -48,7 +52,14 @@ class FastxReader {
   bool pending_header_ = false;  // FASTA: a '>' line was consumed for the next record
   uint64_t n_records_ = 0;
   std::string line_;
+  std::string io_why_, path_;
+  std::string damage_;  // the gzip stream is damaged or cut off (zlib's message)
 };
+
+// The reference's `warn!("Skipping malformed record: {}", e)` when the stream
+// stops at a malformed record (src/utils.rs:17-19): one line on stderr naming
+// the record (0-based index among the records read) and the reason.
+void warn_malformed(const char *path, uint64_t record, const char *why);
 
 // Whole-file convenience (in-memory mode, src/main.rs:44).
 int read_fastx_all(const char *path, std::vector<uint8_t> &bases, std::vector<uint64_t> &offsets,

@@ -145,6 +145,7 @@ int enqueue_lif(nk_counter *c, int streaming, uint32_t fuse_want, bool part,
   }
   // partitioned count with its partials pending: the prep zeroed the currents and
   // only overflowed buckets added into them, so only those buckets are read
+  if (!wire && c->pend_slices && (rc = hist_ready(c, s))) return rc;
   const uint32_t *over = (!wire && c->pend_slices && c->part_used) ? c->p_over.p : nullptr;
   if (!fuse_want && (rc = c->sc8.ensure(c->pool))) return rc;
   HIPCHK(launch_lif_apply(c->cur.p, wire ? wire : c->partials.p, wire ? 1u : c->pend_slices,

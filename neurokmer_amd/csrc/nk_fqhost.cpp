@@ -1,7 +1,13 @@
 // nk_fqhost.cpp — see nk_fqhost.h.
 #include "nk_fqhost.h"
 
+#if defined(__x86_64__) || defined(__i386__)
 #include <emmintrin.h>
+#define NK_RELAX() _mm_pause()
+#else
+#define NK_RELAX() std::this_thread::yield()
+#endif
+#include <errno.h>
 #include <fcntl.h>
 #include <string.h>
 #include <sys/stat.h>
@@ -37,7 +43,7 @@ void HostPool::loop(int t) {
     uint64_t g = gen_.load(std::memory_order_acquire);
     for (int i = 0; g == seen && !quit_.load(std::memory_order_relaxed); ++i) {
       if (i < kSpin) {
-        _mm_pause();
+        NK_RELAX();
       } else {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return gen_.load(std::memory_order_acquire) != seen || quit_.load(); });
@@ -55,6 +61,7 @@ void HostPool::loop(int t) {
 }
 
 void HostPool::run(const std::function<void(int)> &fn) {
+  std::lock_guard<std::mutex> one(run_mu_);  // one call at a time (handles on several host threads)
   if (n_ == 1) {
     fn(0);
     return;
@@ -69,7 +76,7 @@ void HostPool::run(const std::function<void(int)> &fn) {
   fn(0);
   for (int i = 0; pending_.load(std::memory_order_acquire) != 0; ++i) {
     if (i < kSpin) {
-      _mm_pause();
+      NK_RELAX();
     } else {
       std::unique_lock<std::mutex> lk(mu_);
       done_cv_.wait(lk, [&] { return pending_.load(std::memory_order_acquire) == 0; });
@@ -83,6 +90,7 @@ HostFile::~HostFile() {
 }
 
 int HostFile::open(const char *path, std::string &err) {
+  path_ = path;
   fd_ = ::open(path, O_RDONLY);
   if (fd_ < 0) {
     err = std::string("cannot open ") + path;
@@ -107,6 +115,7 @@ void find_newlines(const uint8_t *p, size_t a, size_t b, std::vector<uint32_t> &
     if (p[i] == '\n') out.push_back((uint32_t)i);
     ++i;
   }
+#if defined(__x86_64__) || defined(__i386__)
   const __m128i nl = _mm_set1_epi8('\n');
   for (; i + 64 <= b; i += 64) {
     const __m128i *q = reinterpret_cast<const __m128i *>(p + i);
@@ -119,9 +128,15 @@ void find_newlines(const uint8_t *p, size_t a, size_t b, std::vector<uint32_t> &
       m &= m - 1;
     }
   }
+#else
+  for (const uint8_t *q; i < b && (q = (const uint8_t *)memchr(p + i, '\n', b - i)); i = (size_t)(q - p) + 1)
+    out.push_back((uint32_t)(q - p));
+  i = b;
+#endif
   for (; i < b; ++i)
     if (p[i] == '\n') out.push_back((uint32_t)i);
 }
+
 
 // the lines of the window: line i ends at the i-th '\n' (or, the extra
 // unterminated last line at eof, at len) and starts after line i - 1
@@ -144,6 +159,14 @@ enum Problem : int { kNone = 0, kBad = 1, kBlank = 2 };
 
 }  // namespace
 
+HostPool &shared_host_pool() {
+  static HostPool pool([] {  // the box's CPU share for one GPU (at most 16 threads)
+    const unsigned hc = std::thread::hardware_concurrency();
+    return (int)std::max<unsigned>(1, std::min<unsigned>(16, hc ? hc : 8));
+  }());
+  return pool;
+}
+
 FqResult fq_extract(uint8_t *in, size_t len, bool eof, uint8_t *bases, uint64_t *ends,
                     uint64_t base_off, HostPool &pool, int fd, uint64_t file_off, FqScratch *scratch,
                     uint64_t max_rec) {
@@ -154,22 +177,37 @@ FqResult fq_extract(uint8_t *in, size_t len, bool eof, uint8_t *bases, uint64_t 
   FqScratch local;
   std::vector<std::vector<uint32_t>> &nl = (scratch ? scratch : &local)->nl;
   if (nl.size() < (size_t)pool.size()) nl.resize(pool.size());
+  std::vector<int> rd_err(T, 0);      // errno of a failed read (-1: the file ended early)
+  std::vector<uint64_t> rd_at(T, 0);  // file offset where it failed
   pool.run([&](int t) {
     if (t >= T) return;
     const size_t a = len * t / T, b = len * (t + 1) / T;
-    if (fd >= 0) {  // this thread's slice, from the page cache (a short read leaves zeros)
+    if (fd >= 0) {  // this thread's slice, from the page cache
       size_t g = 0;
       while (a + g < b) {
         const ssize_t r = pread(fd, in + a + g, b - a - g, (off_t)(file_off + a + g));
-        if (r <= 0) break;
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) {
+          rd_err[t] = r < 0 ? errno : -1;
+          rd_at[t] = file_off + a + g;
+          break;
+        }
         g += (size_t)r;
       }
-      if (a + g < b) memset(in + a + g, 0, b - a - g);
+      if (a + g < b) return;  // (reported below; nothing of this window is taken)
     }
     nl[t].clear();
     nl[t].reserve((b - a) / 48 + 64);
     find_newlines(in, a, b, nl[t]);
   });
+  for (int t = 0; t < T; ++t)
+    if (rd_err[t]) {
+      res.io_error = rd_err[t] > 0 ? std::string("read failed at byte ") + std::to_string(rd_at[t]) + ": " +
+                                         strerror(rd_err[t])
+                                   : "the file ended at byte " + std::to_string(rd_at[t]) +
+                                         " before its size while it was read";
+      return res;
+    }
   Lines L;
   L.nl = nl.data();
   L.T = T;

@@ -47,6 +47,7 @@ class HostPool {
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
   const std::function<void(int)> *fn_ = nullptr;
+  std::mutex run_mu_;
   std::atomic<uint64_t> gen_{0};
   std::atomic<int> pending_{0};
   std::atomic<bool> quit_{false};
@@ -59,7 +60,15 @@ struct FqResult {
   bool stop = false;      // a malformed record follows them: the stream ends
   bool blank = false;     // a blank line where a header is due follows them
   bool more = false;      // max_rec cut the window: records follow (call again from consumed)
+  // fd >= 0: a read of the window failed or the file ended before its size
+  // (nothing is taken: the caller fails with NK_E_IO instead of a silent stop)
+  std::string io_error;
 };
+
+// The process's one pool (at most 16 threads: a one-GPU box's CPU share),
+// shared by every handle's FASTQ ingest (a pool per handle multiplied the
+// spinning threads with the handles)
+HostPool &shared_host_pool();
 
 // Records a window of `len` input bytes can hold: len / 6 + 1 (a record has
 // at least 6 bytes: "@\n\n+\n\n").  A caller with less room for record ends
@@ -93,10 +102,12 @@ class HostFile {
   int open(const char *path, std::string &err);  // 0 or an NK_E_* code
   int fd() const { return fd_; }
   uint64_t size() const { return n_; }
+  const std::string &path() const { return path_; }
 
  private:
   int fd_ = -1;
   uint64_t n_ = 0;
+  std::string path_;
 };
 
 }  // namespace nk

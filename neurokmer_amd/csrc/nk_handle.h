@@ -169,7 +169,6 @@ struct nk_counter {
   // event of each buffer's last H2D, the parser threads
   PinnedBuf ing_he[3];
   hipEvent_t fq_ev[3] = {};
-  HostPool *fq_pool = nullptr;
   FqScratch fq_scratch;
   // LIF table cache key
   bool lif_valid = false;
@@ -191,6 +190,12 @@ struct nk_counter {
   DevBuf<unsigned long long> ovf;
   size_t ovf_zeroed = 0;  // entries known zero
   uint32_t pend_slices = 0;  // K1b partials not yet folded into cur (fused into LIF)
+  // K1b left to the next count's K1a (opts.defer_hist, k_part_fused): 0 none;
+  // 1 pending in the device's slot (nk_count.cpp: hist_*); 2 taken by another
+  // handle's fused count, whose end hist_ev marks
+  int hist_state = 0;
+  uint32_t hist_slices = 0;
+  hipEvent_t hist_ev = nullptr;
   bool cur_in_wire = false;  // nk_wire32 moved the currents into the caller's wire vector
   // multi-GPU export (nk_finalize_export -> nk_merge_export -> [nk_finalize_redo])
   DevBuf<unsigned long long> export_n;  // key counter of k_export_keys (kept zero between uses)
@@ -371,6 +376,14 @@ uint64_t arena_bytes(const nk_counter *c);
 int plan_count(nk_counter *c, uint64_t est_bases, uint64_t slack, uint64_t max_segs,
                       CountPlan &cp, ZeroList &z, bool keep_gen = false, int part_bits = 0);
 hipError_t gen_hist(nk_counter *c, const CountPlan &cp, bool defer_partials, hipStream_t s);
+// the deferred K1b (opts.defer_hist): hist_ready before anything reads this
+// handle's partials (runs it, or waits for the fused count that took it);
+// hist_arena before this handle's next count rewrites its records; hist_void
+// when a reset voids the partials; hist_forget when the handle is freed
+int hist_ready(nk_counter *c, hipStream_t s);
+int hist_arena(nk_counter *c, hipStream_t s);
+void hist_void(nk_counter *c);
+void hist_forget(nk_counter *c);
 uint32_t split_launches(uint64_t n_tiles);
 hipError_t split_pipelined(nk_counter *c, const CountPlan &cp, const KmerInput &in, uint32_t G,
                                   hipStream_t s);

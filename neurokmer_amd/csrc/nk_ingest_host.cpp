@@ -163,10 +163,6 @@ static int ingest_fastq_host(nk_counter *c, const HostFile &hf, bool *fallback, 
   }
   if (!c->fq_ev[0])
     for (hipEvent_t &e : c->fq_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  if (!c->fq_pool) {  // the box's CPU share for one GPU (at most 16 threads)
-    const unsigned hc = std::thread::hardware_concurrency();
-    c->fq_pool = new HostPool((int)std::max<unsigned>(1, std::min<unsigned>(16, hc ? hc : 8)));
-  }
   hipStream_t cs = c->ing_cs;
   // every exit leaves no copy in flight from the pinned buffers
   struct Drain {
@@ -193,10 +189,11 @@ static int ingest_fastq_host(nk_counter *c, const HostFile &hf, bool *fallback, 
     const clk::time_point t0 = clk::now();
     if (used[b]) HIPCHK(hipEventSynchronize(c->fq_ev[b]));
     const FqResult r = fq_extract(rbuf.data(), len, eof, c->ing_hb[b].p,
-                                  reinterpret_cast<uint64_t *>(c->ing_he[b].p), data_end, *c->fq_pool, fd,
+                                  reinterpret_cast<uint64_t *>(c->ing_he[b].p), data_end, shared_host_pool(), fd,
                                   pos, &c->fq_scratch, max_rec_for(len));
     if (prof) t_parse += since(t0);
     ++n_win;
+    if (!r.io_error.empty()) return fail(NK_E_IO, "%s: %s", hf.path().c_str(), r.io_error.c_str());
     if (!r.n_rec && !r.stop && !r.blank && !eof) {
       // a record longer than the window: widen it (no copy may read the buffers)
       if (win >= ((size_t)1 << 31)) return fail(NK_E_PARSE, "a FASTQ record longer than 2 GiB");
@@ -213,6 +210,8 @@ static int ingest_fastq_host(nk_counter *c, const HostFile &hf, bool *fallback, 
     }
     const clk::time_point t1 = clk::now();
     const bool last = r.stop || (eof && !r.more);
+    if (r.stop)  // (src/utils.rs:17-19: the reference warns and ends the stream there)
+      warn_malformed(hf.path().c_str(), n_rec + r.n_rec, "a FASTQ record is malformed or cut off");
     if (n_rec + r.n_rec + 1 > c->in_offs.n) {  // grow the offsets: wait, copy, free
       HIPCHK(hipStreamSynchronize(cs));
       HIPCHK(hipStreamSynchronize(s));
@@ -292,6 +291,7 @@ int ingest_file(nk_counter *c, const char *path, bool *fallback) {
     if ((rc = hb[i].ensure(chunk))) return rc;
   size_t have = src.read(hb[0].p, chunk);
   bool eof = have < chunk;
+  if (src.failed()) return fail(NK_E_IO, "%s: %s", path, src.why().c_str());
   if (!have) return fail(NK_E_PARSE, "empty file");
   const bool fastq = hb[0].p[0] == '@';
   if (hb[0].p[0] != '>' && !fastq)
@@ -376,6 +376,7 @@ int ingest_file(nk_counter *c, const char *path, bool *fallback) {
       const clk::time_point t2 = clk::now();
       got = next.get();
       if (prof) t_read += since(t2);
+      if (src.failed()) return fail(NK_E_IO, "%s: %s", path, src.why().c_str());
       if ((rc = upload(db ^ 1, hb[(ci + 1) % 3].p, got))) return rc;
       if (got == chunk) prefetch((int)((ci + 2) % 3));  // chunk ci - 1's buffer: its H2D is done
     }
@@ -416,6 +417,11 @@ int ingest_file(nk_counter *c, const char *path, bool *fallback) {
     // the carry goes in front of the next chunk's bytes (they sit at + room);
     // enqueued before this chunk's count so the next H2D into this buffer can start
     const bool last = eof || st.stop;
+    if (st.stop)  // (src/utils.rs:17-19: the reference warns and ends the stream there)
+      warn_malformed(path, st.n_rec, src.damage().empty() ? "a FASTQ record is malformed or cut off"
+                                                          : src.damage().c_str());
+    else if (eof && !src.damage().empty())  // (a FASTA record cut by a damaged stream)
+      warn_malformed(path, st.n_rec ? st.n_rec - 1 : 0, src.damage().c_str());
     size_t nc = 0;
     if (!last) {
       const clk::time_point t3 = clk::now();

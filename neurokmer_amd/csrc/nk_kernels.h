@@ -401,6 +401,23 @@ hipError_t launch_part_keys(const uint64_t *keys, const unsigned long long *n_ke
 // kpn[i] = cur[i] + sum of `slices` partials (0: none); cur[i] = 0 after
 hipError_t launch_kpn_fold(const uint32_t *partials, uint32_t slices, uint64_t pool,
                            unsigned long long *cur, uint32_t *kpn, hipStream_t s);
+// K1b of a previous Part count done inside the next count's K1a (k_part_fused):
+// its records (off / fill / cap / sub_shift of that count's PartArgs) into
+// `slices` partials per bucket, as launch_bucket_hist writes them
+constexpr uint32_t kFusePasses = 3;  // a bucket's 32768 bins in thirds (K1a's LDS holds 10923)
+struct HistJob {
+  const uint16_t *off = nullptr;
+  const unsigned long long *fill = nullptr;
+  uint64_t cap = 0;
+  uint32_t n_buckets = 0, sub_shift = 0, slices = 0;
+  uint32_t *partials = nullptr;
+  uint64_t pool = 0;
+  uint32_t n_items = 0;  // n_buckets * slices * kFusePasses (0: no job)
+  uint32_t n_host = 0;   // workgroups [0, n_host) take the items, spread evenly
+};
+bool part_fused_ok(const PartArgs &pa);  // a count whose K1a has the fused form (and whose K1b it can take)
+hipError_t launch_part_fused(const KmerInput &in, int k, int canonical, uint64_t pool,
+                             const PartArgs &pa, const HistJob &hj, hipStream_t s);
 hipError_t launch_bucket_hist(const PartArgs &pa, uint64_t pool, uint32_t slices,
                               uint32_t *partials, hipStream_t s);
 hipError_t launch_partials_add(const uint32_t *partials, uint32_t slices, uint64_t pool,

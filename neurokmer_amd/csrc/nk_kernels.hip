@@ -540,19 +540,32 @@ constexpr uint32_t kSpanTail = 2048;  // last-dispatched workgroups that stamp t
 // the staged tile at store time and written beside its bin offset (pa.key);
 // the position array is not written.  Records past a full region are counted
 // directly as always (pa.currents, when set) and their keys spilled.
-template <bool CANON, int MAXB, bool K16 = false, bool KEYS = false>
-__global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMod fm, PartArgs pa) {
+// LDS of one K1a tile (k_part; in a union with the fused histogram item, k_part_fused)
+template <int MAXB, bool RAW>
+struct PartLds {
+  using S = PartShape<MAXB>;
+  TileLds<kPartTile, RAW> L;
+  uint32_t s_cnt[MAXB + 1];  // + a dummy bucket for non-k-mer positions
+  uint32_t s_start[MAXB + 1];
+  uint32_t s_base[MAXB];
+  uint32_t s_fit[MAXB];
+  __align__(16) uint32_t s_sorted[S::kSortSlots];
+  typename S::GMap s_gmap[S::kGroups];  // store group -> bucket
+};
+
+template <bool CANON, int MAXB, bool K16, bool KEYS>
+__device__ __forceinline__ void part_tile(const KmerInput &in, int k, const FastMod &fm,
+                                          const PartArgs &pa, PartLds<MAXB, !CANON> &sm) {
   using S = PartShape<MAXB>;
   constexpr int kSortSlots = S::kSortSlots;
-  constexpr int kGroups = S::kGroups;
   constexpr int kGroupIters = S::kGroupIters;
-  __shared__ TileLds<kPartTile, !CANON> L;
-  __shared__ uint32_t s_cnt[MAXB + 1];  // + a dummy bucket for non-k-mer positions
-  __shared__ uint32_t s_start[MAXB + 1];
-  __shared__ uint32_t s_base[MAXB];
-  __shared__ uint32_t s_fit[MAXB];
-  __shared__ __align__(16) uint32_t s_sorted[kSortSlots];
-  __shared__ typename S::GMap s_gmap[kGroups];  // store group -> bucket
+  TileLds<kPartTile, !CANON> &L = sm.L;
+  uint32_t(&s_cnt)[MAXB + 1] = sm.s_cnt;
+  uint32_t(&s_start)[MAXB + 1] = sm.s_start;
+  uint32_t(&s_base)[MAXB] = sm.s_base;
+  uint32_t(&s_fit)[MAXB] = sm.s_fit;
+  uint32_t(&s_sorted)[kSortSlots] = sm.s_sorted;
+  typename S::GMap(&s_gmap)[S::kGroups] = sm.s_gmap;
 
   const int tid = threadIdx.x;
   const uint64_t tile = in.tile_base + blockIdx.x;
@@ -767,7 +780,11 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
       typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
       // (plain stores instead wrote as much at pool 16 M, also with the
       // sub-regions per XCD: profiles/r05_l, r05_p)
+#if defined(NK_K1A_OFF_PLAIN)  // A/B: the offsets K1b reads next kept in the caches (MALL)
+      *reinterpret_cast<u32x4 *>(pa.off + dst) = u32x4{off.x, off.y, off.z, off.w};
+#else
       __builtin_nontemporal_store(u32x4{off.x, off.y, off.z, off.w}, reinterpret_cast<u32x4 *>(pa.off + dst));
+#endif
       if (!KEYS)
         __builtin_nontemporal_store(u32x4{pos.x, pos.y, pos.z, pos.w}, reinterpret_cast<u32x4 *>(pa.pos + dst));
       if constexpr (KEYS) {
@@ -816,6 +833,12 @@ __global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMo
   }
   NK_STAMP(7);
 #endif
+}
+
+template <bool CANON, int MAXB, bool K16 = false, bool KEYS = false>
+__global__ __launch_bounds__(kPartBlock) void k_part(KmerInput in, int k, FastMod fm, PartArgs pa) {
+  __shared__ PartLds<MAXB, !CANON> sm;
+  part_tile<CANON, MAXB, K16, KEYS>(in, k, fm, pa, sm);
 }
 
 // Spikes of a neuron in the derived state: the LIF from (v, r) = (0, 0) of
@@ -1025,6 +1048,133 @@ __global__ __launch_bounds__(kHistBlock) void k_bucket_hist(PartArgs pa, uint64_
   }
   uint32_t *dst = partials + (uint64_t)r * pool + nb0;
   for (uint32_t t = threadIdx.x; t < nbins; t += kHistBlock) dst[t] = h[t];
+}
+
+// ---------------------------------------------------------------------------
+// K1a + K1b fused across batches (k_part_fused, round 6).  K1a is bound by its
+// SipHash instructions with HBM ~80 % idle; K1b is bound by HBM and LDS
+// atomics.  So the count of batch i+1 also histograms batch i's records: each
+// workgroup hashes its tile (part_tile) and some also take an item of the
+// previous batch's K1b (HistJob).  K1a's 51.5 KB of LDS (three workgroups per
+// CU) holds no 32768-bin u32 histogram, so an item is one (bucket, slice,
+// third of the bins): it reads the slice's records once and adds each record
+// at byte address off * 4 - third * R * 4 of the union.  A record of another
+// third lands past the histogram: below 0 (wrapped) or past the workgroup's
+// LDS allocation the hardware drops the access (tools/oobtest.hip), and between
+// R words and the allocation's end is unread space of the same union -- so no
+// compare, no branch: one ds_add per record per third.  The partials are
+// k_bucket_hist's (slice r of bucket b at partials[r * pool + b * 32768 ...]).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kFuseRange = (kBinsPerBucket + kFusePasses - 1) / kFusePasses;  // bins per third
+static_assert(kFuseRange * 4 <= sizeof(PartLds<256, false>), "a third of a bucket fits the K1a union");
+// a pad record (0xFFFF) lands past the allocation in every third
+static_assert(4 * 0xFFFFull - 4ull * kFuseRange * (kFusePasses - 1) >= 64 * 1024,
+              "pad records stay past the allocation");
+#ifndef NK_FUSE_KU
+#define NK_FUSE_KU 2  // 16-B loads per lane per round (registers: the kernel keeps 6 waves per SIMD)
+#endif
+
+// item -> (third, bucket, slice); the three thirds of one slice are
+// consecutive items (workgroups close in time: the slice's second and third
+// reads come from the caches)
+__device__ __forceinline__ void fused_hist_item(const HistJob &hj, uint32_t item, uint32_t *h) {
+  const uint32_t third = item % kFusePasses;
+  const uint32_t rest = item / kFusePasses;
+  const uint32_t b = rest % hj.n_buckets, r = rest / hj.n_buckets;
+  const uint64_t nb0 = (uint64_t)b << kBinBits;
+  const uint64_t nbins = hj.pool - nb0 < (uint64_t)kBinsPerBucket ? hj.pool - nb0 : kBinsPerBucket;
+  const uint64_t t0 = (uint64_t)third * kFuseRange;
+  if (t0 >= nbins) return;  // (uniform)
+  const uint32_t cnt = (uint32_t)(nbins - t0 < kFuseRange ? nbins - t0 : kFuseRange);
+  const uint32_t base = (uint32_t)t0 * 4u;
+  const int tid = threadIdx.x;
+  __syncthreads();  // (the LDS: the tile's stores or the previous item read it)
+  for (uint32_t t = tid; t < kFuseRange; t += kPartBlock) h[t] = 0;
+  __syncthreads();
+  char *hb = reinterpret_cast<char *>(h);
+  auto add = [&](uint32_t off) { atomicAdd(reinterpret_cast<uint32_t *>(hb + ((off << 2) - base)), 1u); };
+  // this slice's share [lo, hi) of the bucket's records, sub-region by sub-region
+  const uint32_t nsub = 1u << hj.sub_shift;
+  uint64_t n = 0;
+  for (uint32_t x = 0; x < nsub; ++x) {
+    const uint64_t f = hj.fill[((uint64_t)b << hj.sub_shift) | x] & ((1ull << 40) - 1);
+    n += f < hj.cap ? f : hj.cap;
+  }
+  const uint64_t lo_all = n * r / hj.slices, hi_all = n * (r + 1) / hj.slices;
+  uint64_t c0 = 0;
+  for (uint32_t x = 0; x < nsub; ++x) {
+    const uint64_t vb = ((uint64_t)b << hj.sub_shift) | x;
+    uint64_t nv = hj.fill[vb] & ((1ull << 40) - 1);
+    if (nv > hj.cap) nv = hj.cap;
+    const uint64_t a = lo_all > c0 ? lo_all : c0, z = hi_all < c0 + nv ? hi_all : c0 + nv;
+    const uint64_t lo = a - c0, hi = z > a ? z - c0 : lo;
+    c0 += nv;
+    if (lo >= hi) continue;  // (uniform)
+    const uint16_t *src = hj.off + vb * hj.cap;
+    uint64_t i = lo;
+    for (; i < hi && (i & 7); ++i)
+      if (tid == 0) add(src[i]);
+    const uint64_t hi8 = i + ((hi - i) & ~7ull);
+    constexpr uint64_t step = 8ull * kPartBlock;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    // NK_FUSE_KU 16-B loads per lane per round, the next round's in flight
+    // while this round's records are added (as k_bucket_hist)
+    uint64_t j = i + 8ull * tid;
+    if (j < hi8) {
+      auto load_round = [&](uint64_t jb, u32x4 *v) {
+#pragma unroll
+        for (int t = 0; t < NK_FUSE_KU; ++t) {
+          const uint64_t jt = jb + (uint64_t)t * step;
+          v[t] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src + (jt < hi8 ? jt : i)));
+        }
+      };
+      u32x4 cur[NK_FUSE_KU];
+      load_round(j, cur);
+      for (;;) {
+        const uint64_t jn = j + (uint64_t)NK_FUSE_KU * step;
+        const bool more = jn < hi8;
+        u32x4 nxt[NK_FUSE_KU];
+        load_round(more ? jn : j, nxt);
+#pragma unroll
+        for (int t = 0; t < NK_FUSE_KU; ++t)
+          if (j + (uint64_t)t * step < hi8) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              add(cur[t][e] & 0xFFFFu);
+              add(cur[t][e] >> 16);
+            }
+          }
+        if (!more) break;
+        j = jn;
+#pragma unroll
+        for (int t = 0; t < NK_FUSE_KU; ++t) cur[t] = nxt[t];
+      }
+    }
+    for (uint64_t q = hi8 + tid; q < hi; q += kPartBlock) add(src[q]);
+  }
+  __syncthreads();
+  uint32_t *dst = hj.partials + (uint64_t)r * hj.pool + nb0 + t0;
+  for (uint32_t t = tid; t < cnt; t += kPartBlock) dst[t] = h[t];
+}
+
+// K1a of this batch + K1b items of the previous one (workgroups [0, n_host)
+// take items [ceil(w * n_items / n_host), ceil((w + 1) * n_items / n_host)):
+// spread over the first part of the grid, so no item is in the tail)
+template <bool CANON, bool K16>
+__global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(CANON ? 6 : 4))) void k_part_fused(
+    KmerInput in, int k, FastMod fm, PartArgs pa, HistJob hj) {
+  // the only LDS object of the kernel: a dropped or unread third-of-bucket
+  // access can touch nothing else
+  __shared__ union FU {
+    PartLds<256, !CANON> a;
+    uint32_t h[sizeof(PartLds<256, !CANON>) / 4];
+  } sm;
+  part_tile<CANON, 256, K16, false>(in, k, fm, pa, sm.a);
+  const uint32_t w = blockIdx.x;
+  if (w >= hj.n_host) return;
+  const uint32_t i0 = (uint32_t)(((uint64_t)w * hj.n_items + hj.n_host - 1) / hj.n_host);
+  const uint32_t i1 = (uint32_t)(((uint64_t)(w + 1) * hj.n_items + hj.n_host - 1) / hj.n_host);
+  for (uint32_t it = i0; it < i1; ++it) fused_hist_item(hj, it, sm.h);
 }
 
 __global__ void k_partials_add(const uint32_t *__restrict__ partials, uint32_t slices,
@@ -2547,6 +2697,25 @@ hipError_t launch_part(const KmerInput &in, int k, int canonical, uint64_t pool,
     if (canonical) hipLaunchKernelGGL((k_part<true, kMaxBuckets>), g, bl, dyn, s, in, k, fm, pa);
     else hipLaunchKernelGGL((k_part<false, kMaxBuckets>), g, bl, dyn, s, in, k, fm, pa);
   }
+  return hipGetLastError();
+}
+
+bool part_fused_ok(const PartArgs &pa) {
+  return pa.n_buckets <= 256 && !pa.key && pa.bin_bits == (uint32_t)kBinBits;
+}
+
+hipError_t launch_part_fused(const KmerInput &in, int k, int canonical, uint64_t pool,
+                             const PartArgs &pa, const HistJob &hj, hipStream_t s) {
+  if (!in.n_tiles) return hipSuccess;
+  if (!part_fused_ok(pa) || (hj.n_items && (hj.n_host == 0 || hj.n_host > in.n_tiles || !hj.partials ||
+                                             !hj.off || !hj.fill || !hj.slices ||
+                                             hj.n_buckets > (uint32_t)kMaxBuckets)))
+    return hipErrorInvalidValue;
+  const FastMod fm = make_fastmod(pool);
+  const dim3 g((unsigned)in.n_tiles), bl(kPartBlock);
+  if (canonical && k >= 16) hipLaunchKernelGGL((k_part_fused<true, true>), g, bl, 0, s, in, k, fm, pa, hj);
+  else if (canonical) hipLaunchKernelGGL((k_part_fused<true, false>), g, bl, 0, s, in, k, fm, pa, hj);
+  else hipLaunchKernelGGL((k_part_fused<false, false>), g, bl, 0, s, in, k, fm, pa, hj);
   return hipGetLastError();
 }
 

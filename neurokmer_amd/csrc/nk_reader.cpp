@@ -6,7 +6,11 @@
 #include <unistd.h>
 #include <zlib.h>
 
+#include <errno.h>
+#include <string.h>
+
 #include <algorithm>
+#include <atomic>
 #include <thread>
 #include <vector>
 
@@ -48,7 +52,13 @@ size_t ChunkSource::read(uint8_t *dst, size_t want) {
     while (got < want) {
       const int n = gzread((gzFile)gzf_, dst + got,
                            (unsigned)std::min<size_t>(want - got, (size_t)1 << 30));
-      if (n <= 0) break;
+      if (n <= 0) {
+        int zerr = 0;
+        const char *m = gzerror((gzFile)gzf_, &zerr);
+        if (zerr == Z_ERRNO) why_ = std::string("read failed: ") + strerror(errno);
+        else if (zerr != Z_OK) damage_ = std::string("gzip: ") + (m ? m : "?");
+        break;
+      }
       got += (size_t)n;
     }
     return got;
@@ -64,11 +74,14 @@ size_t ChunkSource::read(uint8_t *dst, size_t want) {
   }();
   const int nt = (int)std::min<size_t>((size_t)kMaxThreads, (want + part - 1) / part);
   std::vector<size_t> got(nt > 0 ? nt : 1, 0);
+  std::atomic<int> err_no{0};
   auto work = [&](int t) {
     const size_t lo = want * t / nt, hi = want * (t + 1) / nt;
     size_t g = 0;
     while (lo + g < hi) {
       const ssize_t n = pread(fd_, dst + lo + g, hi - lo - g, (off_t)(off_ + lo + g));
+      if (n < 0 && errno == EINTR) continue;
+      if (n < 0) err_no = errno;
       if (n <= 0) break;
       g += (size_t)n;
     }
@@ -87,6 +100,12 @@ size_t ChunkSource::read(uint8_t *dst, size_t want) {
     total += got[t];
     if (got[t] < want * (t + 1) / nt - want * t / nt) break;
   }
+  // the file's size is known: fewer bytes than it holds is a failure, not its end
+  if (err_no.load())
+    why_ = std::string("read failed at byte ") + std::to_string(off_ + total) + ": " + strerror(err_no.load());
+  else if (total < want && off_ + total < fsize_)
+    why_ = "the file ended at byte " + std::to_string(off_ + total) + " of " + std::to_string(fsize_) +
+           " while it was read";
   off_ += total;
   return total;
 }

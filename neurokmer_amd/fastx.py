@@ -9,7 +9,14 @@ file or an unknown first byte, like parse_fastx_file.
 from __future__ import annotations
 
 import gzip
+import sys
 from typing import Iterator
+
+
+def _warn(path: str, record: int, why: str) -> None:
+    """src/utils.rs:17-19's `warn!("Skipping malformed record: {}", e)` (stderr)."""
+    print(f"[WARN  neurokmer] Skipping malformed record: {why} (record {record} of {path}); "
+          "the input ends here", file=sys.stderr)
 
 
 def _open(path: str):
@@ -43,6 +50,7 @@ def stream_sequences(path: str) -> Iterator[bytes]:
                 yield bytes(seq)
             else:
                 header_pending = True
+                n = 0
                 while True:
                     if not header_pending:
                         line = f.readline()
@@ -51,17 +59,21 @@ def stream_sequences(path: str) -> Iterator[bytes]:
                         if not line:
                             return
                         if not line.startswith(b"@"):
+                            _warn(path, n, "expected '@' at the start of a FASTQ record")
                             return
                     header_pending = False
                     seq = f.readline()
                     plus = f.readline()
                     qual = f.readline()
                     if not seq or not plus.startswith(b"+") or not qual:
+                        _warn(path, n, "a FASTQ record is malformed or cut off")
                         return
                     seq = seq.rstrip(b"\n").rstrip(b"\r")
                     qual = qual.rstrip(b"\n").rstrip(b"\r")
                     if len(qual) != len(seq):
+                        _warn(path, n, "quality and sequence lengths differ")
                         return
+                    n += 1
                     yield seq
 
     return gen()

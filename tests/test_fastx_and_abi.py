@@ -220,3 +220,44 @@ def test_mapped_fastq_large_synthetic(tmp_path):
         rc, recs, trunc, fb = mapped(p, window, threads)
         assert (rc, fb, trunc) == (0, False, False)
         assert recs == want
+
+
+# --- a stopped input is reported ---------------------------
+# The reference warns when the stream stops at a malformed record
+# (`warn!("Skipping malformed record: {}", e)`, src/utils.rs:17-19); a read that
+# fails (or a file that ends before its size while it is read) is an I/O error,
+# not a quiet end of the input.
+
+def _dump(*args):
+    r = subprocess.run([DUMP, *map(str, args)], capture_output=True, check=True)
+    return json.loads(r.stdout), r.stderr.decode()
+
+
+def test_truncated_fastq_warns_once_and_keeps_earlier_records(tmp_path):
+    p = tmp_path / "cut.fq"
+    p.write_bytes(b"@a\nACGT\n+\nIIII\n@b\nACGTAC\n+\nIII")  # record b cut inside its quality
+    for args in ((p,), (p, "--mapped", 4096, 2)):
+        d, err = _dump(*args)
+        assert d["rc"] == 0 and d["truncated"] and d["records"] == ["41434754"]
+        lines = [ln for ln in err.splitlines() if "Skipping malformed record" in ln]
+        assert len(lines) == 1 and "record 1 of" in lines[0] and str(p) in lines[0]
+
+
+def test_file_ending_early_is_an_io_error(tmp_path):
+    p = tmp_path / "shrinks.fq"
+    bases, offs = synth.make_reads(2000, 150, seed=5)
+    synth.write_fastq(str(p), bases, offs)
+    d, err = _dump(p, "--mapped", 1 << 16, 4, "--shrink", 100_000)
+    assert d["rc"] == _lib.NK_E_IO and "ended at byte" in d["err"]
+    assert "Skipping malformed record" not in err
+
+
+def test_cut_off_gzip_warns_and_stops(tmp_path):
+    p = tmp_path / "cut.fq.gz"
+    raw = b"".join(b"@r%d\nACGTACGT\n+\nIIIIIIII\n" % i for i in range(50_000))
+    z = gzip.compress(raw)
+    p.write_bytes(z[: len(z) // 2])
+    d, err = _dump(p)
+    assert d["rc"] == 0 and d["truncated"] and 0 < len(d["records"]) < 50_000
+    assert all(r == "4143475441434754" for r in d["records"])
+    assert "gzip" in err and "Skipping malformed record" in err
