@@ -116,6 +116,115 @@ def load_side_pmc(workload: str, n_bases: int, k: int, pool: int, width: int) ->
     return d
 
 
+class TorchRanks:
+    """The N-rank job's host-side collectives: torch.distributed (gloo for
+    bootstrap and timing; the data path uses the library's communicator)."""
+
+    def __init__(self, on: bool):
+        self.on = on
+
+    def barrier(self):
+        if self.on:
+            import torch.distributed as dist
+            dist.barrier()
+
+    def max(self, x, dev):
+        """max over ranks of a host number"""
+        if not self.on:
+            return x
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([x], dtype=torch.float64 if isinstance(x, float) else torch.int64,
+                         device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return type(x)(t.item())
+
+    def gather_state(self, ctr):
+        from neurokmer_amd import dist as nkdist
+        return nkdist.gather_state(ctr)
+
+    def close(self):
+        if self.on:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+
+
+class LoopRanks:
+    """--loopback N: the N-rank code path rehearsed on ONE
+    GPU, every rank a host thread of this process with its own handles and
+    streams, the library's collectives over its loopback transport
+    (nk_loop_group_new: device copies + a sum kernel between host barriers,
+    what RCCL does over xGMI).  Host-side barrier / max / state gather through
+    shared memory.  Not a scaling figure: the ranks share one GPU."""
+
+    def __init__(self, world: int):
+        import threading
+        self.world = world
+        self.bar = threading.Barrier(world)
+        self.slots = [None] * world
+        self.local = threading.local()
+
+    def barrier(self):
+        self.bar.wait(timeout=600)
+
+    def max(self, x, dev=None):
+        self.slots[self.local.rank] = x
+        self.bar.wait(timeout=600)
+        m = max(self.slots)
+        self.bar.wait(timeout=600)
+        return type(x)(m)
+
+    def gather_state(self, ctr):
+        from neurokmer_amd import dist as nkdist
+        r, pool = self.local.rank, ctr.pool_size
+        lo, hi, _ = nkdist.slice_bounds(pool, self.world, r)
+        self.slots[r] = {n: a[lo:hi].copy() for n, a in (
+            ("currents", ctr.currents()), ("spike_counts", ctr.spike_counts()),
+            ("voltages", ctr.voltages()), ("refractory", ctr.refractory()))}
+        self.bar.wait(timeout=600)
+        out = {n: np.concatenate([self.slots[q][n] for q in range(self.world)])
+               for n in self.slots[0]}
+        self.bar.wait(timeout=600)
+        return out
+
+    def close(self):
+        pass
+
+
+def loopback_main(args) -> int:
+    """--loopback N: rank_main on N threads sharing one loopback group."""
+    import copy
+    import threading
+    import traceback
+    from neurokmer_amd import dist as nkdist
+    n = args.loopback
+    ctx = LoopRanks(n)
+    grp = nkdist.LoopbackGroup(n)
+    comms = [nkdist.Comm.loopback(grp, r, 0) for r in range(n)]
+    rcs, errs = [1] * n, [None] * n
+
+    def run(r):
+        ctx.local.rank = r
+        try:
+            rcs[r] = rank_main(copy.copy(args), n, r, 0, ctx, comms[r])
+        except Exception:
+            errs[r] = traceback.format_exc()
+            ctx.bar.abort()
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(n)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for e in errs:
+        if e:
+            print(e, file=sys.stderr)
+    for c in comms:
+        c.close()
+    grp.close()
+    return 0 if all(rc == 0 for rc in rcs) and not any(errs) else 1
+
+
 def spawn_ranks(n: int) -> int:
     """Start n ranks of this script (torch.distributed.run, 127.0.0.1) and
     return their exit code.  Runs before any GPU call in this process."""
@@ -233,13 +342,29 @@ def main() -> int:
                          "kernel (nk_opts.defer_hist, k_part_fused); auto: on with >= 3 batches "
                          "in flight on one GPU.  Off by default: the fused kernel leaves the "
                          "finishes no window (0.56-0.57 vs 0.50-0.51 ms per step, profiles/r06_fuse)")
+    ap.add_argument("--loopback", type=int, default=0,
+                    help="N > 1: rehearse the N-rank path on ONE GPU, ranks as threads over the "
+                         "library's loopback transport (not a scaling figure)")
     args = ap.parse_args()
 
+    if args.loopback > 1:
+        if args.workload not in ("config2", "config5"):
+            print("bench.py: --loopback rehearses configs 2 and 5", file=sys.stderr)
+            return 2
+        args.gpus = args.loopback
+        return loopback_main(args)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return spawn_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    return rank_main(args, world, rank, local, None, None)
+
+
+def rank_main(args, world: int, rank: int, local: int, ctx, lcomm) -> int:
+    """One rank's bench (ctx None: this process is the rank, torch.distributed
+    between ranks; else a LoopRanks thread with its loopback communicator)."""
+    loop = ctx is not None
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch with "
               f"torchrun --nproc-per-node {args.gpus} (or no torchrun)", file=sys.stderr)
@@ -258,7 +383,7 @@ def main() -> int:
         args.k, args.pool, args.kmer_width = 63, 256_000_000, 128
     pool, k = args.pool, args.k
     ndev = torch.cuda.device_count()  # counts devices without initialising them
-    shared = world > ndev  # rehearsal: ranks share devices
+    shared = world > ndev and not loop  # rehearsal: ranks share devices (gloo)
     dev_idx = local % max(ndev, 1)
     dist_on = world > 1 or args.force_dist
     # the device collectives: the library's own RCCL communicator (the whole
@@ -287,7 +412,7 @@ def main() -> int:
             args.inflight = 2 if lib_comm else 1
         else:
             args.inflight = 3
-    if dist_on:
+    if dist_on and not loop:
         if "RANK" not in os.environ:  # --force-dist without a launcher: a 1-rank group
             with socket.socket() as sk:
                 sk.bind(("127.0.0.1", 0))
@@ -301,11 +426,16 @@ def main() -> int:
             os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")  # one node, 127.0.0.1
             dist.init_process_group(backend)
     dev = torch.device("cuda", dev_idx)
+    if loop:
+        torch.cuda.set_device(dev_idx)
+    else:
+        ctx = TorchRanks(dist_on)
 
     from neurokmer_amd import SpikingKmerCounter, synth
     from neurokmer_amd import dist as nkdist
     from neurokmer_amd.counter import diag_hash_ms
-    comm = nkdist.Comm(device=dev_idx) if (lib_comm or (dist_on and args.nk_comm)) else None
+    comm = lcomm if loop else \
+        (nkdist.Comm(device=dev_idx) if (lib_comm or (dist_on and args.nk_comm)) else None)
 
     # ---- this rank's input (resident in HBM) -------------------------------
     bases = None  # host copy (host-generated inputs only)
@@ -478,9 +608,7 @@ def main() -> int:
     if args.settle > 0:
         settle = min(int(args.settle / max(per, 1e-4)) + 1, 5000)
         if dist_on:
-            t = torch.tensor([settle], dtype=torch.int64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            settle = int(t.item())
+            settle = ctx.max(settle, dev)
         run(settle, args.inflight)
         torch.cuda.synchronize()
     # timed steps record no events at all (stage_timing 3); K1a's duration
@@ -496,19 +624,17 @@ def main() -> int:
 
     def timed(n, inflight, marks):
         if dist_on:
-            dist.barrier()
+            ctx.barrier()
         torch.cuda.synchronize()
         t_a = time.perf_counter()
         run(n, inflight, marks)
         torch.cuda.synchronize()
         if dist_on:
-            dist.barrier()
+            ctx.barrier()
         torch.cuda.synchronize()
         d = time.perf_counter() - t_a
         if dist_on:
-            t = torch.tensor([d], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            d = float(t.item())
+            d = ctx.max(d, dev)
         return t_a, d
 
     marks = []
@@ -563,8 +689,8 @@ def main() -> int:
     if world > 1 and not args.no_parity_ranks:
         log("parity_ranks: the union of every rank's input on rank 0's GPU")
         pr = parity_ranks(args, ctr, world, rank, dev_idx, nkdist, SpikingKmerCounter, synth,
-                          total_kmers)
-        dist.barrier()
+                          total_kmers, ctx)
+        ctx.barrier()
 
     if rank == 0:
         ms_step = dt / args.steps * 1e3
@@ -619,6 +745,7 @@ def main() -> int:
             "ms_per_step": round(ms_step, 4),
             "inflight": args.inflight,
             "defer_hist": defer_hist,
+            "rehearsal": bool(loop or shared),
             "ms_per_step_one_in_flight": round(dt1 / args.steps * 1e3, 4),
             "ms_per_step_state_written": (round(dt_settle / args.steps * 1e3, 4)
                                           if dt_settle is not None else None),
@@ -636,12 +763,17 @@ def main() -> int:
             "config": {"workload": workload, "k": k, "kmer_width": args.kmer_width,
                        "pool_size": pool, "bases_rank0": int(n_bases), "records_rank0": n_recs,
                        "kmers_rank0": nk_rank, "kmers_total": total_kmers,
-                       "parallelism": f"dp{world}" + (f" (rehearsal: {world} ranks on {ndev} GPU, "
-                                                      f"{backend})" if shared else ""),
+                       "parallelism": f"dp{world}" + (
+                           f" (REHEARSAL, not a scaling figure: {world} ranks as threads of one "
+                           f"process on 1 GPU, the library's loopback transport)" if loop else
+                           f" (rehearsal: {world} ranks on {ndev} GPU, {backend})" if shared else ""),
                        "finish": args.finish if dist_on else None,
-                       "collectives": ((f"in-library RCCL communicator ("
-                                        f"{'nk_finalize_sliced_dist' if args.finish == 'sliced' else 'nk_finalize_dist'}); "
-                                        f"torch.distributed {backend} for bootstrap and timing")
+                       "collectives": ((f"in-library communicator ("
+                                        f"{'nk_finalize_sliced_dist' if args.finish == 'sliced' else 'nk_finalize_dist'})"
+                                        + (" over the loopback transport; host barrier/max between "
+                                           "threads" if loop else
+                                           f" over RCCL; torch.distributed {backend} for bootstrap "
+                                           "and timing"))
                                        if comm is not None
                                        else (f"torch.distributed {backend} from Python" if dist_on
                                              else None))},
@@ -690,15 +822,17 @@ def main() -> int:
                                               dev_idx))
         print(json.dumps(out), flush=True)
     for c in ctrs:
+        if comm is not None:
+            comm.forget(c)
         c.close()
-    if comm is not None:
+    if comm is not None and not loop:
         comm.close()
-    if dist_on:
-        dist.destroy_process_group()
+    if not loop:
+        ctx.close()
     return 0
 
 
-def parity_ranks(args, ctr, world, rank, dev_idx, nkdist, Counter, synth, total_kmers):
+def parity_ranks(args, ctr, world, rank, dev_idx, nkdist, Counter, synth, total_kmers, ctx):
     """N > 1 (collective; the result on rank 0): rank 0 regenerates EVERY rank's
     input, counts their union in ONE process call on its own GPU, and compares
     the N-rank step's final state with it bit for bit.  The reference sums the
@@ -706,7 +840,7 @@ def parity_ranks(args, ctr, world, rank, dev_idx, nkdist, Counter, synth, total_
     records is the N-rank answer (bit-identical currents at 1,
     2, 4 and 8 GPUs).  Pool-sliced state (config5) is gathered first."""
     import torch
-    st = nkdist.gather_state(ctr) if args.finish == "sliced" else None
+    st = ctx.gather_state(ctr) if args.finish == "sliced" else None
     if rank != 0:
         return None
     k, pool = args.k, args.pool

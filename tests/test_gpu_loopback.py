@@ -104,7 +104,8 @@ def _assert_same(a, b, lo=0, hi=None):
 
 
 @pytest.mark.parametrize("world,wire,cap", [(2, "u32", 4096), (3, "u64", 4096), (4, "u32", 4),
-                                            (2, "u64", 1)])
+                                            (2, "u64", 1),
+                                            (8, "u32", 4096), (8, "u32", 4)])  # the 8-GPU node's world
 def test_loopback_finalize_dist(world, wire, cap):
     """nk_finalize_dist: u32 / u64 wire all-reduce, export + all-gather + merge;
     cap 4 and 1 overflow the export segments, so the redo and the two-pass
@@ -113,7 +114,7 @@ def test_loopback_finalize_dist(world, wire, cap):
     from neurokmer_amd import dist as nkdist
     from oracle import cbind
     k, pool = 31, 2_000_000
-    bases, offs = _input(1_200_000, 71 + world, 9)
+    bases, offs = _input(1_200_000, 71 + world, 9 if world < 8 else 19)
     shards = _shards(bases, offs, world)
     tk = int(offs[-1]) if wire == "u32" else None
     steps = 2
@@ -150,6 +151,12 @@ def test_loopback_finalize_dist(world, wire, cap):
     (3, 64, 2_000_000, 1000, 4096),       # the metric's pool
     (2, 64, 2_000_000, 20000, 4096),      # spike counts past 4095 in a slice: the refine redo
     (3, 64, 2_000_000, 20000, 4096),      # ... at world 3, after every case above in this process
+    # world 8 (the driver's 8-GPU node): the metric's pool with the u32 wire
+    # (bench.py's default N > 1 finish), a truncation redo, and config 5's
+    # shape (k = 63, 128-bit keys, a pool not divisible by 8)
+    (8, 64, 2_000_000, 1000, 4096),
+    (8, 64, 2_000_000, 1000, 4),
+    (8, 128, (1 << 22) + 5, 1000, 4096),
 ])
 def test_loopback_finalize_sliced_dist(world, width, pool, steps, cap):
     """nk_finalize_sliced_dist: reduce-scatter of a zero-padded wire (a pool
@@ -160,7 +167,7 @@ def test_loopback_finalize_sliced_dist(world, width, pool, steps, cap):
     from neurokmer_amd import SpikingKmerCounter
     from neurokmer_amd import dist as nkdist
     k = 63 if pool > 2_000_000 else 31
-    bases, offs = _input(900_000, 81 + world, 7)
+    bases, offs = _input(900_000, 81 + world, 7 if world < 8 else 17)
     shards = _shards(bases, offs, world)
     tk = int(offs[-1]) if width == 64 else None
 
