@@ -240,7 +240,9 @@ def spawn_ranks(n: int) -> int:
 def cpu_baseline(bases: np.ndarray, offsets: np.ndarray, k: int, pool: int):
     """oracle/nk_oracle.c's restatement of process_parallel (src/spiking_hash.rs:
     84-201) over the whole input: one thread per record like rayon's par_iter
-    over records (:94-95), exact k-mer map, serial merge, serial 1000-step LIF."""
+    over records (:94-95), exact k-mer map, serial merge, serial 1000-step LIF
+    (memoised by count for fresh neurons: the port is faster than the reference
+    there, so the GPU ratio is conservative)."""
     from oracle import cbind
     threads = offsets.size - 1
     ref = cbind.OracleCounter(k, 1.0, 0.95, 2, 1.0, pool, True)
@@ -986,8 +988,10 @@ def extras(args, ctr, bases, offsets, nk, d_bases, d_offs, s_handle, dev_idx, Co
             "sample": (f"the whole rank-0 config-2 input ({bases.size:,} bases, {nk:,} k-mers, "
                        f"{n_recs} records, pool {pool:,}, k={k}, canonical): oracle/nk_oracle.c "
                        f"process_parallel restatement, one thread per record like rayon over "
-                       f"records (src/spiking_hash.rs:94-95), exact k-mer map, serial merge and "
-                       f"1000-step LIF")}
+                       f"records (src/spiking_hash.rs:94-95), exact k-mer map, serial merge; the "
+                       f"1000-step LIF serial over neurons, run once per distinct count among "
+                       f"fresh neurons and reused (a fresh neuron's spikes are a function of its "
+                       f"count, oracle/nk_oracle.c:558-592) -- the reference steps every neuron")}
         # SURVEY.md §8d's optional stronger baseline, labelled as such: the same
         # currents and spike counts by chunked threads with no exact k-mer map
         # and a memoised LIF (oracle/nk_oracle.c nko_lean_currents_lif)

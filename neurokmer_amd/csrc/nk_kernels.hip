@@ -707,7 +707,11 @@ __device__ __forceinline__ void part_tile(const KmerInput &in, int k, const Fast
     }
     if (tid == 0) s_start[B] = carry;
   }
-  const uint32_t xs = blockIdx.x & ((1u << pa.sub_shift) - 1u);  // this tile's sub-region (its XCD)
+  // this tile's sub-region: its XCD in a one-launch count (workgroup i runs on
+  // XCD i mod 8); by the tile, not the workgroup, so that the many small
+  // launches of a chunked count (file ingest) still fill the eight evenly
+  // (block 0 of every launch went to sub-region 0)
+  const uint32_t xs = (uint32_t)tile & ((1u << pa.sub_shift) - 1u);
   for (uint32_t b = tid; b < B; b += kPartBlock) {
     const uint32_t c = (s_cnt[b] + 7u) & ~7u;
     uint32_t fit = 0, base = 0;

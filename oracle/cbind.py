@@ -54,7 +54,8 @@ def lib():
         L.nko_process_sequence.argtypes = [C.c_void_p, u8p, C.c_size_t]
         L.nko_lean_currents_lif.restype = C.c_int
         L.nko_lean_currents_lif.argtypes = [u8p, u64p, C.c_size_t, C.c_size_t, C.c_int, C.c_uint64,
-                                            C.c_uint64, C.c_int, u64p, u64p, u64p]
+                                            C.c_uint64, C.c_float, C.c_float, C.c_uint32, C.c_int,
+                                            u64p, u64p, u64p]
         L.nko_simulate_spikes_auto.restype = None
         L.nko_simulate_spikes_auto.argtypes = [C.c_void_p]
         for fn, rt in (("nko_currents", u64p), ("nko_voltages", f32p), ("nko_refractory", u32p),
@@ -331,16 +332,19 @@ class OracleAssoc:
         return [(int(km[i]), float(sim[i])) for i in range(n)]
 
 
-def lean_currents_lif(bases, offsets, k, pool, canonical=True, steps=1000, n_threads=1):
+def lean_currents_lif(bases, offsets, k, pool, canonical=True, steps=1000, n_threads=1,
+                      threshold=1.0, leak=0.95, refractory=2):
     """The lean CPU baseline (nko_lean_currents_lif; not the reference's
-    structure): (currents, spike counts, total spikes) of one in-memory call."""
+    structure): (currents, spike counts, total spikes) of one in-memory call
+    from the reset state (the LIF memoised by count)."""
     bases = np.ascontiguousarray(bases, np.uint8)
     offsets = np.ascontiguousarray(offsets, np.uint64)
     cur = np.zeros(pool, np.uint64)
     sp = np.zeros(pool, np.uint64)
     tot = np.zeros(1, np.uint64)
     rc = lib().nko_lean_currents_lif(_ptr(bases, C.c_uint8), _ptr(offsets, C.c_uint64),
-                                     offsets.size - 1, k, int(canonical), pool, steps, n_threads,
+                                     offsets.size - 1, k, int(canonical), pool, steps,
+                                     float(threshold), float(leak), int(refractory), n_threads,
                                      _ptr(cur, C.c_uint64), _ptr(sp, C.c_uint64), _ptr(tot, C.c_uint64))
     if rc:
         raise ValueError("nko_lean_currents_lif failed (k <= 32, pool >= 1)")

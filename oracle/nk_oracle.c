@@ -735,6 +735,8 @@ typedef struct {
   size_t n_recs, k;
   int canonical;
   uint64_t pool, steps, w_lo, w_hi; /* this thread's windows [w_lo, w_hi) of all windows */
+  float thr, leak;                  /* LIF parameters (src/models.rs:20-51) */
+  uint32_t refr;
   uint64_t *cur;                    /* this thread's currents (pool) */
   uint64_t *cur_all, *spikes, n_lo, n_hi, total; /* the LIF phase: neurons [n_lo, n_hi) */
   int nthreads, idx;
@@ -787,7 +789,7 @@ static void *lean_lif(void *p) {
       float v = 0.0f;
       uint32_t r = 0;
       sp = 0;
-      nko_lif(c, t->steps, 1.0f, 0.95f, 2, 0, &v, &r, &sp);
+      nko_lif(c, t->steps, t->thr, t->leak, t->refr, 0, &v, &r, &sp);
       if (c < kMemo) memo[c] = sp;
     }
     t->spikes[i] = sp;
@@ -797,8 +799,21 @@ static void *lean_lif(void *p) {
   return NULL;
 }
 
+/* fn(ctx[j]) on n threads; a thread that cannot be created runs its share
+   on the calling thread */
+static void run_threads(void *(*fn)(void *), lean_ctx *t, pthread_t *th, int n) {
+  int *made = (int *)calloc((size_t)n, sizeof(int));
+  for (int j = 0; j < n; ++j) made[j] = made && pthread_create(&th[j], NULL, fn, &t[j]) == 0;
+  for (int j = 0; j < n; ++j) {
+    if (made && made[j]) pthread_join(th[j], NULL);
+    else fn(&t[j]);
+  }
+  free(made);
+}
+
 int nko_lean_currents_lif(const uint8_t *bases, const uint64_t *offsets, size_t n_recs, size_t k,
-                          int canonical, uint64_t pool, uint64_t steps, int n_threads,
+                          int canonical, uint64_t pool, uint64_t steps, float thr, float leak,
+                          uint32_t refr, int n_threads,
                           uint64_t *currents, uint64_t *spikes, uint64_t *total_spikes) {
   if (!pool || k < 1 || k > 32 || n_threads < 1) return -1;
   uint64_t nw = 0;
@@ -813,6 +828,7 @@ int nko_lean_currents_lif(const uint8_t *bases, const uint64_t *offsets, size_t 
   for (int j = 0; j < n_threads; ++j) {
     t[j].bases = bases; t[j].offsets = offsets; t[j].n_recs = n_recs; t[j].k = k;
     t[j].canonical = canonical; t[j].pool = pool; t[j].steps = steps;
+    t[j].thr = thr; t[j].leak = leak; t[j].refr = refr;
     t[j].w_lo = nw * (uint64_t)j / (uint64_t)n_threads;
     t[j].w_hi = nw * (uint64_t)(j + 1) / (uint64_t)n_threads;
     t[j].cur = (uint64_t *)calloc(pool, sizeof(uint64_t));
@@ -823,10 +839,8 @@ int nko_lean_currents_lif(const uint8_t *bases, const uint64_t *offsets, size_t 
     if (!t[j].cur) rc = -1;
   }
   if (!rc) {
-    for (int j = 0; j < n_threads; ++j) pthread_create(&th[j], NULL, lean_count, &t[j]);
-    for (int j = 0; j < n_threads; ++j) pthread_join(th[j], NULL);
-    for (int j = 0; j < n_threads; ++j) pthread_create(&th[j], NULL, lean_lif, &t[j]);
-    for (int j = 0; j < n_threads; ++j) pthread_join(th[j], NULL);
+    run_threads(lean_count, t, th, n_threads);
+    run_threads(lean_lif, t, th, n_threads);  /* (after every count: the LIF sums them) */
     uint64_t tot = 0;
     for (int j = 0; j < n_threads; ++j) tot += t[j].total;
     *total_spikes = tot;

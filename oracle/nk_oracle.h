@@ -86,9 +86,13 @@ void nko_simulate_spikes_auto(nko_counter *c);
  * the canonical key is a function of its window alone, models.rs:254-286),
  * per-thread u64 currents summed, then the 1000-step LIF of every neuron from
  * the fresh state in parallel over neurons (nko_lif: the reference's update
- * loop, bit-identical).  Writes currents[pool], spikes[pool], *total_spikes. */
+ * loop, bit-identical, with threshold thr, leak and refractory period refr;
+ * spikes memoised by count, which the fresh state makes exact).  Writes
+ * currents[pool], spikes[pool], *total_spikes.  A thread that cannot be
+ * created runs its share on the calling thread. */
 int nko_lean_currents_lif(const uint8_t *bases, const uint64_t *offsets, size_t n_recs, size_t k,
-                          int canonical, uint64_t pool, uint64_t steps, int n_threads,
+                          int canonical, uint64_t pool, uint64_t steps, float thr, float leak,
+                          uint32_t refr, int n_threads,
                           uint64_t *currents, uint64_t *spikes, uint64_t *total_spikes);
 /* process_sequence (src/spiking_hash.rs:203-273): per-record single-step form */
 int nko_process_sequence(nko_counter *c, const uint8_t *seq, size_t len);

@@ -747,16 +747,35 @@ def test_ingest_fastq_record_longer_than_carry_room(tmp_path):
 
 
 @pytest.mark.parametrize("fastq_device,max_rec", [(False, None), (True, None), (False, 7)])
-def test_ingest_fastq_stops_at_malformed_record(tmp_path, fastq_device, max_rec):
+def test_ingest_fastq_stops_at_malformed_record(tmp_path, capfd, fastq_device, max_rec):
     reads, roffs = synth.make_reads(300, 120, seed=7)
     p = tmp_path / "bad.fq"
     synth.write_fastq(str(p), reads, roffs)
     lines = p.read_bytes().split(b"\n")
     lines[4 * 150 + 3] = lines[4 * 150 + 3][:-1]  # record 150: quality one byte short
     p.write_bytes(b"\n".join(lines))
+    capfd.readouterr()
     recs = _ingest_check(str(p), 19, 3001, True, True, 2000, fastq_device=fastq_device,
                          max_rec=max_rec)
     assert len(recs) == 150
+    # the reference's `warn!("Skipping malformed record: ...")` (src/utils.rs:17-19):
+    # the library's own line (and the Python mirror's, which the check reads too)
+    err = capfd.readouterr().err
+    assert sum("Skipping malformed record" in ln and "record 150 of" in ln
+               for ln in err.splitlines()) == 2, err
+
+
+@pytest.mark.parametrize("fastq_device", [False, True])
+def test_ingest_fastq_xcd_subregions_many_small_launches(tmp_path, fastq_device):
+    """Pool > 4.2 M (K1a's per-XCD sub-regions) counted in many small launches
+    (1 MB ingest windows): every launch's tiles fill the eight sub-regions
+    evenly, and the result is the oracle's."""
+    reads, roffs = synth.make_reads(24_000, 150, seed=8, n_rate=0.001, repeats_per_mb=2000,
+                                    motif_len=70)
+    p = tmp_path / "sub.fq"
+    synth.write_fastq(str(p), reads, roffs)
+    recs = _ingest_check(str(p), 31, 6_000_007, True, True, 1_000_003, fastq_device=fastq_device)
+    assert len(recs) == 24_000
 
 
 def test_ingest_fastq_blank_lines_use_host_reader(tmp_path):

@@ -424,3 +424,13 @@ def test_lean_cpu_baseline_matches_the_restatement(canon, threads):
     np.testing.assert_array_equal(cur, r.currents())
     np.testing.assert_array_equal(sp, r.spike_counts())
     assert tot == r.total_spikes
+    # other LIF parameters reach the lean LIF too (they were fixed)
+    cur2, sp2, tot2 = cbind.lean_currents_lif(bases, offs, k, pool, canonical=canon,
+                                              n_threads=threads, steps=300, threshold=0.5,
+                                              leak=0.9, refractory=3)
+    r2 = cbind.OracleCounter(k, 0.5, 0.9, 3, 1.0, pool, canon)
+    r2.set_steps(300)
+    r2.process_parallel_arrays(bases, offs)
+    np.testing.assert_array_equal(cur2, r2.currents())
+    np.testing.assert_array_equal(sp2, r2.spike_counts())
+    assert tot2 == r2.total_spikes
