@@ -87,7 +87,17 @@ int plan_count(nk_counter *c, uint64_t est_bases, uint64_t slack, uint64_t max_s
   const bool wide_ok = keys_ok && P <= (1ull << 31);
   const int forced = wide_bits_forced();
   if (atomic_forced()) return NK_OK;  // tests: the direct-atomic kernels at any size
-  if (forced > 0 && wide_ok) cp.path = CountPath::Wide;
+  // Part past 128 buckets (P > 4.2 M) leaves ~13-record segments per (tile,
+  // bucket) at config 3's 16 M: K1a wrote 15.2 B per k-mer for 4 (partial
+  // lines of scattered 16-B stores) and reserved 489 times per tile.  A count
+  // that keeps its records in one launch takes the wide path there instead:
+  // <= 128 coarse buckets (long segments of u32 records, the keys rolled in
+  // registers as K1a does: gen_rolled64), then the split into the 32768-neuron
+  // buckets.  (NK_PART_BIG=1: the Part path as before, A/B.)  Chunked and
+  // streamed counts keep Part (they keep every record for the uniques scan).
+  const bool big_wide = cp.km == 0 && keep_gen && !part_bits && B > kSubMinBuckets && wide_ok &&
+                        c->canonical && !getenv("NK_PART_BIG");
+  if ((forced > 0 || big_wide) && wide_ok) cp.path = CountPath::Wide;
   else if (cp.km == 0 && B <= (uint64_t)kMaxBuckets) cp.path = CountPath::Part;
   else if (keys_ok && B <= (uint64_t)kMaxBuckets) cp.path = CountPath::Gen;
   else if (wide_ok) cp.path = CountPath::Wide;
@@ -115,7 +125,10 @@ int plan_count(nk_counter *c, uint64_t est_bases, uint64_t slack, uint64_t max_s
     // descriptors, a 64-way split.  Config 5 (P = 256 M): 123 buckets of 2^21
     // bins, the count 77.1 ms against 79.7 with 245 of 2^20 and 79.4 with 62 of
     // 2^22 (the uniques scan of a top bucket grows with it, profiles/r05_i)
-    constexpr uint64_t kCoarse = 128;
+    // (the Part pools past 4.2 M, big_wide: at most 64 -- config 3's count
+    // 23.7 vs 25.2 ms with 62 coarse buckets of 2^18 against 123 of 2^17,
+    // the longer segments and fewer split tiles, profiles/r06_c3)
+    const uint64_t kCoarse = big_wide ? 64 : 128;
     int bits = kBinBits;
     while (((P + (1ull << bits) - 1) >> bits) > kCoarse) ++bits;
     if (forced > bits) bits = std::min(forced, kBinBits + kMaxSplitBits);

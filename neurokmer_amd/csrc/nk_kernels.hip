@@ -499,11 +499,18 @@ __global__ void k_set_merge128(MergeSrc m, FastMod fm, UniqArgs u) {
 constexpr int kPartPerThread = kPartTile / kPartBlock;  // 16
 constexpr uint32_t kPadOff = 0xFFFFu;                    // sentinel bin of a pad record
 // MAXB: bucket capacity of the launch (256 for pools <= 8.4 M, 512 up to
-// 16.7 M); the LDS sort area holds the tile plus the worst-case padding
+// 16.7 M).  The store groups are 8 records of one bucket (the reservations
+// are multiples of 8).  MAXB 256: the LDS sort area holds the tile plus the
+// worst-case padding, so every group is 16-B aligned there too.  MAXB 512
+// (UNPAD): the sort area holds the tile's 8192 records only and a group's
+// pad records are made at store time -- 14 KB less LDS (64.5 -> 50.6 KB), so
+// three workgroups share a CU instead of two (config 3's pool, 16 M).
 template <int MAXB>
 struct PartShape {
-  static constexpr int kSortSlots = kPartTile + 7 * MAXB;  // records + worst-case padding
-  static constexpr int kGroups = kSortSlots / 8;           // 8-record store groups
+  static constexpr bool kUnpad = MAXB > 256;
+  static constexpr int kPadded = kPartTile + 7 * MAXB;     // records + worst-case padding
+  static constexpr int kSortSlots = kUnpad ? kPartTile + 8 : kPadded;
+  static constexpr int kGroups = kPadded / 8;              // 8-record store groups
   static constexpr int kGroupIters = (kGroups + kPartBlock - 1) / kPartBlock;
   using GMap = typename std::conditional<(MAXB > 256), uint16_t, uint8_t>::type;
 };
@@ -546,7 +553,8 @@ struct PartLds {
   using S = PartShape<MAXB>;
   TileLds<kPartTile, RAW> L;
   uint32_t s_cnt[MAXB + 1];  // + a dummy bucket for non-k-mer positions
-  uint32_t s_start[MAXB + 1];
+  uint32_t s_start[MAXB + 1];  // padded (groups, reservations)
+  uint32_t s_ustart[PartShape<MAXB>::kUnpad ? MAXB + 1 : 1];  // unpadded (the LDS sort)
   uint32_t s_base[MAXB];
   uint32_t s_fit[MAXB];
   __align__(16) uint32_t s_sorted[S::kSortSlots];
@@ -562,6 +570,8 @@ __device__ __forceinline__ void part_tile(const KmerInput &in, int k, const Fast
   TileLds<kPartTile, !CANON> &L = sm.L;
   uint32_t(&s_cnt)[MAXB + 1] = sm.s_cnt;
   uint32_t(&s_start)[MAXB + 1] = sm.s_start;
+  constexpr bool kUnpad = S::kUnpad;
+  uint32_t *s_ustart = sm.s_ustart;
   uint32_t(&s_base)[MAXB] = sm.s_base;
   uint32_t(&s_fit)[MAXB] = sm.s_fit;
   uint32_t(&s_sorted)[kSortSlots] = sm.s_sorted;
@@ -706,6 +716,20 @@ __device__ __forceinline__ void part_tile(const KmerInput &in, int k, const Fast
       carry += __shfl(x, 63, 64);
     }
     if (tid == 0) s_start[B] = carry;
+  } else if (kUnpad && tid < 128) {  // the unpadded starts (the dummy bucket B last), wave 1
+    const uint32_t l = tid - 64;
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 <= B; b0 += 64) {
+      uint32_t b = b0 + l;
+      uint32_t c = b <= B ? s_cnt[b] : 0;
+      uint32_t x = c;
+      for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(x, o, 64);
+        if (l >= (uint32_t)o) x += y;
+      }
+      if (b <= B) s_ustart[b] = carry + x - c;
+      carry += __shfl(x, 63, 64);
+    }
   }
   // this tile's sub-region: its XCD in a one-launch count (workgroup i runs on
   // XCD i mod 8); by the tile, not the workgroup, so that the many small
@@ -741,14 +765,15 @@ __device__ __forceinline__ void part_tile(const KmerInput &in, int k, const Fast
   {
     uint32_t st[kPartPerThread];
 #pragma unroll
-    for (int j = 0; j < kPartPerThread; ++j) st[j] = s_start[E[j] >> 16];
+    for (int j = 0; j < kPartPerThread; ++j) st[j] = kUnpad ? s_ustart[E[j] >> 16] : s_start[E[j] >> 16];
 #pragma unroll
     for (int j = 0; j < kPartPerThread; ++j)
       s_sorted[st[j] + (E[j] & 0xFFFFu)] = O[j] | ((uint32_t)(q0 + j) << 16);
   }
   for (uint32_t b = tid; b < B; b += kPartBlock) {
     const uint32_t c = s_cnt[b], st = s_start[b], cp = (c + 7u) & ~7u;
-    for (uint32_t i = c; i < cp; ++i) s_sorted[st + i] = 0xFFFFFFFFu;
+    if (!kUnpad)
+      for (uint32_t i = c; i < cp; ++i) s_sorted[st + i] = 0xFFFFFFFFu;
     for (uint32_t g = st >> 3; g < (st + cp) >> 3; ++g) s_gmap[g] = (typename S::GMap)b;
   }
   __syncthreads();
@@ -762,8 +787,18 @@ __device__ __forceinline__ void part_tile(const KmerInput &in, int k, const Fast
     if (g >= n_groups) break;
     const uint32_t b = s_gmap[g];
     const uint32_t j8 = g * 8 - s_start[b];
-    const uint4 w0 = *reinterpret_cast<const uint4 *>(&s_sorted[g * 8]);
-    const uint4 w1 = *reinterpret_cast<const uint4 *>(&s_sorted[g * 8 + 4]);
+    uint4 w0, w1;
+    if (kUnpad) {  // the group's records from the unpadded sort, its pads made here
+      const uint32_t src = s_ustart[b] + j8, c = s_cnt[b];
+      uint32_t w[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) w[i] = j8 + (uint32_t)i < c ? s_sorted[src + i] : 0xFFFFFFFFu;
+      w0 = make_uint4(w[0], w[1], w[2], w[3]);
+      w1 = make_uint4(w[4], w[5], w[6], w[7]);
+    } else {
+      w0 = *reinterpret_cast<const uint4 *>(&s_sorted[g * 8]);
+      w1 = *reinterpret_cast<const uint4 *>(&s_sorted[g * 8 + 4]);
+    }
 #if defined(NK_ABL_NOWRITE)  // ablation: LDS sort kept, no HBM record stores
     if (w0.x == 0x12345678u && w1.w == 0x9ABCDEF0u) pa.overflow[b] = 1u;
     continue;

@@ -147,6 +147,62 @@ __device__ __forceinline__ void sort_and_store(const uint32_t (&E)[PER], const u
 
 }  // namespace
 
+// k <= 32, canonical (KM 0): the lane's 16 windows rolled in registers exactly
+// as K1a does it (nk_kernels.hip part_tile: the first window from the bit
+// streams, the next 15 as funnel shifts of two 96-bit words per strand,
+// src/models.rs:254-286) -- the generic loop extracted every window from LDS
+// (window_key: six LDS words and 64-bit variable shifts per key).  Pools past
+// 4.2 M take this wide count (two levels: long segments per (tile, coarse
+// bucket) instead of ~13-record ones per (tile, 32768-neuron bucket)).
+template <bool SMALL>
+__device__ __forceinline__ void gen_rolled64(const TileLds<kPartTile, false> &L, const KmerInput &in,
+                                             uint64_t T0, int q0, int k, const FastMod &fm,
+                                             uint32_t nb, int bb, uint32_t omask, uint32_t ltag,
+                                             uint32_t *s_cnt, uint32_t (&E)[kPer], uint32_t (&O)[kPer]) {
+  const uint64_t rem = in.n_bases - T0;  // >= 1
+  const uint64_t nrange = rem >= (uint64_t)k ? rem - (uint64_t)k + 1 : 0;
+  uint32_t ok = ~(L.WIN[q0 >> 5] >> (q0 & 31)) & 0xFFFFu;
+  if (nrange < (uint64_t)q0 + kPer) ok &= nrange > (uint64_t)q0 ? (1u << (uint32_t)(nrange - q0)) - 1u : 0u;
+  const uint64_t p0 = T0 + (uint64_t)q0;
+  if (in.pos_lo > p0) ok &= in.pos_lo - p0 >= (uint64_t)kPer ? 0u : ~((1u << (uint32_t)(in.pos_lo - p0)) - 1u);
+  if (in.pos_hi < p0 + kPer) ok &= in.pos_hi > p0 ? (1u << (uint32_t)(in.pos_hi - p0)) - 1u : 0u;
+  const int twok = 2 * k;
+  const uint64_t mask2k = (k >= 32) ? ~0ULL : ((1ULL << twok) - 1ULL);
+  uint64_t fwd, rev;
+  {
+    const int w = q0 >> 4;  // q0 is 16-aligned: shift 0
+    const uint64_t x = ((uint64_t)L.F[w] << 32) | L.F[w + 1];
+    fwd = x >> (64 - twok);
+    rev = (((uint64_t)L.R[w + 1] << 32) | L.R[w]) & mask2k;
+  }
+  uint32_t inF, inR;  // codes of the 15 bases rolled in: positions q0+k .. q0+k+14
+  {
+    const int s0 = q0 + k;
+    const int w = s0 >> 4, sh = 2 * (s0 & 15);
+    inF = (uint32_t)(((((uint64_t)L.F[w] << 32) | L.F[w + 1]) << sh) >> 32);
+    inR = (uint32_t)((((uint64_t)L.R[w + 1] << 32) | L.R[w]) >> sh);
+  }
+  const uint32_t g0 = inF, g1 = (uint32_t)fwd, g2 = (uint32_t)(fwd >> 32);
+  const unsigned __int128 X = ((unsigned __int128)inR << twok) | rev;
+  const uint32_t x0 = (uint32_t)X, x1 = (uint32_t)(X >> 32), x2 = (uint32_t)(X >> 64);
+  const uint32_t mlo = (uint32_t)mask2k, mhi = (uint32_t)(mask2k >> 32);
+  const uint32_t pv = (uint32_t)fm.p;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    if (j) {
+      fwd = ((uint64_t)(__builtin_amdgcn_alignbit(g2, g1, 32 - 2 * j) & mhi) << 32) |
+            (__builtin_amdgcn_alignbit(g1, g0, 32 - 2 * j) & mlo);
+      rev = ((uint64_t)(__builtin_amdgcn_alignbit(x2, x1, 2 * j) & mhi) << 32) |
+            (__builtin_amdgcn_alignbit(x1, x0, 2 * j) & mlo);
+    }
+    const uint64_t h = sip13_u64(fwd < rev ? fwd : rev);
+    const uint32_t idx = SMALL ? fastmod32_p(h, fm, pv) : (uint32_t)fastmod(h, fm);
+    const uint32_t b = ((ok >> j) & 1u) ? (idx >> bb) : nb;
+    E[j] = (b << 16) | atomicAdd(&s_cnt[b], 1u);
+    O[j] = (idx & omask) | ltag;
+  }
+}
+
 // --kmer-width=128, canonical, 48 < k <= 64 (config 5: k = 63): the lane's 16
 // windows from 6 forward and 6 complement code words read once from LDS, each
 // window's two 128-bit strands by funnel shifts of constant (2j) and uniform
@@ -261,6 +317,15 @@ __device__ __forceinline__ void gen_tile(const KmerInput &in, int k, const FastM
 
   const int q0 = tid * kPer;
   uint32_t E[kPer], O[kPer];
+  if constexpr (KM == 0 && CANON && !KEYS) {
+    if (small_pool) gen_rolled64<true>(L, in, T0, q0, k, fm, nb, bb, omask, ltag, sm.s_cnt, E, O);
+    else gen_rolled64<false>(L, in, T0, q0, k, fm, nb, bb, omask, ltag, sm.s_cnt, E, O);
+    sort_and_store<WIDE, kPer>(E, O, nb, sm.s_cnt, sm.s_start, sm.s_base, sm.s_fit, sm.s_rec,
+                               sm.s_gmap, ga.fill, ga.overflow, ga.cap,
+                               reinterpret_cast<typename S::Rec *>(ga.rec), 0, bb, ga.currents, ga.desc,
+                               ga.max_segs, (uint32_t)tile);
+    return;
+  }
   if constexpr (KM == 2 && CANON) {
     if (k > 48) {  // (uniform) the lane's 16 windows rolled from registers
       // (the pool's modulo a template argument too: a uniform branch per
