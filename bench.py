@@ -335,10 +335,6 @@ def main() -> int:
                     help="batches in flight (default: 3 on one GPU, 1 across ranks and for "
                          "config5): > 1 "
                          "overlaps a batch's finish with the next batch's count")
-    ap.add_argument("--count-streams", type=int, default=1, choices=(1, 2),
-                    help="2: batches alternate between two count streams (A/B, with "
-                         "NK_COUNT_CHAIN=1: a count kernel waits for the previous batch's count "
-                         "kernel, not its histogram)")
     ap.add_argument("--defer-hist", choices=("auto", "on", "off"), default="off",
                     help="each handle's bucket histogram (K1b) inside the next handle's count "
                          "kernel (nk_opts.defer_hist, k_part_fused); auto: on with >= 3 batches "
@@ -518,9 +514,6 @@ def rank_main(args, world: int, rank: int, local: int, ctx, lcomm) -> int:
     # 0.529-0.537 vs 0.507-0.514 ms, profiles/r02_s31); handles alternating
     # between two count streams (0.5166 vs 0.5026 ms, profiles/r03_cs2).
     count_streams = [torch.cuda.Stream(device=dev)] * args.inflight
-    batch_streams = [count_streams[0]] + ([torch.cuda.Stream(device=dev)]
-                                          if args.count_streams == 2 else [])
-    n_started = [0]
     run_stream = count_streams[0]
     fin_stream = (torch.cuda.Stream(device=dev, priority=torch.cuda.Stream.priority_range()[1])
                   if args.inflight > 1 else run_stream)
@@ -537,8 +530,7 @@ def rank_main(args, world: int, rank: int, local: int, ctx, lcomm) -> int:
     def start(j):
         """Enqueue one batch's count on handle j (returns at once)."""
         t_s = time.perf_counter()
-        c, cs = ctrs[j], batch_streams[n_started[0] % len(batch_streams)]
-        n_started[0] += 1
+        c, cs = ctrs[j], count_streams[j]
         sh = cs.cuda_stream
         c.reset(sh, blocking=False)
         if side:

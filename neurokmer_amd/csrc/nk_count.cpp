@@ -417,51 +417,6 @@ void hist_forget(nk_counter *c) {
   c->hist_state = 0;
 }
 
-// ---------------------------------------------------------------------------
-// Count chain (NK_COUNT_CHAIN=1, A/B): the partitioned count kernel of one
-// batch waits for the previous batch's count KERNEL on the device (an event
-// recorded right after it), not for its K1b -- with batches alternating
-// between two count streams, K1a of batch i+1 then starts as K1b of batch i
-// drains instead of after it, its prep and the kernel gaps off the path.
-// ---------------------------------------------------------------------------
-namespace {
-struct ChainSlot {
-  hipEvent_t ev[2] = {nullptr, nullptr};
-  int next = 0;
-  bool valid = false;
-  hipStream_t s = nullptr;
-};
-std::mutex g_chain_mu;
-ChainSlot g_chain[kHistSlots];
-bool chain_on() {
-  static const bool on = getenv("NK_COUNT_CHAIN") && atoi(getenv("NK_COUNT_CHAIN")) != 0;
-  return on;
-}
-}  // namespace
-
-// before the count kernel on s: wait for the previous chained count kernel
-int chain_wait(nk_counter *c, hipStream_t s) {
-  if (!chain_on()) return NK_OK;
-  std::lock_guard<std::mutex> g(g_chain_mu);
-  ChainSlot &h = g_chain[(unsigned)c->device % kHistSlots];
-  if (h.valid && h.s != s) HIPCHK(hipStreamWaitEvent(s, h.ev[h.next ^ 1], 0));
-  return NK_OK;
-}
-
-// right after the count kernel on s
-int chain_mark(nk_counter *c, hipStream_t s) {
-  if (!chain_on()) return NK_OK;
-  std::lock_guard<std::mutex> g(g_chain_mu);
-  ChainSlot &h = g_chain[(unsigned)c->device % kHistSlots];
-  for (hipEvent_t &e : h.ev)
-    if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence));
-  HIPCHK(hipEventRecord(h.ev[h.next], s));
-  h.next ^= 1;
-  h.valid = true;
-  h.s = s;
-  return NK_OK;
-}
-
 // a positive integer from the environment (tests: force the rare branches)
 uint32_t env_u32(const char *name, uint32_t dflt) {
   const char *e = getenv(name);
@@ -637,14 +592,12 @@ int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_offs,
     const bool fusable = !keyed && part_fused_ok(cp.pa) && in.n_tiles >= kFuseMinTiles;
     HistJob hj{};
     nk_counter *taken = fusable ? hist_take(c, s, in.n_tiles, hj) : nullptr;
-    if ((rc = chain_wait(c, s))) return rc;
     if (taken) {
       HIPCHK(launch_part_fused(in, (int)c->k, c->canonical, c->pool, cp.pa, hj, s));
       HIPCHK(hipEventRecord(taken->hist_ev, s));
     } else {
       HIPCHK(launch_part(in, (int)c->k, c->canonical, c->pool, cp.pa, s));
     }
-    if ((rc = chain_mark(c, s))) return rc;
     HIPCHK(mark(c, 2, s));
     c->last_pa = cp.pa;
     // this count's K1b: left to the next count on this stream, or now
