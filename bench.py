@@ -512,7 +512,10 @@ def rank_main(args, world: int, rank: int, local: int, ctx, lcomm) -> int:
     # Measured slower and not kept: a stream per handle with 3 in flight (the
     # third count's queue was not served until the finish queue went idle,
     # 0.529-0.537 vs 0.507-0.514 ms, profiles/r02_s31); handles alternating
-    # between two count streams (0.5166 vs 0.5026 ms, profiles/r03_cs2).
+    # between two count streams (0.5166 vs 0.5026 ms, profiles/r03_cs2; round 6,
+    # each count kernel ordered only after the previous batch's count kernel so
+    # that it could start beside that batch's K1b: 0.523-0.531 vs 0.510-0.516
+    # ms, profiles/r06_ab).
     count_streams = [torch.cuda.Stream(device=dev)] * args.inflight
     run_stream = count_streams[0]
     fin_stream = (torch.cuda.Stream(device=dev, priority=torch.cuda.Stream.priority_range()[1])
