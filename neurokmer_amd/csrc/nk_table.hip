@@ -316,7 +316,7 @@ __device__ __forceinline__ void xg_load(const uint64_t *kp, const uint8_t *bp, u
 // entries written neuron by neuron straight from the lanes -- no 4096-slot
 // table to clear and read back, no CAS probes, no reorder pass.  A group with
 // more than kWsMax records or a neuron with more than 128 is left to
-// k_xgroup's hash table (ws_done[group] == 0).
+// k_xgroup's hash table: listed in ws_list ([0] = count), for k_xgroup_list.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kWsMax = 4096;  // records of a group the sort path takes
 constexpr uint32_t kWsNeuron = 128;  // records of one neuron (two per lane)
@@ -336,61 +336,88 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
   const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), l, 64);
   return ((uint64_t)hi << 32) | lo;
 }
-// one compare-exchange step of a bitonic network over element index e
-// (partner e ^ j on another lane): keep the min where the direction and the
-// half agree
-__device__ __forceinline__ uint64_t bstep(uint64_t x, uint32_t e, uint32_t k, uint32_t j) {
-  const uint64_t y = shfl_xor64(x, (int)j);
-  const bool up = (e & k) == 0, lower = (e & j) == 0;
-  const uint64_t lo = x < y ? x : y, hi = x < y ? y : x;
-  return lower == up ? lo : hi;
+// the value of lane (this lane ^ J), J a power of two < 64, without the LDS
+// crossbar where a DPP pattern exists: quad_perm for 1 and 2, a row rotate by
+// 8 for 8; ds_swizzle's xor mode for 4 and 16; ds_bpermute for 32
+template <int J>
+__device__ __forceinline__ uint32_t xlane32(uint32_t v) {
+  if constexpr (J == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
+  else if constexpr (J == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+  else if constexpr (J == 8) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+  else if constexpr (J == 4 || J == 16) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (J << 10));
+  else return (uint32_t)__shfl_xor((int)v, J, 64);
 }
-// ascending sort of the 128 keys {x0: elements 0..63 (lane), x1: 64..127}
-// (TWO false: only x0, 64 elements)
+template <int J>
+__device__ __forceinline__ uint64_t xlane64(uint64_t v) {
+  return ((uint64_t)xlane32<J>((uint32_t)(v >> 32)) << 32) | xlane32<J>((uint32_t)v);
+}
+// one compare-exchange step of a bitonic network over element index e
+// (partner e ^ J on another lane): keep the min where the direction (bit K of
+// e) and the half (bit J) agree
+template <int K, int J>
+__device__ __forceinline__ uint64_t bstep(uint64_t x, uint32_t e) {
+  const uint64_t y = xlane64<J>(x);
+  const bool keep_min = ((e & (uint32_t)K) == 0) == ((e & (uint32_t)J) == 0);
+  return (x < y) == keep_min ? x : y;
+}
+// the steps J, J/2 .. 1 of merge stage K over {x0: elements 0..63 (lane),
+// x1: 64..127 (TWO)}; J == 64 pairs x0 with x1 in the lane
+template <int K, int J, bool TWO>
+__device__ __forceinline__ void bmerge(uint64_t &x0, uint64_t &x1, uint32_t lane) {
+  if constexpr (J == 64) {
+    const uint64_t lo = x0 < x1 ? x0 : x1, hi = x0 < x1 ? x1 : x0;
+    x0 = lo;
+    x1 = hi;
+  } else {
+    x0 = bstep<K, J>(x0, lane);
+    if constexpr (TWO) x1 = bstep<K, J>(x1, 64u + lane);
+  }
+  if constexpr (J > 1) bmerge<K, J / 2, TWO>(x0, x1, lane);
+}
+// ascending sort of 128 (TWO) or 64 keys, from merge stage K on
+template <int K, bool TWO>
+__device__ __forceinline__ void wave_sort_from(uint64_t &x0, uint64_t &x1, uint32_t lane) {
+  bmerge<K, K / 2, TWO>(x0, x1, lane);
+  if constexpr (K < (TWO ? 128 : 64)) wave_sort_from<K * 2, TWO>(x0, x1, lane);
+}
 template <bool TWO>
 __device__ __forceinline__ void wave_sort(uint64_t &x0, uint64_t &x1, uint32_t lane) {
-  constexpr uint32_t N = TWO ? 128u : 64u;
-#pragma unroll
-  for (uint32_t k = 2; k <= N; k <<= 1) {
-#pragma unroll
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      if (j == 64) {  // partner in the other register of this lane (k == 128: ascending)
-        const uint64_t lo = x0 < x1 ? x0 : x1, hi = x0 < x1 ? x1 : x0;
-        x0 = lo;
-        x1 = hi;
-      } else {
-        x0 = bstep(x0, lane, k, j);
-        if (TWO) x1 = bstep(x1, 64u + lane, k, j);
-      }
-    }
-  }
+  wave_sort_from<2, TWO>(x0, x1, lane);
 }
 
 // two independent 64-key sorts interleaved (two neurons of <= 64 records: the
-// shuffles of one hide the other's latency)
+// exchanges of one hide the other's latency)
+template <int K, int J>
+__device__ __forceinline__ void bmerge2(uint64_t &a, uint64_t &b, uint32_t lane) {
+  a = bstep<K, J>(a, lane);
+  b = bstep<K, J>(b, lane);
+  if constexpr (J > 1) bmerge2<K, J / 2>(a, b, lane);
+}
+template <int K>
+__device__ __forceinline__ void wave_sort64x2_from(uint64_t &a, uint64_t &b, uint32_t lane) {
+  bmerge2<K, K / 2>(a, b, lane);
+  if constexpr (K < 64) wave_sort64x2_from<K * 2>(a, b, lane);
+}
 __device__ __forceinline__ void wave_sort64x2(uint64_t &a, uint64_t &b, uint32_t lane) {
-#pragma unroll
-  for (uint32_t k = 2; k <= 64u; k <<= 1) {
-#pragma unroll
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      a = bstep(a, lane, k, j);
-      b = bstep(b, lane, k, j);
-    }
-  }
+  wave_sort64x2_from<2>(a, b, lane);
 }
 
 // PAIR: a wave sorts neurons n and n + 4 together when both hold <= 64 records
 template <bool PAIR>
-__global__ __launch_bounds__(kXsBlock) void k_xgroup_ws(XGroupArgs t, uint8_t *__restrict__ ws_done) {
+__global__ __launch_bounds__(kXsBlock) void k_xgroup_ws(XGroupArgs t, uint32_t *__restrict__ ws_list) {
   __shared__ unsigned long long s_key[kWsMax];
   __shared__ uint32_t ncnt[kGroupN], nst[kGroupN], ncur[kGroupN], ndist[kGroupN], s_w[4];
   __shared__ uint32_t s_bad;
   const uint32_t g = blockIdx.x, b = blockIdx.y, NG = t.n_groups, tid = threadIdx.x;
   const uint32_t lane = tid & 63, wv = tid >> 6;
-  uint8_t &done = ws_done[(uint64_t)b * NG + g];
   const uint64_t n0 = ((uint64_t)b << t.bin_bits) + ((uint64_t)g << t.ggbits);
-  if (n0 >= t.pool || t.overflow[b]) {  // (k_xgroup writes the side neurons)
-    if (tid == 0) done = 0;
+  if (n0 >= t.pool) return;
+  // a group left to the hash table (its side neurons, too big, a hot neuron)
+  auto decline = [&]() {
+    if (tid == 0) ws_list[1 + atomicAdd(ws_list, 1u)] = b * NG + g;
+  };
+  if (t.overflow[b]) {
+    decline();
     return;
   }
   const uint32_t nG = (uint32_t)(t.pool - n0 < (uint64_t)(1u << t.ggbits) ? t.pool - n0 : (1u << t.ggbits));
@@ -399,7 +426,7 @@ __global__ __launch_bounds__(kXsBlock) void k_xgroup_ws(XGroupArgs t, uint8_t *_
   const uint64_t gs = base + gst[g], ge = base + gst[g + 1];
   const uint32_t nrec = (uint32_t)(ge - gs);
   if (ge - gs > kWsMax || t.hash_max) {  // (uniform) the hash table's (NK_XHASH_MAX: its side-list tests)
-    if (tid == 0) done = 0;
+    decline();
     return;
   }
   if (tid < kGroupN) ncnt[tid] = 0;
@@ -436,7 +463,7 @@ __global__ __launch_bounds__(kXsBlock) void k_xgroup_ws(XGroupArgs t, uint8_t *_
   }
   __syncthreads();
   if (s_bad) {  // (uniform) a hot neuron: the hash table takes the group
-    if (tid == 0) done = 0;
+    decline();
     return;
   }
 #pragma unroll
@@ -536,24 +563,21 @@ __global__ __launch_bounds__(kXsBlock) void k_xgroup_ws(XGroupArgs t, uint8_t *_
     t.uniq[i] = 0;
     t.cnt[i] = 0;
   }
-  if (tid == 0) {
-    if (D) atomicAdd(&t.bdist[b], (unsigned long long)D);
-    done = 1;
-  }
+  if (tid == 0 && D) atomicAdd(&t.bdist[b], (unsigned long long)D);
 }
 
-// 4096-slot LDS table (48 KB with its counts): three workgroups per CU
-__global__ __launch_bounds__(kXsBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_xgroup(XGroupArgs t) {
+// 4096-slot LDS table (48 KB with its counts): three workgroups per CU.
+// Group g of bucket b (uniform across the workgroup).
+__device__ __forceinline__ void xgroup_hash(const XGroupArgs &t, const uint32_t g, const uint32_t b) {
   constexpr int kHashBits = 12, kHashSlots = 1 << kHashBits, kSlotsPer = kHashSlots / kXsBlock;
   constexpr uint32_t kHashMax = kHashSlots * 5 / 8;
   __shared__ unsigned long long hk[kHashSlots];
   __shared__ uint32_t hc[kHashSlots];
   __shared__ uint32_t bc[kGroupN], bcur[kGroupN], spc[kGroupN], s_w[4];
   __shared__ uint32_t s_fail;
-  const uint32_t g = blockIdx.x, b = blockIdx.y, NG = t.n_groups, tid = threadIdx.x;
+  const uint32_t NG = t.n_groups, tid = threadIdx.x;
   const uint64_t n0 = ((uint64_t)b << t.bin_bits) + ((uint64_t)g << t.ggbits);
   if (n0 >= t.pool) return;
-  if (t.ws_done && t.ws_done[(uint64_t)b * NG + g]) return;  // k_xgroup_ws took the group
   const uint32_t nG = (uint32_t)(t.pool - n0 < (uint64_t)(1u << t.ggbits) ? t.pool - n0 : (1u << t.ggbits));
   if (t.overflow[b]) {  // side bucket
     if (tid < nG) {
@@ -700,6 +724,21 @@ __global__ __launch_bounds__(kXsBlock) __attribute__((amdgpu_waves_per_eu(3))) v
   if (tid == 0 && used) atomicAdd(&t.bdist[b], used);
 }
 
+__global__ __launch_bounds__(kXsBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_xgroup(XGroupArgs t) {
+  xgroup_hash(t, blockIdx.x, blockIdx.y);
+}
+
+// the groups k_xgroup_ws left (ws_list: [0] count, then bucket * n_groups + group)
+__global__ __launch_bounds__(kXsBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_xgroup_list(
+    XGroupArgs t, const uint32_t *__restrict__ ws_list) {
+  const uint32_t n = ws_list[0];
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint32_t e = ws_list[1 + i];
+    xgroup_hash(t, e % t.n_groups, e / t.n_groups);
+    __syncthreads();  // (the LDS table of the next group)
+  }
+}
+
 // the entry counts: one block over the buckets
 __global__ __launch_bounds__(256) void k_xfinish(XGroupArgs t, unsigned long long *n,
                                                  const unsigned long long *n_side_uniq) {
@@ -757,14 +796,19 @@ hipError_t xgroup_build(const XGroupArgs &t, hipStream_t s) {
   // twice as long (2.92-2.94 vs 2.94-2.95 ms, profiles/r03_xssub)
   hipLaunchKernelGGL(k_xscatter, dim3(8u * ((t.n_buckets + 7u) / 8u) * t.n_slices), dim3(kXsBlock),
                      0, s, t);
-  if (t.ws_done) {  // the sort path first; k_xgroup takes the groups it left
+  if (t.ws_list) {  // the sort path first; the hash table takes the groups it left
     static const bool single = getenv("NK_XG_WS1") != nullptr;  // A/B: one neuron per wave at a time
+    hipError_t e = hipMemsetAsync(t.ws_list, 0, 4, s);
+    if (e != hipSuccess) return e;
     if (single)
-      hipLaunchKernelGGL(k_xgroup_ws<false>, dim3(t.n_groups, t.n_buckets), dim3(kXsBlock), 0, s, t, t.ws_done);
+      hipLaunchKernelGGL(k_xgroup_ws<false>, dim3(t.n_groups, t.n_buckets), dim3(kXsBlock), 0, s, t, t.ws_list);
     else
-      hipLaunchKernelGGL(k_xgroup_ws<true>, dim3(t.n_groups, t.n_buckets), dim3(kXsBlock), 0, s, t, t.ws_done);
+      hipLaunchKernelGGL(k_xgroup_ws<true>, dim3(t.n_groups, t.n_buckets), dim3(kXsBlock), 0, s, t, t.ws_list);
+    // three 48-KB workgroups per CU, each looping over the list (usually empty)
+    hipLaunchKernelGGL(k_xgroup_list, dim3(768), dim3(kXsBlock), 0, s, t, (const uint32_t *)t.ws_list);
+  } else {
+    hipLaunchKernelGGL(k_xgroup, dim3(t.n_groups, t.n_buckets), dim3(kXsBlock), 0, s, t);
   }
-  hipLaunchKernelGGL(k_xgroup, dim3(t.n_groups, t.n_buckets), dim3(kXsBlock), 0, s, t);
   return hipGetLastError();
 }
 
