@@ -338,7 +338,7 @@ void nk_free(nk_counter *c) {
   c->x_pres.release(); c->x_tmp.release(); c->x_n.release();
   c->x_ent.release(); c->p_key.release(); c->xg_key.release(); c->xg_key2.release();
   c->xg_side.release(); c->xg_off.release(); c->xg_over.release(); c->xg_cnt.release();
-  c->xg_gst.release(); c->xg_trec.release(); c->xg_fill.release(); c->xg_bin2.release(); c->xg_ws.release();
+  c->xg_gst.release(); c->xg_trec.release(); c->xg_fill.release(); c->xg_bin2.release();
   c->xg_bctr.release();
   c->d_keys.release(); c->d_meta.release(); c->d_vals.release(); c->touched.release();
   c->tile_rec.release(); c->hist.release(); c->tie_cnt.release(); c->uniq.release();

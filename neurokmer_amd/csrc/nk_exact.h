@@ -102,9 +102,6 @@ struct XGroupArgs {
   uint32_t *kpn;                      // [pool] kmer_per_neuron (side neurons: 0, added later)
   uint32_t hash_max = 0;              // tests: fewer distinct keys per pass (0: the LDS table's)
   uint32_t hash_bits = 12;            // log2 LDS table slots of k_xgroup (xgroup_hash_bits())
-  // [1 + buckets * groups] or null: k_xgroup_ws (per-neuron wave sort) first;
-  // the groups it leaves listed ([0] = count) for the hash table (NK_XG_HASH=1: null)
-  uint32_t *ws_list = nullptr;
 };
 // 2^gbits neurons per LDS pass for n_records records over `pool` neurons, and
 // whether the expected distinct keys of a pass fit the LDS table; the group

@@ -262,7 +262,6 @@ struct nk_counter {
   DevBuf<uint32_t> xg_over, xg_cnt, xg_gst, xg_trec;
   DevBuf<unsigned long long> xg_fill, xg_bctr;
   DevBuf<uint8_t> xg_bin2;
-  DevBuf<uint32_t> xg_ws;  // the groups k_xgroup_ws leaves to the hash table
   // process_sequence: delta counts on top of the sorted table, kmer_per_neuron
   DevBuf<unsigned long long> d_keys, d_meta;
   DevBuf<uint32_t> d_vals;

@@ -308,274 +308,15 @@ __device__ __forceinline__ void xg_load(const uint64_t *kp, const uint8_t *bp, u
   }
 }
 
-// ---------------------------------------------------------------------------
-// k_xgroup_ws (round 6): the group's records counting-
-// sorted by neuron in LDS, then each neuron's keys (<= 128) sorted by one wave
-// in registers (bitonic network over the 64 lanes, two keys per lane), equal
-// keys adjacent: heads by ballot, runs' lengths from the next head, the
-// entries written neuron by neuron straight from the lanes -- no 4096-slot
-// table to clear and read back, no CAS probes, no reorder pass.  A group with
-// more than kWsMax records or a neuron with more than 128 is left to
-// k_xgroup's hash table: listed in ws_list ([0] = count), for k_xgroup_list.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kWsMax = 4096;  // records of a group the sort path takes
-constexpr uint32_t kWsNeuron = 128;  // records of one neuron (two per lane)
-
-__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
-  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64);
-  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
-  return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int d) {
-  const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, d, 64);
-  const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), d, 64);
-  return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
-  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, l, 64);
-  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), l, 64);
-  return ((uint64_t)hi << 32) | lo;
-}
-// the value of lane (this lane ^ J), J a power of two < 64, without the LDS
-// crossbar where a DPP pattern exists: quad_perm for 1 and 2, a row rotate by
-// 8 for 8; ds_swizzle's xor mode for 4 and 16; ds_bpermute for 32
-template <int J>
-__device__ __forceinline__ uint32_t xlane32(uint32_t v) {
-  if constexpr (J == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
-  else if constexpr (J == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
-  else if constexpr (J == 8) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
-  else if constexpr (J == 4 || J == 16) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (J << 10));
-  else return (uint32_t)__shfl_xor((int)v, J, 64);
-}
-template <int J>
-__device__ __forceinline__ uint64_t xlane64(uint64_t v) {
-  return ((uint64_t)xlane32<J>((uint32_t)(v >> 32)) << 32) | xlane32<J>((uint32_t)v);
-}
-// one compare-exchange step of a bitonic network over element index e
-// (partner e ^ J on another lane): keep the min where the direction (bit K of
-// e) and the half (bit J) agree
-template <int K, int J>
-__device__ __forceinline__ uint64_t bstep(uint64_t x, uint32_t e) {
-  const uint64_t y = xlane64<J>(x);
-  const bool keep_min = ((e & (uint32_t)K) == 0) == ((e & (uint32_t)J) == 0);
-  return (x < y) == keep_min ? x : y;
-}
-// the steps J, J/2 .. 1 of merge stage K over {x0: elements 0..63 (lane),
-// x1: 64..127 (TWO)}; J == 64 pairs x0 with x1 in the lane
-template <int K, int J, bool TWO>
-__device__ __forceinline__ void bmerge(uint64_t &x0, uint64_t &x1, uint32_t lane) {
-  if constexpr (J == 64) {
-    const uint64_t lo = x0 < x1 ? x0 : x1, hi = x0 < x1 ? x1 : x0;
-    x0 = lo;
-    x1 = hi;
-  } else {
-    x0 = bstep<K, J>(x0, lane);
-    if constexpr (TWO) x1 = bstep<K, J>(x1, 64u + lane);
-  }
-  if constexpr (J > 1) bmerge<K, J / 2, TWO>(x0, x1, lane);
-}
-// ascending sort of 128 (TWO) or 64 keys, from merge stage K on
-template <int K, bool TWO>
-__device__ __forceinline__ void wave_sort_from(uint64_t &x0, uint64_t &x1, uint32_t lane) {
-  bmerge<K, K / 2, TWO>(x0, x1, lane);
-  if constexpr (K < (TWO ? 128 : 64)) wave_sort_from<K * 2, TWO>(x0, x1, lane);
-}
-template <bool TWO>
-__device__ __forceinline__ void wave_sort(uint64_t &x0, uint64_t &x1, uint32_t lane) {
-  wave_sort_from<2, TWO>(x0, x1, lane);
-}
-
-// two independent 64-key sorts interleaved (two neurons of <= 64 records: the
-// exchanges of one hide the other's latency)
-template <int K, int J>
-__device__ __forceinline__ void bmerge2(uint64_t &a, uint64_t &b, uint32_t lane) {
-  a = bstep<K, J>(a, lane);
-  b = bstep<K, J>(b, lane);
-  if constexpr (J > 1) bmerge2<K, J / 2>(a, b, lane);
-}
-template <int K>
-__device__ __forceinline__ void wave_sort64x2_from(uint64_t &a, uint64_t &b, uint32_t lane) {
-  bmerge2<K, K / 2>(a, b, lane);
-  if constexpr (K < 64) wave_sort64x2_from<K * 2>(a, b, lane);
-}
-__device__ __forceinline__ void wave_sort64x2(uint64_t &a, uint64_t &b, uint32_t lane) {
-  wave_sort64x2_from<2>(a, b, lane);
-}
-
-// PAIR: a wave sorts neurons n and n + 4 together when both hold <= 64 records
-template <bool PAIR>
-__global__ __launch_bounds__(kXsBlock) void k_xgroup_ws(XGroupArgs t, uint32_t *__restrict__ ws_list) {
-  __shared__ unsigned long long s_key[kWsMax];
-  __shared__ uint32_t ncnt[kGroupN], nst[kGroupN], ncur[kGroupN], ndist[kGroupN], s_w[4];
-  __shared__ uint32_t s_bad;
-  const uint32_t g = blockIdx.x, b = blockIdx.y, NG = t.n_groups, tid = threadIdx.x;
-  const uint32_t lane = tid & 63, wv = tid >> 6;
-  const uint64_t n0 = ((uint64_t)b << t.bin_bits) + ((uint64_t)g << t.ggbits);
-  if (n0 >= t.pool) return;
-  // a group left to the hash table (its side neurons, too big, a hot neuron)
-  auto decline = [&]() {
-    if (tid == 0) ws_list[1 + atomicAdd(ws_list, 1u)] = b * NG + g;
-  };
-  if (t.overflow[b]) {
-    decline();
-    return;
-  }
-  const uint32_t nG = (uint32_t)(t.pool - n0 < (uint64_t)(1u << t.ggbits) ? t.pool - n0 : (1u << t.ggbits));
-  const uint32_t *gst = t.gstart + (uint64_t)b * (NG + 1);
-  const uint64_t base = (uint64_t)b * t.cap;
-  const uint64_t gs = base + gst[g], ge = base + gst[g + 1];
-  const uint32_t nrec = (uint32_t)(ge - gs);
-  if (ge - gs > kWsMax || t.hash_max) {  // (uniform) the hash table's (NK_XHASH_MAX: its side-list tests)
-    decline();
-    return;
-  }
-  if (tid < kGroupN) ncnt[tid] = 0;
-  if (tid == 0) s_bad = 0;
-  // the group's records, all loads in flight at once (<= 16 per thread)
-  constexpr int kWsPer = kWsMax / kXsBlock;
-  const uint8_t *bp = t.bin2 + gs;
-  const uint64_t *kp = t.key2 + gs;
-  uint32_t bn[kWsPer];
-  uint64_t ky[kWsPer];
-#pragma unroll
-  for (int u = 0; u < kWsPer; ++u) {
-    const uint32_t i = (uint32_t)u * kXsBlock + tid;
-    bn[u] = i < nrec ? (uint32_t)bp[i] : 0xFFu;
-  }
-#pragma unroll
-  for (int u = 0; u < kWsPer; ++u) {
-    const uint32_t i = (uint32_t)u * kXsBlock + tid;
-    ky[u] = i < nrec ? kp[i] : 0ull;
-  }
-  __syncthreads();
-  // records per neuron; each record's rank within its neuron
-#pragma unroll
-  for (int u = 0; u < kWsPer; ++u)
-    if (bn[u] != 0xFFu) bn[u] |= atomicAdd(&ncnt[bn[u]], 1u) << 8;
-  __syncthreads();
-  // neuron starts (one value per thread, nG <= 128 neurons)
-  const uint32_t c_me = tid < nG ? ncnt[tid] : 0u;
-  uint32_t tot;
-  const uint32_t st_me = block_excl_scan(c_me, s_w, &tot);
-  if (tid < nG) {
-    nst[tid] = st_me;
-    if (c_me > kWsNeuron) s_bad = 1u;
-  }
-  __syncthreads();
-  if (s_bad) {  // (uniform) a hot neuron: the hash table takes the group
-    decline();
-    return;
-  }
-#pragma unroll
-  for (int u = 0; u < kWsPer; ++u)
-    if ((bn[u] & 0xFFu) != 0xFFu) s_key[nst[bn[u] & 0xFFu] + (bn[u] >> 8)] = ky[u];
-  __syncthreads();
-  // each wave: its neurons' keys sorted in registers, written back in order;
-  // distinct keys per neuron (heads of runs).  (Pads are ~0 and sort last; a
-  // real ~0 key sorts just before them.)
-  auto put = [&](uint32_t n, uint64_t x0, uint64_t x1) {
-    const uint32_t c = ncnt[n], st = nst[n];
-    // (the shuffles unconditional: a lane outside the branch that reads lane
-    // 0 would read 0 from an inactive lane)
-    const uint64_t u0 = shfl_up64(x0, 1), u1 = shfl_up64(x1, 1), l63 = readlane64(x0, 63);
-    const uint64_t p0 = lane ? u0 : 0ull, p1 = lane ? u1 : l63;
-    const bool h0 = lane < c && (lane == 0 || x0 != p0);
-    const bool h1 = 64u + lane < c && x1 != p1;
-    const uint64_t m0 = __ballot(h0), m1 = __ballot(h1);
-    if (lane < c) s_key[st + lane] = x0;
-    if (64u + lane < c) s_key[st + 64u + lane] = x1;
-    if (lane == 0) ndist[n] = (uint32_t)(__popcll(m0) + __popcll(m1));
-  };
-  auto one = [&](uint32_t n) {
-    const uint32_t c = ncnt[n], st = nst[n];
-    uint64_t x0 = lane < c ? (uint64_t)s_key[st + lane] : ~0ull;
-    uint64_t x1 = 64u + lane < c ? (uint64_t)s_key[st + 64u + lane] : ~0ull;
-#if !defined(NK_WS_NOSORT)  // (ablation builds, tools/ab_build.sh: results wrong)
-    if (c > 64) wave_sort<true>(x0, x1, lane);
-    else if (c > 1) wave_sort<false>(x0, x1, lane);
-#endif
-    put(n, x0, x1);
-  };
-  constexpr uint32_t kWaves = kXsBlock / 64;
-  if constexpr (PAIR) {
-    for (uint32_t n = wv; n < nG; n += 2 * kWaves) {
-      const uint32_t m = n + kWaves;
-      const uint32_t ca = ncnt[n], cb = m < nG ? ncnt[m] : 0u;
-      if (ca <= 64 && cb <= 64) {  // (uniform)
-        uint64_t a = lane < ca ? (uint64_t)s_key[nst[n] + lane] : ~0ull;
-        uint64_t bb = lane < cb ? (uint64_t)s_key[nst[m < nG ? m : n] + lane] : ~0ull;
-#if !defined(NK_WS_NOSORT)
-        wave_sort64x2(a, bb, lane);
-#endif
-        put(n, a, ~0ull);
-        if (m < nG) put(m, bb, ~0ull);
-      } else {
-        one(n);
-        if (m < nG) one(m);
-      }
-    }
-  } else {
-    for (uint32_t n = wv; n < nG; n += kWaves) one(n);
-  }
-  __syncthreads();
-  // the group's entries: neuron by neuron from the group's table base
-  const uint32_t d_me = tid < nG ? ndist[tid] : 0u;
-  uint32_t D;
-  const uint32_t ds_me = block_excl_scan(d_me, s_w, &D);
-  const unsigned long long tbase = t.bbase[b] + gst[g];
-  if (tid < nG) {
-    ncur[tid] = ds_me;  // the neuron's first entry in the group's range
-    t.ent[n0 + tid] = (tbase + ds_me) | ((unsigned long long)d_me << 40);
-    t.kpn[n0 + tid] = d_me;  // kmer_per_neuron (src/spiking_hash.rs:167-172)
-  }
-  __syncthreads();
-  for (uint32_t n = wv; n < nG; n += kXsBlock / 64) {
-    const uint32_t c = ncnt[n], st = nst[n];
-    const uint64_t x0 = lane < c ? (uint64_t)s_key[st + lane] : ~0ull;
-    const uint64_t x1 = 64u + lane < c ? (uint64_t)s_key[st + 64u + lane] : ~0ull;
-    // (the shuffles unconditional: a lane outside the branch that reads lane
-    // 0 would read 0 from an inactive lane)
-    const uint64_t u0 = shfl_up64(x0, 1), u1 = shfl_up64(x1, 1), l63 = readlane64(x0, 63);
-    const uint64_t p0 = lane ? u0 : 0ull, p1 = lane ? u1 : l63;
-    const bool h0 = lane < c && (lane == 0 || x0 != p0);
-    const bool h1 = 64u + lane < c && x1 != p1;
-    const uint64_t m0 = __ballot(h0), m1 = __ballot(h1);
-    const unsigned long long at = tbase + ncur[n];
-    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;  // lanes < this one
-    if (h0) {
-      const uint64_t rest = lane < 63 ? m0 >> (lane + 1) : 0ull;
-      const uint32_t next = rest ? lane + 1 + (uint32_t)__builtin_ctzll(rest)
-                                 : (m1 ? 64u + (uint32_t)__builtin_ctzll(m1) : c);
-      const uint32_t r = (uint32_t)__popcll(m0 & below);
-      t.uniq[at + r] = x0;
-      t.cnt[at + r] = next - lane;
-    }
-    if (h1) {
-      const uint64_t rest = lane < 63 ? m1 >> (lane + 1) : 0ull;
-      const uint32_t next = rest ? 64u + lane + 1 + (uint32_t)__builtin_ctzll(rest) : c;
-      const uint32_t r = (uint32_t)(__popcll(m0) + __popcll(m1 & below));
-      t.uniq[at + r] = x1;
-      t.cnt[at + r] = next - (64u + lane);
-    }
-  }
-  // the rest of the group's range: (0, count 0); its distinct keys to the bucket
-  for (unsigned long long i = tbase + D + tid; i < tbase + nrec; i += kXsBlock) {
-    t.uniq[i] = 0;
-    t.cnt[i] = 0;
-  }
-  if (tid == 0 && D) atomicAdd(&t.bdist[b], (unsigned long long)D);
-}
-
-// 4096-slot LDS table (48 KB with its counts): three workgroups per CU.
-// Group g of bucket b (uniform across the workgroup).
-__device__ __forceinline__ void xgroup_hash(const XGroupArgs &t, const uint32_t g, const uint32_t b) {
+// 4096-slot LDS table (48 KB with its counts): three workgroups per CU
+__global__ __launch_bounds__(kXsBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_xgroup(XGroupArgs t) {
   constexpr int kHashBits = 12, kHashSlots = 1 << kHashBits, kSlotsPer = kHashSlots / kXsBlock;
   constexpr uint32_t kHashMax = kHashSlots * 5 / 8;
   __shared__ unsigned long long hk[kHashSlots];
   __shared__ uint32_t hc[kHashSlots];
   __shared__ uint32_t bc[kGroupN], bcur[kGroupN], spc[kGroupN], s_w[4];
   __shared__ uint32_t s_fail;
-  const uint32_t NG = t.n_groups, tid = threadIdx.x;
+  const uint32_t g = blockIdx.x, b = blockIdx.y, NG = t.n_groups, tid = threadIdx.x;
   const uint64_t n0 = ((uint64_t)b << t.bin_bits) + ((uint64_t)g << t.ggbits);
   if (n0 >= t.pool) return;
   const uint32_t nG = (uint32_t)(t.pool - n0 < (uint64_t)(1u << t.ggbits) ? t.pool - n0 : (1u << t.ggbits));
@@ -724,21 +465,6 @@ __device__ __forceinline__ void xgroup_hash(const XGroupArgs &t, const uint32_t 
   if (tid == 0 && used) atomicAdd(&t.bdist[b], used);
 }
 
-__global__ __launch_bounds__(kXsBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_xgroup(XGroupArgs t) {
-  xgroup_hash(t, blockIdx.x, blockIdx.y);
-}
-
-// the groups k_xgroup_ws left (ws_list: [0] count, then bucket * n_groups + group)
-__global__ __launch_bounds__(kXsBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_xgroup_list(
-    XGroupArgs t, const uint32_t *__restrict__ ws_list) {
-  const uint32_t n = ws_list[0];
-  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-    const uint32_t e = ws_list[1 + i];
-    xgroup_hash(t, e % t.n_groups, e / t.n_groups);
-    __syncthreads();  // (the LDS table of the next group)
-  }
-}
-
 // the entry counts: one block over the buckets
 __global__ __launch_bounds__(256) void k_xfinish(XGroupArgs t, unsigned long long *n,
                                                  const unsigned long long *n_side_uniq) {
@@ -796,19 +522,7 @@ hipError_t xgroup_build(const XGroupArgs &t, hipStream_t s) {
   // twice as long (2.92-2.94 vs 2.94-2.95 ms, profiles/r03_xssub)
   hipLaunchKernelGGL(k_xscatter, dim3(8u * ((t.n_buckets + 7u) / 8u) * t.n_slices), dim3(kXsBlock),
                      0, s, t);
-  if (t.ws_list) {  // the sort path first; the hash table takes the groups it left
-    static const bool single = getenv("NK_XG_WS1") != nullptr;  // A/B: one neuron per wave at a time
-    hipError_t e = hipMemsetAsync(t.ws_list, 0, 4, s);
-    if (e != hipSuccess) return e;
-    if (single)
-      hipLaunchKernelGGL(k_xgroup_ws<false>, dim3(t.n_groups, t.n_buckets), dim3(kXsBlock), 0, s, t, t.ws_list);
-    else
-      hipLaunchKernelGGL(k_xgroup_ws<true>, dim3(t.n_groups, t.n_buckets), dim3(kXsBlock), 0, s, t, t.ws_list);
-    // three 48-KB workgroups per CU, each looping over the list (usually empty)
-    hipLaunchKernelGGL(k_xgroup_list, dim3(768), dim3(kXsBlock), 0, s, t, (const uint32_t *)t.ws_list);
-  } else {
-    hipLaunchKernelGGL(k_xgroup, dim3(t.n_groups, t.n_buckets), dim3(kXsBlock), 0, s, t);
-  }
+  hipLaunchKernelGGL(k_xgroup, dim3(t.n_groups, t.n_buckets), dim3(kXsBlock), 0, s, t);
   return hipGetLastError();
 }
 

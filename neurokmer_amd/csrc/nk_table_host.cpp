@@ -276,10 +276,6 @@ int build_grouped(nk_counter *c, const KmerInput &in0, const PartArgs *keyed, hi
   t.kpn = c->kpn.p;
   t.hash_max = env_u32("NK_XHASH_MAX", 0);
   t.hash_bits = xgroup_hash_bits();
-  if (!env_u32("NK_XG_HASH", 0)) {  // the per-neuron wave sort first (k_xgroup_ws)
-    if ((rc = c->xg_ws.ensure(1 + B * t.n_groups))) return rc;
-    t.ws_list = c->xg_ws.p;
-  }
   HIPCHK(xgroup_build(t, s));
   unsigned long long cnt[2] = {0, 0};  // grouped span, side records
   HIPCHK(hipMemcpyAsync(cnt, c->x_n.p + 4, 16, hipMemcpyDeviceToHost, s));

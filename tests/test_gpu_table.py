@@ -85,8 +85,6 @@ def oracle(bases, offs, k, pool, canon):
 
 MODES = [
     pytest.param(dict(exact=True), id="fused"),
-    # the hash table for every group (no per-neuron wave sort, k_xgroup_ws)
-    pytest.param(dict(exact=True, NK_XG_HASH=1), id="hash"),
     pytest.param(dict(exact=False), id="standalone"),
     pytest.param(dict(exact=True, NK_EXACT_SORT=1), id="sorted"),
     pytest.param(dict(exact=True, NK_XHASH_MAX=40), id="side"),
@@ -133,8 +131,8 @@ def test_overflowed_regions_spill_to_the_side(exact, k):
 @pytest.mark.parametrize("run_t", [5_000, 90])
 def test_all_t_key_k32(mode, run_t):
     """k = 32 non-canonical: the all-T window is the key ~0 (the LDS table's
-    empty marker), counted beside the table; a short T run leaves its neuron
-    under 128 records, so the wave sort (k_xgroup_ws) takes it, ~0 sorting last."""
+    empty marker), counted beside the table; a long T run (one hot neuron) and
+    a short one (~70 records of ~0 among its neuron's others)."""
     rnd, _ = synth.make_records(50_000, 1, seed=9)
     bases = np.concatenate([rnd[:20_000], np.full(run_t, ord("T"), np.uint8), rnd[20_000:],
                             np.full(40, ord("t"), np.uint8)])
