@@ -302,7 +302,10 @@ hipError_t batch_count(nk_counter *c, const CountPlan &cp, const KmerInput &in, 
 // fusable count on the same stream, from the same host thread and of another
 // handle, takes it (its own K1b then waits in the slot in turn).  The owner's
 // readers (hist_ready) wait for the fused kernel's end (hist_ev), or run the
-// K1b themselves when nothing took it.
+// K1b themselves when nothing took it.  hist_state (under g_hist_mu): 0 none,
+// 1 in the slot, 2 enqueued (hist_ev recorded after it), 3 being taken (the
+// taking thread is between hist_take and hist_taken: a reader on another
+// thread waits for 2).
 // ---------------------------------------------------------------------------
 namespace {
 struct HistSlot {
@@ -355,7 +358,7 @@ nk_counter *hist_take(nk_counter *c, hipStream_t s, uint64_t n_tiles, HistJob &h
   hj.pool = a->pool;
   hj.n_items = pa.n_buckets * a->hist_slices * kFusePasses;
   hj.n_host = fuse_hosts(n_tiles);
-  a->hist_state = 2;
+  a->hist_state = 3;
   return a;
 }
 
@@ -366,10 +369,10 @@ bool hist_leave(nk_counter *c, hipStream_t s) {
   if (h.owner && h.owner != c) {
     if (h.tid != std::this_thread::get_id()) return false;
     // an older pending K1b of this thread that no count took (another
-    // stream): it runs now, on its own stream
+    // stream): it runs now, on its own stream; its readers wait for hist_ev
     nk_counter *a = h.owner;
-    if (hist_run(a, h.s) != hipSuccess) return false;
-    a->hist_state = 0;
+    if (hist_run(a, h.s) != hipSuccess || hipEventRecord(a->hist_ev, h.s) != hipSuccess) return false;
+    a->hist_state = 2;
   }
   h.owner = c;
   h.s = s;
@@ -378,43 +381,51 @@ bool hist_leave(nk_counter *c, hipStream_t s) {
   return true;
 }
 
-void hist_unslot(nk_counter *c) {
+// the taking count's fused kernel and hist_ev are enqueued
+void hist_taken(nk_counter *a) {
   std::lock_guard<std::mutex> g(g_hist_mu);
-  HistSlot &h = slot_of(c->device);
-  if (h.owner == c) h.owner = nullptr;
+  a->hist_state = 2;
+}
+
+// c's pending K1b for a reader: 0 none, 1 still in the slot (now out of it),
+// 2 enqueued (wait for hist_ev).  keep2: leave state 2 set (the histogram's
+// kernel may still be writing c's partials).
+int hist_claim(nk_counter *c, bool keep2) {
+  for (;;) {
+    {
+      std::lock_guard<std::mutex> g(g_hist_mu);
+      const int st = c->hist_state;
+      if (st != 3) {
+        if (st == 1) {
+          HistSlot &h = slot_of(c->device);
+          if (h.owner == c) h.owner = nullptr;
+        }
+        if (!(keep2 && st == 2)) c->hist_state = 0;
+        return st;
+      }
+    }
+    std::this_thread::yield();  // another thread is launching the kernel that took it
+  }
 }
 }  // namespace
 
 int hist_ready(nk_counter *c, hipStream_t s) {
-  if (c->hist_state == 1) {
-    hist_unslot(c);
-    c->hist_state = 0;
-    HIPCHK(hist_run(c, s));
-  } else if (c->hist_state == 2) {
-    c->hist_state = 0;
-    HIPCHK(hipStreamWaitEvent(s, c->hist_ev, 0));
-  }
+  const int st = hist_claim(c, false);
+  if (st == 1) HIPCHK(hist_run(c, s));
+  else if (st == 2) HIPCHK(hipStreamWaitEvent(s, c->hist_ev, 0));
   return NK_OK;
 }
 
 int hist_arena(nk_counter *c, hipStream_t s) {
-  if (c->hist_state == 1) hist_unslot(c);
-  else if (c->hist_state == 2) HIPCHK(hipStreamWaitEvent(s, c->hist_ev, 0));
-  c->hist_state = 0;
+  // (state 1: the pending histogram is dropped, the arena is about to be rewritten)
+  if (hist_claim(c, false) == 2) HIPCHK(hipStreamWaitEvent(s, c->hist_ev, 0));
   return NK_OK;
 }
 
-void hist_void(nk_counter *c) {
-  if (c->hist_state == 1) {
-    hist_unslot(c);
-    c->hist_state = 0;
-  }
-}
+void hist_void(nk_counter *c) { (void)hist_claim(c, true); }
 
 void hist_forget(nk_counter *c) {
-  hist_unslot(c);
-  if (c->hist_state == 2) (void)hipEventSynchronize(c->hist_ev);
-  c->hist_state = 0;
+  if (hist_claim(c, false) == 2) (void)hipEventSynchronize(c->hist_ev);
 }
 
 // a positive integer from the environment (tests: force the rare branches)
@@ -593,8 +604,15 @@ int accumulate(nk_counter *c, const uint8_t *d_bases, const uint64_t *d_offs,
     HistJob hj{};
     nk_counter *taken = fusable ? hist_take(c, s, in.n_tiles, hj) : nullptr;
     if (taken) {
-      HIPCHK(launch_part_fused(in, (int)c->k, c->canonical, c->pool, cp.pa, hj, s));
-      HIPCHK(hipEventRecord(taken->hist_ev, s));
+      hipError_t e = launch_part_fused(in, (int)c->k, c->canonical, c->pool, cp.pa, hj, s);
+      if (e != hipSuccess) {  // the taken histogram standalone, then this count's K1a
+        (void)hipGetLastError();
+        if (hist_run(taken, s) == hipSuccess) e = launch_part(in, (int)c->k, c->canonical, c->pool, cp.pa, s);
+      }
+      const hipError_t r = hipEventRecord(taken->hist_ev, s);
+      hist_taken(taken);
+      HIPCHK(e);
+      HIPCHK(r);
     } else {
       HIPCHK(launch_part(in, (int)c->k, c->canonical, c->pool, cp.pa, s));
     }

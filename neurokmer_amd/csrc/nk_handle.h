@@ -191,8 +191,9 @@ struct nk_counter {
   size_t ovf_zeroed = 0;  // entries known zero
   uint32_t pend_slices = 0;  // K1b partials not yet folded into cur (fused into LIF)
   // K1b left to the next count's K1a (opts.defer_hist, k_part_fused): 0 none;
-  // 1 pending in the device's slot (nk_count.cpp: hist_*); 2 taken by another
-  // handle's fused count, whose end hist_ev marks
+  // 1 pending in the device's slot (nk_count.cpp: hist_*); 2 enqueued (taken
+  // by another handle's fused count, or run standalone), its end marked by
+  // hist_ev; 3 being taken.  Read and written under nk_count.cpp's slot lock.
   int hist_state = 0;
   uint32_t hist_slices = 0;
   hipEvent_t hist_ev = nullptr;

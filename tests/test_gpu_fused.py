@@ -147,3 +147,43 @@ def test_deferred_histogram_owner_freed_or_reset():
     _check(c, x0, "c")
     b.close()
     c.close()
+
+
+def test_deferred_histogram_counted_on_one_thread_read_on_another():
+    """Counts enqueued by a worker thread (each one's K1b taken by the next, the
+    last left in the slot under that thread), then read from the main thread --
+    one handle used by one thread at a time, as the header states -- while the
+    main thread's own deferred counts on other handles never take the worker's
+    pending histogram (a slot is taken only from the thread that left it)."""
+    import threading
+    pool = 2_000_000
+    inputs = _inputs(pool, 3)
+    ctrs = [SpikingKmerCounter(K, 1.0, 0.95, 2, 1.0, pool, True, defer_hist=True) for _ in range(3)]
+    st = torch.cuda.Stream()
+    err = []
+
+    def worker():
+        try:
+            for i, c in enumerate(ctrs):
+                b, o, d_b, d_o = inputs[i][:4]
+                c.accumulate_device(d_b.data_ptr(), d_o.data_ptr(), o.size - 1, b.size, st.cuda_stream)
+        except Exception as e:  # pragma: no cover - reported below
+            err.append(e)
+
+    t = threading.Thread(target=worker)
+    t.start()
+    t.join()
+    assert not err, err
+    # the main thread counts on two other handles on the same stream first
+    other = [SpikingKmerCounter(K, 1.0, 0.95, 2, 1.0, pool, True, defer_hist=True) for _ in range(2)]
+    for j, c in enumerate(other):
+        b, o, d_b, d_o = inputs[2 - j][:4]
+        c.accumulate_device(d_b.data_ptr(), d_o.data_ptr(), o.size - 1, b.size, st.cuda_stream)
+    for i, c in enumerate(ctrs):
+        c.finalize(False, st.cuda_stream)
+        _check(c, inputs[i], i)
+    for j, c in enumerate(other):
+        c.finalize(False, st.cuda_stream)
+        _check(c, inputs[2 - j], f"other{j}")
+    for c in ctrs + other:
+        c.close()
