@@ -438,8 +438,10 @@ int nk_diag_hash_ms(int device, uint64_t n_keys, uint64_t pool, int reps, float 
  * config-5 count kernel's hash), or 64.  (No reference counterpart.) */
 int nk_diag_hash_ms_w(int device, uint64_t n_keys, uint64_t pool, int width, int reps, float *ms);
 /* Diagnostic: the best of `reps` device times (ms) of a kernel that recomputes
- * the key of every record the handle's last count kept (the partitioned count,
- * k <= 32, one batch, no exact table) from its position in the input -- the
+ * the key of every record the handle's last count kept (the one-level
+ * partitioned count: k <= 32, pool <= 4.2 M -- larger pools count through the
+ * wide two-level path, which keeps no such records -- one batch, no exact
+ * table; otherwise NK_E_INVALID) from its position in the input -- the
  * tile from the segment descriptors, the k bases from the resident input --
  * and XOR-folds the keys into *checksum (may be NULL): what an exact-table pass
  * that reads positions instead of K1a-written keys would pay for its keys.
