@@ -77,7 +77,8 @@ typedef struct nk_opts {
                             NK_KMER_COMPAT keys. */
   uint32_t defer_hist;   /* 1: batches in flight on one stream (several handles
                             counting one after the other, each finish on another
-                            stream): a partitioned count (k <= 32, pool <= 8.4 M)
+                            stream): a one-level partitioned count (k <= 32,
+                            pool <= 4.2 M canonical, <= 8.4 M otherwise)
                             leaves its bucket histogram (K1b) pending and the
                             next such count on the same stream and host thread
                             -- of another handle -- runs it inside its own hash
@@ -86,7 +87,10 @@ typedef struct nk_opts {
                             same; whatever reads this handle's counts first
                             waits for that kernel (or runs the histogram itself
                             when no count took it).  Default 0: each count
-                            histograms its own records. */
+                            histograms its own records.  (Measured slower on
+                            the bench's three batches in flight: the other
+                            batches' finish kernels wait for the longer
+                            fused kernel) */
   uint32_t reserved[10];
 } nk_opts;
 
