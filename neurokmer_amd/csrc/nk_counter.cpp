@@ -53,9 +53,10 @@ uint64_t cost_fixed(double cost) {  // Rust `(cost * 1000.0) as u64`
 // queue), which a marker recorded then would wait for as well.
 hipStream_t pick_stream(nk_counter *c, void *s) {
   hipStream_t t = s ? (hipStream_t)s : c->own_stream;
-  if (c->last_s && c->last_s != t && c->order_ev &&
+  if (c->last_s && c->last_s != t && !c->quiescent && c->order_ev &&
       (c->order_eager || hipEventRecord(c->order_ev, c->last_s) == hipSuccess))
     (void)hipStreamWaitEvent(t, c->order_ev, 0);
+  c->quiescent = false;
   c->order_eager = false;
   c->last_s = t;
   return t;
@@ -282,6 +283,8 @@ nk_counter *nk_new(size_t k, float threshold, float leak, uint32_t refractory, d
   c->opts = o;
   c->w128 = o.kmer_width == NK_KMER_128;
   c->device = o.device;
+  // (the ordering events keep the system-scope fence: without it the step
+  // measured 0.512-0.534 against 0.497-0.508 ms, profiles/r06_ab/order_fence)
   bool ok = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) == hipSuccess &&
             hipEventCreateWithFlags(&c->order_ev, hipEventDisableTiming) == hipSuccess &&
             hipEventCreateWithFlags(&c->hist_ev, hipEventDisableTiming) == hipSuccess;

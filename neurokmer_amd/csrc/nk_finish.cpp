@@ -463,6 +463,10 @@ int nk_finalize(nk_counter *c, int streaming, void *stream) {
   c->top_valid = true;
   // an accumulate on this handle precedes: report its stages too
   collect_timings(c, c->have_input);
+  // the readback was seen and every correction synchronised: nothing of this
+  // handle is pending (a stage marker after k_gather touches no buffer), so
+  // the next call on another stream starts without a cross-stream wait
+  c->quiescent = true;
   return NK_OK;
 }
 

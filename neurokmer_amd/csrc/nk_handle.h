@@ -318,6 +318,10 @@ struct nk_counter {
   hipStream_t last_s = nullptr;  // stream of the previous enqueue (pick_stream)
   hipEvent_t order_ev = nullptr;
   bool order_eager = false;  // order_ev marks the end of the last call (record_order)
+  // every operation enqueued so far is known complete (nk_finalize saw its
+  // readback, which the finish's last kernel writes after its last access):
+  // the next stream switch needs no wait (pick_stream)
+  bool quiescent = false;
   int timing_pending = 0;  // 0: stage_ms is current; 1/2: collect (without/with count) on demand
   // ev[1]/ev[2] (around the count kernel) rotate through a ring, one pair per
   // accumulate call, so every call's K1 time stays readable (nk_count_history)
