@@ -289,18 +289,43 @@ int ingest_file(nk_counter *c, const char *path, bool *fallback) {
   PinnedBuf *hb = c->ing_hb;
   for (int i = 0; i < 3; ++i)
     if ((rc = hb[i].ensure(chunk))) return rc;
-  size_t have = src.read(hb[0].p, chunk);
-  bool eof = have < chunk;
-  if (src.failed()) return fail(NK_E_IO, "%s: %s", path, src.why().c_str());
-  if (!have) return fail(NK_E_PARSE, "empty file");
-  const bool fastq = hb[0].p[0] == '@';
-  if (hb[0].p[0] != '>' && !fastq)
-    return fail(NK_E_PARSE, "unknown format: first byte is neither '>' nor '@'");
+  // a chunk is read in pieces (the reader thread) and each piece goes up as
+  // soon as it is in (upload_pieces), so a chunk's H2D overlaps its own read:
+  // a 117 MB FASTA took 5.3 ms with whole-chunk uploads, the read and the
+  // copy of each 64 MiB chunk one after the other
+  const size_t piece = std::min<size_t>(chunk, (size_t)16 << 20);
+  std::atomic<size_t> ready[3];
   std::future<size_t> next;
   auto prefetch = [&](int b) {
-    next = std::async(std::launch::async, [&src, hb, b, chunk] { return src.read(hb[b].p, chunk); });
+    ready[b].store(0, std::memory_order_relaxed);
+    std::atomic<size_t> *rp = &ready[b];
+    next = std::async(std::launch::async, [&src, hb, b, chunk, piece, rp] {
+      size_t got = 0;
+      while (got < chunk) {
+        const size_t want = std::min(piece, chunk - got);
+        const size_t n = src.read(hb[b].p + got, want);
+        got += n;
+        rp->store(got, std::memory_order_release);
+        if (n < want) break;  // the end of the input (or a failed read: src.failed())
+      }
+      return got;
+    });
   };
-  if (!eof) prefetch(1);
+  prefetch(0);
+  // the format from the first bytes in
+  while (!ready[0].load(std::memory_order_acquire) &&
+         next.wait_for(std::chrono::microseconds(20)) != std::future_status::ready) {
+  }
+  if (!ready[0].load(std::memory_order_acquire)) {
+    (void)next.get();
+    if (src.failed()) return fail(NK_E_IO, "%s: %s", path, src.why().c_str());
+    return fail(NK_E_PARSE, "empty file");
+  }
+  const bool fastq = hb[0].p[0] == '@';
+  if (hb[0].p[0] != '>' && !fastq) {
+    (void)next.get();
+    return fail(NK_E_PARSE, "unknown format: first byte is neither '>' nor '@'");
+  }
   // resident input: the file size bounds the bases of a plain file
   const uint64_t fsize = src.file_size();
   uint64_t cap_bases = (src.gz() ? 4 * fsize : fsize) + 64;
@@ -329,15 +354,31 @@ int ingest_file(nk_counter *c, const char *path, bool *fallback) {
     }
   } drain{cs, &next};
   bool used[2] = {false, false};
-  // chunk bytes -> draws[b] + room on the copy stream, once the carry out of
-  // that buffer and its parse are done
-  auto upload = [&](int b, const uint8_t *h, size_t n) -> int {
+  // the chunk the reader fills into host buffer hb -> draws[b] + room on the
+  // copy stream, piece by piece as the reader has them (once the carry out of
+  // that buffer and its parse are done); *n = its bytes
+  auto upload_pieces = [&](int b, int hbi, size_t *n) -> int {
     if (used[b]) HIPCHK(hipStreamWaitEvent(cs, ev_free[b], 0));
-    HIPCHK(hipMemcpyAsync(draws[b]->p + room, h, n, hipMemcpyHostToDevice, cs));
+    size_t up = 0;
+    for (;;) {
+      const bool done = next.wait_for(std::chrono::seconds(0)) == std::future_status::ready;
+      const size_t r = ready[hbi].load(std::memory_order_acquire);  // (final once done)
+      if (r > up) {
+        HIPCHK(hipMemcpyAsync(draws[b]->p + room + up, hb[hbi].p + up, r - up, hipMemcpyHostToDevice, cs));
+        up = r;
+      }
+      if (done) break;
+      (void)next.wait_for(std::chrono::microseconds(20));
+    }
+    *n = next.get();
     HIPCHK(hipEventRecord(ev_copied[b], cs));
     return NK_OK;
   };
-  if ((rc = upload(0, hb[0].p, have))) return rc;
+  size_t have = 0;
+  if ((rc = upload_pieces(0, 0, &have))) return rc;
+  if (src.failed()) return fail(NK_E_IO, "%s: %s", path, src.why().c_str());
+  bool eof = have < chunk;
+  if (!eof) prefetch(1);
   int db = 0;        // the device buffer of this chunk
   uint64_t ci = 0;   // this chunk's number (host buffer ci % 3)
   size_t carry = 0;  // bytes of the previous chunk in front of this one
@@ -374,10 +415,9 @@ int ingest_file(nk_counter *c, const char *path, bool *fallback) {
     size_t got = 0;
     if (!eof) {
       const clk::time_point t2 = clk::now();
-      got = next.get();
+      if ((rc = upload_pieces(db ^ 1, (int)((ci + 1) % 3), &got))) return rc;
       if (prof) t_read += since(t2);
       if (src.failed()) return fail(NK_E_IO, "%s: %s", path, src.why().c_str());
-      if ((rc = upload(db ^ 1, hb[(ci + 1) % 3].p, got))) return rc;
       if (got == chunk) prefetch((int)((ci + 2) % 3));  // chunk ci - 1's buffer: its H2D is done
     }
     const clk::time_point t0 = clk::now();

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "neurokmer.h"
+#include "nk_fqhost.h"
 
 namespace nk {
 
@@ -63,19 +64,19 @@ size_t ChunkSource::read(uint8_t *dst, size_t want) {
     }
     return got;
   }
-  // plain file: split the read over threads (page-cache copies run at the
-  // memory bandwidth of several cores, one core copies ~5-10 GB/s)
-  // up to 16 threads (a one-GPU box's CPU share; 8 read a 10 GB FASTQ from
-  // the page cache at ~24 GB/s, the limiter of config 3, profiles/r04_s2)
-  const size_t part = (size_t)4 << 20;
-  static const int kMaxThreads = [] {
-    const unsigned hc = std::thread::hardware_concurrency();
-    return (int)std::max<unsigned>(1, std::min<unsigned>(16, hc ? hc : 8));
-  }();
-  const int nt = (int)std::min<size_t>((size_t)kMaxThreads, (want + part - 1) / part);
-  std::vector<size_t> got(nt > 0 ? nt : 1, 0);
+  // plain file: split the read over the process's host pool (page-cache
+  // copies run at the memory bandwidth of several cores, one core copies ~5-10
+  // GB/s; up to 16 threads, a one-GPU box's CPU share: 8 read a 10 GB FASTQ
+  // from the page cache at ~24 GB/s, profiles/r04_s2).  Parts of >= 1 MiB, so
+  // a 16 MiB piece of a chunk (nk_ingest_host.cpp) still takes 16 threads;
+  // the pool's threads persist (a thread per part and call cost ~15 us each).
+  HostPool &pool = shared_host_pool();
+  const size_t part = (size_t)1 << 20;
+  const int nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)pool.size(), (want + part - 1) / part));
+  std::vector<size_t> got(nt, 0);
   std::atomic<int> err_no{0};
   auto work = [&](int t) {
+    if (t >= nt) return;
     const size_t lo = want * t / nt, hi = want * (t + 1) / nt;
     size_t g = 0;
     while (lo + g < hi) {
@@ -87,14 +88,8 @@ size_t ChunkSource::read(uint8_t *dst, size_t want) {
     }
     got[t] = g;
   };
-  if (nt <= 1) {
-    work(0);
-  } else {
-    std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
-    work(0);
-    for (auto &x : th) x.join();
-  }
+  if (nt <= 1) work(0);
+  else pool.run(work);
   size_t total = 0;  // contiguous from the start: a short part ends the file
   for (int t = 0; t < nt; ++t) {
     total += got[t];

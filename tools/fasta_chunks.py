@@ -1,6 +1,7 @@
 """The FASTA file path (nk_process_file_parallel: device FASTA parse, the
 bench's end_to_end.fasta_file) at several ingest chunk sizes (NK_INGEST_CHUNK,
-read per call): median of 5 calls each, results checked equal.
+read per call): median of 5 calls each from the reset state, results checked
+equal.  NK_AB_LIB selects another build for an A/B.
 Usage: python tools/fasta_chunks.py [MiB ...]"""
 import os
 import statistics
@@ -21,9 +22,11 @@ try:
     for rnd in range(2):
         for mib in sizes:
             os.environ["NK_INGEST_CHUNK"] = str(mib << 20)
+            g.reset()
             g.process_file_parallel(path)  # warm (buffers sized for this chunk)
             ts = []
             for _ in range(5):
+                g.reset()  # (each call from the reset state: results comparable)
                 t = time.perf_counter()
                 g.process_file_parallel(path)
                 ts.append(time.perf_counter() - t)
