@@ -1,11 +1,16 @@
 // nk_ingest.hip — GPU FASTA/FASTQ parse of one raw chunk (nk_ingest.h).
 //
-// FASTA (5 launches, 3 passes over the chunk): A per 4-KiB block: the last
-// line start and the header lines that start in it; B one block: exclusive
-// max-scan of the line starts and sum-scan of the headers; C per block: the
-// base bytes (now that every byte's line kind is known); D one block: scan of
-// the base counts, the new totals and the carried line state; E per block:
-// scatter of the bases and of the record offsets.
+// FASTA (5 launches, 3 passes over the chunk, each thread one aligned 16-B
+// group as the FASTQ passes read them): A per 4-KiB block: the last line
+// start and the header lines that start in it; B one block: exclusive
+// max-scan of the line starts and sum-scan of the headers (their totals kept
+// for D); C per block: the base bytes (now that every byte's line kind is
+// known); D one block: scan of the base counts, the new totals and the carried
+// line state; E per block: the bases compacted in LDS and stored as one run,
+// the record offsets.  (Round 6: byte loads, byte stores scattered by thread
+// and D walking the chunk's last block on one thread took ~0.95 ms per 64 MB
+// -- D alone 0.49 ms --, the limiter of a FASTA file's path,
+// profiles/r06_ab/fasta_overlap/kernel_stats_piecewise.csv.)
 //
 // FASTQ (the chunk starts at a record boundary, at any address: A and C read
 // aligned 16-B groups and mask the bytes outside the chunk): A newline counts;
@@ -33,11 +38,9 @@ struct FaScratch {
   unsigned long long *hdr;    // [NB] header lines starting in the block
   unsigned long long *keep;   // [NB] base bytes in the block
   unsigned long long base_out, rec_base;  // resident positions of this chunk
+  long long ls_all;           // the chunk's last line start (-1: none)
+  unsigned long long hdr_all; // header lines starting in the chunk
 };
-
-__device__ __forceinline__ bool is_ls(const uint8_t *R, uint64_t i, uint32_t at_line_start) {
-  return i == 0 ? at_line_start != 0 : R[i - 1] == '\n';
-}
 
 // exclusive block scans over up to 1024 threads
 template <typename T, typename Op>
@@ -71,23 +74,72 @@ struct OpMax {
   __device__ long long operator()(long long a, long long b) const { return a > b ? a : b; }
 };
 
+// The newline passes read the chunk as 16-B groups aligned in memory (the
+// chunk may start anywhere: a FASTQ carry is copied in front of the new data
+// on the device): group g covers bytes [16 g - head, 16 g - head + 16) of the
+// chunk, head = its start's offset in its 16-B line; bytes outside [0, L) are
+// masked.  The buffer holds >= 16 readable bytes past the chunk.
+__device__ __forceinline__ void load_group(const uint8_t *R, uint64_t L, uint32_t head, uint64_t g,
+                                           uint8_t (&by)[kIPer]) {
+  const uint4 v = *reinterpret_cast<const uint4 *>(R - head + 16 * g);
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < kIPer; ++j) {
+    const long long i = (long long)(16 * g + j) - (long long)head;
+    by[j] = (i >= 0 && (uint64_t)i < L) ? (uint8_t)(w[j >> 2] >> (8 * (j & 3))) : (uint8_t)0;
+  }
+}
+
 // ---- FASTA ------------------------------------------------------------------
-__global__ __launch_bounds__(kIB) void k_fa_a(const uint8_t *__restrict__ R, uint64_t L,
+// thread = 16-B group g = blockIdx.x * kIB + threadIdx.x (bytes 16 g - head ..
+// of the chunk); prev = the byte before the group (the lane below's last one,
+// or a load for lane 0), for the line-start test of its first byte
+struct FaGroup {
+  uint8_t by[kIPer];
+  long long base;  // the chunk index of by[0]
+  uint8_t prev;
+};
+__device__ __forceinline__ void fa_load(const uint8_t *R, uint64_t L, uint32_t head, FaGroup &x) {
+  const uint64_t g = (uint64_t)blockIdx.x * kIB + threadIdx.x;
+  x.base = 16 * (long long)g - (long long)head;
+  if (x.base < (long long)L) {
+    load_group(R, L, head, g, x.by);  // (the buffer holds 16 readable bytes past the chunk)
+  } else {
+#pragma unroll
+    for (int j = 0; j < kIPer; ++j) x.by[j] = 0;
+  }
+  uint8_t p = (uint8_t)__shfl_up((int)x.by[kIPer - 1], 1, 64);  // (every lane takes part)
+  if ((threadIdx.x & 63) == 0) {
+    const long long i = x.base - 1;
+    p = (i >= 0 && i < (long long)L) ? R[i] : (uint8_t)0;
+  }
+  x.prev = p;
+}
+__device__ __forceinline__ bool fa_in(const FaGroup &x, int j, uint64_t L) {
+  const long long i = x.base + j;
+  return i >= 0 && i < (long long)L;
+}
+// byte j (inside the chunk) starts a line
+__device__ __forceinline__ bool fa_ls(const FaGroup &x, int j, uint32_t als) {
+  if (x.base + j == 0) return als != 0;
+  return (j ? x.by[j - 1] : x.prev) == '\n';
+}
+
+__global__ __launch_bounds__(kIB) void k_fa_a(const uint8_t *__restrict__ R, uint64_t L, uint32_t head,
                                               const IngestState *__restrict__ st, FaScratch f) {
   __shared__ long long s_l[kIB / 64];
   __shared__ unsigned long long s_h[kIB / 64];
-  const uint64_t b0 = (uint64_t)blockIdx.x * kIS + (uint64_t)threadIdx.x * kIPer;
   const uint32_t als = st->at_line_start;
+  FaGroup x;
+  fa_load(R, L, head, x);
   long long last = -1;
   unsigned long long h = 0;
-  for (int j = 0; j < kIPer; ++j) {
-    const uint64_t i = b0 + j;
-    if (i >= L) break;
-    if (is_ls(R, i, als)) {
-      last = (long long)i;
-      h += R[i] == '>';
+#pragma unroll
+  for (int j = 0; j < kIPer; ++j)
+    if (fa_in(x, j, L) && fa_ls(x, j, als)) {
+      last = x.base + j;
+      h += x.by[j] == '>';
     }
-  }
   long long tl;
   unsigned long long th;
   block_scan_excl<long long>(last, -1LL, OpMax(), s_l, &tl);
@@ -115,11 +167,17 @@ __device__ void scan_array_excl(T *a, uint64_t n, T ident, Op op, T *s_w, T *tot
   if (total_out) *total_out = tot;
 }
 
-__global__ __launch_bounds__(kScanT) void k_fa_b(uint64_t NB, FaScratch f) {
+__global__ __launch_bounds__(kScanT) void k_fa_b(uint64_t NB, FaScratch f, FaScratch *__restrict__ fs) {
   __shared__ long long s_l[kScanT / 64];
   __shared__ unsigned long long s_h[kScanT / 64];
-  scan_array_excl<long long>(f.ls, NB, -1LL, OpMax(), s_l, nullptr);
-  scan_array_excl<unsigned long long>(f.hdr, NB, 0ull, OpAdd(), s_h, nullptr);
+  long long tl;
+  unsigned long long th;
+  scan_array_excl<long long>(f.ls, NB, -1LL, OpMax(), s_l, &tl);
+  scan_array_excl<unsigned long long>(f.hdr, NB, 0ull, OpAdd(), s_h, &th);
+  if (threadIdx.x == 0) {
+    fs->ls_all = tl;
+    fs->hdr_all = th;
+  }
 }
 
 // header kind of the line holding byte i, given the line start at or before
@@ -128,36 +186,34 @@ __device__ __forceinline__ bool line_hdr(const uint8_t *R, long long ls, const I
   return ls >= 0 ? R[ls] == '>' : st.line_is_hdr != 0;
 }
 
-// per thread: my 16 bytes' line starts folded with the block carry; returns
-// the line start in effect before my first byte
-__device__ __forceinline__ long long thread_carry_ls(const uint8_t *R, uint64_t L, uint64_t b0,
-                                                     uint32_t als, long long blk_carry,
-                                                     long long *s_l) {
+// the line start in effect before the group's first byte: the block's carry
+// folded with the block's threads below
+__device__ __forceinline__ long long fa_carry_ls(const FaGroup &x, uint64_t L, uint32_t als,
+                                                 long long blk_carry, long long *s_l) {
   long long last = -1;
-  for (int j = 0; j < kIPer; ++j) {
-    const uint64_t i = b0 + j;
-    if (i >= L) break;
-    if (is_ls(R, i, als)) last = (long long)i;
-  }
+#pragma unroll
+  for (int j = 0; j < kIPer; ++j)
+    if (fa_in(x, j, L) && fa_ls(x, j, als)) last = x.base + j;
   long long tot;
   const long long ex = block_scan_excl<long long>(last, -1LL, OpMax(), s_l, &tot);
   return ex > blk_carry ? ex : blk_carry;
 }
 
-__global__ __launch_bounds__(kIB) void k_fa_c(const uint8_t *__restrict__ R, uint64_t L,
+__global__ __launch_bounds__(kIB) void k_fa_c(const uint8_t *__restrict__ R, uint64_t L, uint32_t head,
                                               const IngestState *__restrict__ st, FaScratch f) {
   __shared__ long long s_l[kIB / 64];
   __shared__ unsigned long long s_k[kIB / 64];
   const IngestState S = *st;
-  const uint64_t b0 = (uint64_t)blockIdx.x * kIS + (uint64_t)threadIdx.x * kIPer;
-  long long ls = thread_carry_ls(R, L, b0, S.at_line_start, f.ls[blockIdx.x], s_l);
+  FaGroup x;
+  fa_load(R, L, head, x);
+  const long long ls = fa_carry_ls(x, L, S.at_line_start, f.ls[blockIdx.x], s_l);
   unsigned long long keep = 0;
   bool hdr = line_hdr(R, ls, S);
+#pragma unroll
   for (int j = 0; j < kIPer; ++j) {
-    const uint64_t i = b0 + j;
-    if (i >= L) break;
-    if (is_ls(R, i, S.at_line_start)) hdr = R[i] == '>';
-    const uint8_t c = R[i];
+    if (!fa_in(x, j, L)) continue;
+    const uint8_t c = x.by[j];
+    if (fa_ls(x, j, S.at_line_start)) hdr = c == '>';
     keep += !hdr && c != '\n' && c != '\r';
   }
   unsigned long long tk;
@@ -176,18 +232,8 @@ __global__ __launch_bounds__(kScanT) void k_fa_d(const uint8_t *__restrict__ R, 
   __syncthreads();
   if (threadIdx.x != 0) return;
   IngestState S = *st;
-  // headers in this chunk: exclusive prefix of the last block + its own count
-  unsigned long long nh = 0;
-  {
-    const uint64_t b = NB - 1;
-    nh = fs->hdr[b];
-    for (uint64_t i = b * kIS; i < L; ++i) nh += is_ls(R, i, S.at_line_start) && R[i] == '>';
-  }
-  // the line state after the chunk: the last line start = the blocks before
-  // the last one (exclusive max-scan) or one in the last block
-  long long last_ls = fs->ls[NB - 1];
-  for (uint64_t i = (NB - 1) * kIS; i < L; ++i)
-    if (is_ls(R, i, S.at_line_start)) last_ls = (long long)i;
+  const unsigned long long nh = fs->hdr_all;  // headers in this chunk (k_fa_b's totals)
+  const long long last_ls = fs->ls_all;      // the chunk's last line start
   const bool ends_nl = L > 0 && R[L - 1] == '\n';
   uint32_t hdr_after = S.line_is_hdr;
   if (!ends_nl && L > 0) hdr_after = line_hdr(R, last_ls, S) ? 1u : 0u;
@@ -201,44 +247,49 @@ __global__ __launch_bounds__(kScanT) void k_fa_d(const uint8_t *__restrict__ R, 
   offsets[S.n_rec] = S.data_end;  // provisional end of the last record
 }
 
-__global__ __launch_bounds__(kIB) void k_fa_e(const uint8_t *__restrict__ R, uint64_t L,
+__global__ __launch_bounds__(kIB) void k_fa_e(const uint8_t *__restrict__ R, uint64_t L, uint32_t head,
                                               const IngestState *__restrict__ st_before,
                                               const FaScratch *__restrict__ fs, FaScratch f,
                                               uint8_t *__restrict__ bases,
                                               uint64_t *__restrict__ offsets) {
   __shared__ long long s_l[kIB / 64];
   __shared__ unsigned long long s_k[kIB / 64], s_h[kIB / 64];
+  __shared__ uint8_t s_out[kIS];  // the block's bases, compacted
   const IngestState S = *st_before;  // the state the chunk started from
-  const uint64_t b0 = (uint64_t)blockIdx.x * kIS + (uint64_t)threadIdx.x * kIPer;
-  long long ls = thread_carry_ls(R, L, b0, S.at_line_start, f.ls[blockIdx.x], s_l);
+  FaGroup x;
+  fa_load(R, L, head, x);
+  const long long ls = fa_carry_ls(x, L, S.at_line_start, f.ls[blockIdx.x], s_l);
   unsigned long long keep = 0, h = 0;
   bool hdr = line_hdr(R, ls, S);
+#pragma unroll
   for (int j = 0; j < kIPer; ++j) {
-    const uint64_t i = b0 + j;
-    if (i >= L) break;
-    if (is_ls(R, i, S.at_line_start)) {
-      hdr = R[i] == '>';
+    if (!fa_in(x, j, L)) continue;
+    const uint8_t c = x.by[j];
+    if (fa_ls(x, j, S.at_line_start)) {
+      hdr = c == '>';
       h += hdr;
     }
-    const uint8_t c = R[i];
     keep += !hdr && c != '\n' && c != '\r';
   }
   unsigned long long tk, th;
   unsigned long long kp = block_scan_excl<unsigned long long>(keep, 0ull, OpAdd(), s_k, &tk);
   unsigned long long hp = block_scan_excl<unsigned long long>(h, 0ull, OpAdd(), s_h, &th);
-  kp += fs->base_out + f.keep[blockIdx.x];
+  const unsigned long long blk_out = fs->base_out + f.keep[blockIdx.x];  // the block's first base
   hp += fs->rec_base + f.hdr[blockIdx.x];
   hdr = line_hdr(R, ls, S);
+#pragma unroll
   for (int j = 0; j < kIPer; ++j) {
-    const uint64_t i = b0 + j;
-    if (i >= L) break;
-    if (is_ls(R, i, S.at_line_start)) {
-      hdr = R[i] == '>';
-      if (hdr) offsets[hp++] = kp;  // a record starts: bases before it
+    if (!fa_in(x, j, L)) continue;
+    const uint8_t c = x.by[j];
+    if (fa_ls(x, j, S.at_line_start)) {
+      hdr = c == '>';
+      if (hdr) offsets[hp++] = blk_out + kp;  // a record starts: bases before it
     }
-    const uint8_t c = R[i];
-    if (!hdr && c != '\n' && c != '\r') bases[kp++] = c;
+    if (!hdr && c != '\n' && c != '\r') s_out[kp++] = c;
   }
+  __syncthreads();
+  // one run of consecutive bytes per block: consecutive lanes, consecutive bytes
+  for (uint32_t o = threadIdx.x; o < (uint32_t)tk; o += kIB) bases[blk_out + o] = s_out[o];
 }
 
 // ---- FASTQ ------------------------------------------------------------------
@@ -253,22 +304,6 @@ struct FqScratch {
   unsigned long long first_bad;  // min index of a flagged record (~0: none)
 };
 constexpr int kRecBlock = 1024;  // records per block of the D/G passes
-
-// The newline passes read the chunk as 16-B groups aligned in memory (the
-// chunk may start anywhere: a FASTQ carry is copied in front of the new data
-// on the device): group g covers bytes [16 g - head, 16 g - head + 16) of the
-// chunk, head = its start's offset in its 16-B line; bytes outside [0, L) are
-// masked.  The buffer holds >= 16 readable bytes past the chunk.
-__device__ __forceinline__ void load_group(const uint8_t *R, uint64_t L, uint32_t head, uint64_t g,
-                                           uint8_t (&by)[kIPer]) {
-  const uint4 v = *reinterpret_cast<const uint4 *>(R - head + 16 * g);
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int j = 0; j < kIPer; ++j) {
-    const long long i = (long long)(16 * g + j) - (long long)head;
-    by[j] = (i >= 0 && (uint64_t)i < L) ? (uint8_t)(w[j >> 2] >> (8 * (j & 3))) : (uint8_t)0;
-  }
-}
 
 __global__ __launch_bounds__(kIB) void k_fq_a(const uint8_t *__restrict__ R, uint64_t L,
                                               uint32_t head, FqScratch f) {
@@ -445,7 +480,8 @@ size_t ingest_scratch_bytes(size_t chunk_cap) {
 hipError_t ingest_fasta(const uint8_t *raw, size_t len, bool eof, const IngestBufs &bufs,
                         IngestState *st, hipStream_t s) {
   (void)eof;
-  const uint64_t NB = blocks_for(len ? len : 1);
+  const uint32_t head = (uint32_t)((uintptr_t)raw & 15);
+  const uint64_t NB = blocks_for(len + head ? len + head : 1);
   uint8_t *p = (uint8_t *)bufs.scratch;
   FaScratch *fs = (FaScratch *)p;
   p += 256;
@@ -462,12 +498,12 @@ hipError_t ingest_fasta(const uint8_t *raw, size_t len, bool eof, const IngestBu
   e = hipMemcpyAsync(before, st, sizeof(IngestState), hipMemcpyDeviceToDevice, s);
   if (e != hipSuccess) return e;
   if (!len) return hipSuccess;
-  hipLaunchKernelGGL(k_fa_a, dim3((unsigned)NB), dim3(kIB), 0, s, raw, (uint64_t)len, st, f);
-  hipLaunchKernelGGL(k_fa_b, dim3(1), dim3(kScanT), 0, s, NB, f);
-  hipLaunchKernelGGL(k_fa_c, dim3((unsigned)NB), dim3(kIB), 0, s, raw, (uint64_t)len, st, f);
+  hipLaunchKernelGGL(k_fa_a, dim3((unsigned)NB), dim3(kIB), 0, s, raw, (uint64_t)len, head, st, f);
+  hipLaunchKernelGGL(k_fa_b, dim3(1), dim3(kScanT), 0, s, NB, f, fs);
+  hipLaunchKernelGGL(k_fa_c, dim3((unsigned)NB), dim3(kIB), 0, s, raw, (uint64_t)len, head, st, f);
   hipLaunchKernelGGL(k_fa_d, dim3(1), dim3(kScanT), 0, s, raw, (uint64_t)len, NB, st, fs,
                      bufs.offsets);
-  hipLaunchKernelGGL(k_fa_e, dim3((unsigned)NB), dim3(kIB), 0, s, raw, (uint64_t)len, before, fs,
+  hipLaunchKernelGGL(k_fa_e, dim3((unsigned)NB), dim3(kIB), 0, s, raw, (uint64_t)len, head, before, fs,
                      f, bufs.bases, bufs.offsets);
   return hipGetLastError();
 }

@@ -713,6 +713,23 @@ def test_ingest_fasta_chunks(tmp_path, k, canon, chunk):
     assert len(recs) == 11
 
 
+@pytest.mark.parametrize("chunk", [4099, 65536])
+def test_ingest_fasta_long_header_and_inner_gt(tmp_path, chunk):
+    """A header line longer than several chunks (its line state carried from
+    chunk to chunk), '>' inside a sequence line (a base byte, not a record),
+    a header as the file's last line without a newline."""
+    bases, offs = synth.make_records(60_000, 3, seed=chunk % 89)
+    p = tmp_path / "h.fa"
+    synth.write_fasta(str(p), bases, offs, width=70)
+    data = p.read_bytes()
+    data = data.replace(b">s1\n", b">s1 " + b"x" * 10_000 + b"\n", 1)
+    lines = data.split(b"\n")
+    lines[5] = lines[5][:20] + b">" + lines[5][20:]
+    data = b"\n".join(lines) + b">tail header, no newline"
+    p.write_bytes(data)
+    _ingest_check(str(p), 21, 5003, True, False, chunk)
+
+
 @pytest.mark.parametrize("chunk", [1000, 30000, 1 << 26])
 @pytest.mark.parametrize("streaming", [True, False])
 @pytest.mark.parametrize("fastq_device", [False, True])
