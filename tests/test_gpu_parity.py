@@ -713,6 +713,35 @@ def test_ingest_fasta_chunks(tmp_path, k, canon, chunk):
     assert len(recs) == 11
 
 
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_ingest_fasta_random_layout(tmp_path, seed):
+    """Random FASTA layouts against the reader's rules (neurokmer_amd/fastx.py,
+    src/utils.rs:9-24): lines of 0..200 bytes, headers with '>' and spaces
+    inside, '>' and '\\r' inside sequence lines, CRLF on some lines, blank
+    lines, no final newline -- at chunk sizes that cut lines and headers
+    anywhere (the 16-B-group parse: each group's first byte's line start
+    comes from the lane below or a load)."""
+    rng = np.random.default_rng(seed)
+    alpha = np.frombuffer(b"ACGTNacgt>\r", np.uint8)
+    parts = []
+    for r in range(int(rng.integers(20, 60))):
+        hdr = bytes(rng.choice(np.frombuffer(b"abc >xyz_123", np.uint8), int(rng.integers(0, 90))))
+        parts.append(b">" + hdr + (b"\r\n" if rng.random() < 0.3 else b"\n"))
+        for _ in range(int(rng.integers(0, 12))):
+            line = bytes(rng.choice(alpha, int(rng.integers(0, 200)),
+                                    p=[0.235] * 4 + [0.01] * 5 + [0.005, 0.005]))
+            if line.startswith(b">"):
+                line = b"A" + line
+            parts.append(line + (b"\r\n" if rng.random() < 0.3 else b"\n"))
+    data = b"".join(parts)
+    if rng.random() < 0.5:
+        data = data.rstrip(b"\r\n")
+    p = tmp_path / "r.fa"
+    p.write_bytes(data)
+    chunk = int(rng.integers(4099, 70_000))
+    _ingest_check(str(p), 11, 997, True, False, chunk)
+
+
 @pytest.mark.parametrize("chunk", [4099, 65536])
 def test_ingest_fasta_long_header_and_inner_gt(tmp_path, chunk):
     """A header line longer than several chunks (its line state carried from
