@@ -32,7 +32,12 @@ template <typename T>
 struct Buf {
   T *p = nullptr;
   size_t n = 0;
-  bool ensure(size_t want, bool zero = false) {
+  // zero_on: zero a new allocation on that stream, ahead of the caller's work
+  // there (hipMemset runs on the null stream, which does not order against
+  // non-blocking streams: a rank's wire written on its stream was zeroed after
+  // it, now and then -- the loopback world-3 refine case lost a whole rank's
+  // counts in 3 of 40 runs, tools/loop_flake.py)
+  bool ensure(size_t want, hipStream_t zero_on = nullptr, bool zero = false) {
     if (want <= n) return true;
     if (p) (void)hipFree(p);
     p = nullptr;
@@ -41,7 +46,7 @@ struct Buf {
       p = nullptr;
       return false;
     }
-    if (zero && hipMemset(p, 0, want * sizeof(T)) != hipSuccess) return false;
+    if (zero && hipMemsetAsync(p, 0, want * sizeof(T), zero_on) != hipSuccess) return false;
     n = want;
     return true;
   }
@@ -348,13 +353,13 @@ static int finalize_sliced_dist_impl(nk_counter *c, nk_comm *m, int streaming,
   }
   const void *slice = nullptr;
   if (small) {
-    OOM(b.wire32.ensure(std::max<uint64_t>(W * S, 1), true) && b.part32.ensure(std::max<uint64_t>(S, 1)),
+    OOM(b.wire32.ensure(std::max<uint64_t>(W * S, 1), s, true) && b.part32.ensure(std::max<uint64_t>(S, 1)),
         "slice wire");
     RC(nk_wire32(c, b.wire32.p, stream));
     if (S) RC(reduce_scatter(m, b.wire32.p, b.part32.p, S, false, s));
     slice = b.part32.p;
   } else {
-    OOM(b.wire64.ensure(std::max<uint64_t>(W * S, 1), true) && b.part64.ensure(std::max<uint64_t>(S, 1)),
+    OOM(b.wire64.ensure(std::max<uint64_t>(W * S, 1), s, true) && b.part64.ensure(std::max<uint64_t>(S, 1)),
         "slice wire");
     uint64_t *cur = nk::counter_currents_on(c, s);
     if (!cur && P) return NK_E_DEVICE;

@@ -690,7 +690,10 @@ uint32_t *nk_device_kmer_per_neuron(nk_counter *c) {
   if (table_ready(c, &s)) return nullptr;
   if (!c->kpn_valid) {
     (void)hipSetDevice(c->device);
-    if (c->kpn.ensure(c->pool) || hipMemset(c->kpn.p, 0, c->pool * 4) != hipSuccess) return nullptr;
+    // (on the handle's stream, waited for: the caller may use the pointer on any stream)
+    if (c->kpn.ensure(c->pool) || hipMemsetAsync(c->kpn.p, 0, c->pool * 4, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return nullptr;
     c->kpn_valid = true;
   }
   return c->kpn.p;
