@@ -515,8 +515,16 @@ static int accumulate(nko_counter *c, const uint8_t *bases, const uint64_t *offs
   }
   if (n_threads == 1) fold_worker(&args[0]);
   else {
-    for (int t = 0; t < n_threads; ++t) pthread_create(&th[t], NULL, fold_worker, &args[t]);
-    for (int t = 0; t < n_threads; ++t) pthread_join(th[t], NULL);
+    /* the workers pull records from s.next: a thread that cannot be created
+       has its (empty or partial) share run on the calling thread */
+    int *made = (int *)calloc((size_t)n_threads, sizeof(int));
+    for (int t = 0; t < n_threads; ++t)
+      made[t] = pthread_create(&th[t], NULL, fold_worker, &args[t]) == 0;
+    for (int t = 0; t < n_threads; ++t) {
+      if (made[t]) pthread_join(th[t], NULL);
+      else fold_worker(&args[t]);
+    }
+    free(made);
   }
   /* reduce: elementwise u64 sum (:145-154) */
   memset(c->currents, 0, P * sizeof(uint64_t));
