@@ -648,6 +648,20 @@ def rank_main(args, world: int, rank: int, local: int, ctx, lcomm) -> int:
         same_inflight = all(c.top_abundant_neurons(20) == ctrs[0].top_abundant_neurons(20) and
                             c.energy.total_spikes() == ctrs[0].energy.total_spikes()
                             for c in ctrs[1:])
+    # the overlapped run's K1a launches on the device clock, all handles merged:
+    # the count stream's time between one K1a's end and the next one's start
+    # (K1b, prep, the launch gaps) without a profiler in the process
+    count_gap = None
+    if args.inflight > 1 and not side:
+        st = sorted(x for j, c in enumerate(ctrs)
+                    for x in c.count_stamps(len(range(j, args.steps, args.inflight))))
+        gaps = [(b[0] - a[1]) * 1e-2 for a, b in zip(st, st[1:])]
+        per = [(b[0] - a[0]) * 1e-2 for a, b in zip(st, st[1:])]
+        if gaps:
+            count_gap = {"launches": len(st),
+                         "k1a_end_to_next_start_us_median": round(float(np.median(gaps)), 1),
+                         "k1a_start_to_start_us_median": round(float(np.median(per)), 1),
+                         "k1a_start_to_start_us_mean": round(float(np.mean(per)), 1)}
     # the same K steps one batch at a time: the step latency, and K1a's
     # duration without the other batch's finish beside it (the roofline)
     marks1 = []
@@ -802,6 +816,7 @@ def rank_main(args, world: int, rank: int, local: int, ctx, lcomm) -> int:
             "step_ms_host": [round((b - a) * 1e3, 4) for a, b in zip([t0] + marks[:-1], marks)],
             "k1a_ms_steps": [round(x, 4) for x in spans],
             "k1a_ms_steps_overlapped": [round(x, 4) for x in spans2],
+            "count_stream_device_clock": count_gap,
             "total_spikes": total_spikes,
         }
         if pr is not None:

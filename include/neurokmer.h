@@ -432,6 +432,12 @@ int nk_set_stage_timing(nk_counter *c, uint32_t level);
  * stage_timing 2.  Synchronises the handle's stream.  -> count, or < 0.
  * (No reference counterpart: measurement only.) */
 int nk_count_spans(nk_counter *c, float *ms, int cap);
+/* The same launches' raw [start, end] stamps (s_memrealtime, 10 ns ticks of the
+ * device's constant clock, one clock for every handle on the device), two words
+ * per launch, oldest first: the gap between one handle's K1a end and another's
+ * next K1a start, with nothing in the stream.  -> launches, or < 0.
+ * (No reference counterpart: measurement only.) */
+int nk_count_stamps(nk_counter *c, unsigned long long *ticks, int cap);
 /* Diagnostic: the best of `reps` device times (ms) of a kernel that computes
  * SipHash-1-3 (key 0) of n_keys u64 keys generated in registers plus the exact
  * `% pool` (nk_device.h: sip13_u64 + fastmod32, the count kernel's per-k-mer

@@ -45,7 +45,7 @@ EXPORTS = (
     "nk_willshaw_stored", "nk_assoc_new", "nk_assoc_free", "nk_assoc_pattern_size",
     "nk_assoc_store_kmers", "nk_assoc_find_similar",
     "nk_exact_owner", "nk_exact_partition", "nk_exact_adopt", "nk_device_kmer_per_neuron",
-    "nk_set_stage_timing", "nk_diag_hash_ms", "nk_diag_hash_ms_w", "nk_diag_key_gather_ms", "nk_count_spans", "nk_simulate_spikes_auto",
+    "nk_set_stage_timing", "nk_diag_hash_ms", "nk_diag_hash_ms_w", "nk_diag_key_gather_ms", "nk_count_spans", "nk_count_stamps", "nk_simulate_spikes_auto",
     "nk_comm_unique_id", "nk_comm_new", "nk_comm_free", "nk_finalize_dist", "nk_finalize_sliced_dist",
     "nk_settle", "nk_comm_forget", "nk_loop_group_new", "nk_loop_group_free", "nk_comm_new_loopback",
     "nk_last_error",
@@ -154,6 +154,7 @@ def load(share_torch: bool = True):
         "nk_last_timings": (C.c_int, [vp, P(C.c_char_p), P(C.c_float), C.c_int]),
         "nk_count_history": (C.c_int, [vp, P(C.c_float), C.c_int]),
         "nk_count_spans": (C.c_int, [vp, P(C.c_float), C.c_int]),
+        "nk_count_stamps": (C.c_int, [vp, P(C.c_ulonglong), C.c_int]),
         "nk_set_stage_timing": (C.c_int, [vp, C.c_uint32]),
         "nk_diag_hash_ms": (C.c_int, [C.c_int, u64, u64, C.c_int, P(C.c_float)]),
         "nk_diag_hash_ms_w": (C.c_int, [C.c_int, u64, u64, C.c_int, C.c_int, P(C.c_float)]),

@@ -335,6 +335,13 @@ class SpikingKmerCounter:
         m = _lib.check(self._L.nk_count_spans(self._h, buf, n))
         return [float(buf[i]) for i in range(m)]
 
+    def count_stamps(self, n: int) -> list:
+        """[(start, end)] s_memrealtime ticks (10 ns, one device clock) of the
+        same K1a launches as count_spans, oldest first."""
+        buf = (C.c_ulonglong * max(2 * n, 2))()
+        m = _lib.check(self._L.nk_count_stamps(self._h, buf, n))
+        return [(int(buf[2 * i]), int(buf[2 * i + 1])) for i in range(m)]
+
 
 def diag_hash_ms(n_keys: int, pool: int, device: int = 0, reps: int = 5, width: int = 64) -> float:
     """Best device time (ms) of SipHash-1-3 + exact % pool over n_keys keys

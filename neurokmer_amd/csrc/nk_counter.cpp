@@ -593,6 +593,22 @@ int nk_count_spans(nk_counter *c, float *ms, int cap) {
   return n;
 }
 
+int nk_count_stamps(nk_counter *c, unsigned long long *ticks, int cap) {
+  if (!c || (!ticks && cap > 0) || cap < 0) return fail(NK_E_INVALID, "null argument");
+  (void)hipSetDevice(c->device);
+  const int n = (int)std::min<uint64_t>(std::min<uint64_t>(c->span_calls, nk_counter::kCountRing), (uint64_t)cap);
+  if (!n) return 0;
+  std::vector<unsigned long long> h(2 * nk_counter::kCountRing);
+  if (c->last_s) HIPCHK(hipStreamSynchronize(c->last_s));
+  HIPCHK(hipMemcpy(h.data(), c->span.p, h.size() * 8, hipMemcpyDeviceToHost));
+  for (int i = 0; i < n; ++i) {
+    const uint64_t call = c->span_calls - (uint64_t)n + (uint64_t)i;
+    ticks[2 * i] = h[2 * (call % nk_counter::kCountRing)];
+    ticks[2 * i + 1] = h[2 * (call % nk_counter::kCountRing) + 1];
+  }
+  return n;
+}
+
 int nk_count_history(const nk_counter *c, float *ms, int cap) {
   if (!c || !ms || cap <= 0) return 0;
   (void)hipSetDevice(c->device);
