@@ -648,13 +648,27 @@ def rank_main(args, world: int, rank: int, local: int, ctx, lcomm) -> int:
         same_inflight = all(c.top_abundant_neurons(20) == ctrs[0].top_abundant_neurons(20) and
                             c.energy.total_spikes() == ctrs[0].energy.total_spikes()
                             for c in ctrs[1:])
+    # the same K steps one batch at a time: the step latency, and K1a's
+    # duration without the other batch's finish beside it (the roofline)
+    marks1 = []
+    _, dt1 = timed(args.steps, 1, marks1) if args.inflight > 1 else (t0, dt)
+
+    log(f"timed {args.steps} steps: {dt / args.steps * 1e3:.4f} ms/step")
     # the overlapped run's K1a launches on the device clock, all handles merged:
     # the count stream's time between one K1a's end and the next one's start
-    # (K1b, prep, the launch gaps) without a profiler in the process
+    # (K1b, prep, the launch gaps) without a profiler in the process.  Read
+    # after the one-at-a-time run (handle 0's overlapped launches precede its
+    # K one-at-a-time ones in its ring): read between the two runs, the device
+    # copies measured the one-at-a-time run's K1a ~15 % slower (0.47-0.49 vs
+    # 0.406 ms, sessions r06zm-r06_final7)
     count_gap = None
     if args.inflight > 1 and not side:
-        st = sorted(x for j, c in enumerate(ctrs)
-                    for x in c.count_stamps(len(range(j, args.steps, args.inflight))))
+        st = []
+        for j, c in enumerate(ctrs):
+            n_ov = len(range(j, args.steps, args.inflight))
+            extra = args.steps if j == 0 else 0
+            st += c.count_stamps(n_ov + extra)[:n_ov]
+        st.sort()
         gaps = [(b[0] - a[1]) * 1e-2 for a, b in zip(st, st[1:])]
         per = [(b[0] - a[0]) * 1e-2 for a, b in zip(st, st[1:])]
         if gaps:
@@ -662,12 +676,6 @@ def rank_main(args, world: int, rank: int, local: int, ctx, lcomm) -> int:
                          "k1a_end_to_next_start_us_median": round(float(np.median(gaps)), 1),
                          "k1a_start_to_start_us_median": round(float(np.median(per)), 1),
                          "k1a_start_to_start_us_mean": round(float(np.mean(per)), 1)}
-    # the same K steps one batch at a time: the step latency, and K1a's
-    # duration without the other batch's finish beside it (the roofline)
-    marks1 = []
-    _, dt1 = timed(args.steps, 1, marks1) if args.inflight > 1 else (t0, dt)
-
-    log(f"timed {args.steps} steps: {dt / args.steps * 1e3:.4f} ms/step")
     # K1a of every step of the one-at-a-time run (in-kernel stamps), and of
     # handle 1's steps in the overlapped run (the other batch's finish beside it)
     spans = ctr.count_spans(args.steps)
