@@ -654,28 +654,6 @@ def rank_main(args, world: int, rank: int, local: int, ctx, lcomm) -> int:
     _, dt1 = timed(args.steps, 1, marks1) if args.inflight > 1 else (t0, dt)
 
     log(f"timed {args.steps} steps: {dt / args.steps * 1e3:.4f} ms/step")
-    # the overlapped run's K1a launches on the device clock, all handles merged:
-    # the count stream's time between one K1a's end and the next one's start
-    # (K1b, prep, the launch gaps) without a profiler in the process.  Read
-    # after the one-at-a-time run (handle 0's overlapped launches precede its
-    # K one-at-a-time ones in its ring): read between the two runs, the device
-    # copies measured the one-at-a-time run's K1a ~15 % slower (0.47-0.49 vs
-    # 0.406 ms, sessions r06zm-r06_final7)
-    count_gap = None
-    if args.inflight > 1 and not side:
-        st = []
-        for j, c in enumerate(ctrs):
-            n_ov = len(range(j, args.steps, args.inflight))
-            extra = args.steps if j == 0 else 0
-            st += c.count_stamps(n_ov + extra)[:n_ov]
-        st.sort()
-        gaps = [(b[0] - a[1]) * 1e-2 for a, b in zip(st, st[1:])]
-        per = [(b[0] - a[0]) * 1e-2 for a, b in zip(st, st[1:])]
-        if gaps:
-            count_gap = {"launches": len(st),
-                         "k1a_end_to_next_start_us_median": round(float(np.median(gaps)), 1),
-                         "k1a_start_to_start_us_median": round(float(np.median(per)), 1),
-                         "k1a_start_to_start_us_mean": round(float(np.mean(per)), 1)}
     # K1a of every step of the one-at-a-time run (in-kernel stamps), and of
     # handle 1's steps in the overlapped run (the other batch's finish beside it)
     spans = ctr.count_spans(args.steps)
@@ -824,7 +802,6 @@ def rank_main(args, world: int, rank: int, local: int, ctx, lcomm) -> int:
             "step_ms_host": [round((b - a) * 1e3, 4) for a, b in zip([t0] + marks[:-1], marks)],
             "k1a_ms_steps": [round(x, 4) for x in spans],
             "k1a_ms_steps_overlapped": [round(x, 4) for x in spans2],
-            "count_stream_device_clock": count_gap,
             "total_spikes": total_spikes,
         }
         if pr is not None:

@@ -576,15 +576,22 @@ int nk_set_stage_timing(nk_counter *c, uint32_t level) {
   return NK_OK;
 }
 
+// The K1a stamp ring to the host (after the handle's stream has drained)
+static int read_span_ring(nk_counter *c, std::vector<unsigned long long> &h) {
+  h.assign(2 * nk_counter::kCountRing, 0ull);
+  if (c->last_s) HIPCHK(hipStreamSynchronize(c->last_s));
+  HIPCHK(hipMemcpy(h.data(), c->span.p, h.size() * 8, hipMemcpyDeviceToHost));
+  return NK_OK;
+}
+
 int nk_count_spans(nk_counter *c, float *ms, int cap) {
   if (!c || (!ms && cap > 0) || cap < 0) return fail(NK_E_INVALID, "null argument");
   (void)hipSetDevice(c->device);
   const uint64_t have = std::min<uint64_t>(c->span_calls, nk_counter::kCountRing);
   const int n = (int)std::min<uint64_t>(have, (uint64_t)cap);
   if (!n) return 0;
-  std::vector<unsigned long long> h(2 * nk_counter::kCountRing);
-  if (c->last_s) HIPCHK(hipStreamSynchronize(c->last_s));
-  HIPCHK(hipMemcpy(h.data(), c->span.p, h.size() * 8, hipMemcpyDeviceToHost));
+  std::vector<unsigned long long> h;
+  if (int rc = read_span_ring(c, h)) return rc;
   for (int i = 0; i < n; ++i) {
     const uint64_t call = c->span_calls - (uint64_t)n + (uint64_t)i;
     const unsigned long long *w = &h[2 * (call % nk_counter::kCountRing)];
@@ -598,9 +605,8 @@ int nk_count_stamps(nk_counter *c, unsigned long long *ticks, int cap) {
   (void)hipSetDevice(c->device);
   const int n = (int)std::min<uint64_t>(std::min<uint64_t>(c->span_calls, nk_counter::kCountRing), (uint64_t)cap);
   if (!n) return 0;
-  std::vector<unsigned long long> h(2 * nk_counter::kCountRing);
-  if (c->last_s) HIPCHK(hipStreamSynchronize(c->last_s));
-  HIPCHK(hipMemcpy(h.data(), c->span.p, h.size() * 8, hipMemcpyDeviceToHost));
+  std::vector<unsigned long long> h;
+  if (int rc = read_span_ring(c, h)) return rc;
   for (int i = 0; i < n; ++i) {
     const uint64_t call = c->span_calls - (uint64_t)n + (uint64_t)i;
     ticks[2 * i] = h[2 * (call % nk_counter::kCountRing)];
